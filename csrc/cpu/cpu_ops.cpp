@@ -1,0 +1,294 @@
+// cpu_ops.cpp — CPU reference backend: BINARY encoding + population utilities.
+// Mirrors csrc/kernels/binary.hip and csrc/kernels/util.hip operation by
+// operation (see the comments there for the semantics).
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <numeric>
+#include <stdexcept>
+#include <vector>
+
+#include "pga/cpu.hpp"
+
+namespace pga {
+namespace cpu {
+
+uint32_t encoding_run(int mode, const GenArgs& a, unsigned long long* best_parts) {
+  switch (a.encoding) {
+    case ENC_BINARY: return binary_run(mode, a, best_parts);
+    case ENC_REAL: return real_run(mode, a, best_parts);
+    default: return perm_run(mode, a, best_parts);
+  }
+}
+
+static uint32_t roulette_pick(const float* cumfit, uint32_t S, uint32_t w) {
+  float total = cumfit[S - 1];
+  if (!(total > 0.f)) return word_to_index(w, S);
+  float target = word_to_unit(w) * total;
+  uint32_t lo = 0, hi = S - 1;
+  while (lo < hi) {
+    uint32_t mid = (lo + hi) >> 1;
+    if (cumfit[mid] < target) lo = mid + 1; else hi = mid;
+  }
+  return lo;
+}
+
+void select_parents(const GenArgs& a, uint64_t child, uint32_t& pa, uint32_t& pb) {
+  const uint32_t S = (uint32_t)a.S;
+  if (a.selection == SEL_TOURNAMENT) {
+    const uint32_t k = a.tour_k;
+    uint32_t best[2];
+    for (uint32_t p = 0; p < 2; ++p) {
+      uint32_t b = word_to_index(pool_word(a.key, child, W_SEL + p * k), S);
+      float bs = a.score_cur[b];
+      for (uint32_t j = 1; j < k; ++j) {
+        uint32_t c = word_to_index(pool_word(a.key, child, W_SEL + p * k + j), S);
+        float cs = a.score_cur[c];
+        if (bs < cs) { bs = cs; b = c; }
+      }
+      best[p] = b;
+    }
+    pa = best[0];
+    pb = best[1];
+  } else if (a.selection == SEL_ROULETTE) {
+    pa = roulette_pick(a.cumfit, S, pool_word(a.key, child, W_SEL + 0));
+    pb = roulette_pick(a.cumfit, S, pool_word(a.key, child, W_SEL + 1));
+  } else {
+    pa = word_to_index(pool_word(a.key, child, W_SEL + 0), S);
+    pb = word_to_index(pool_word(a.key, child, W_SEL + 1), S);
+  }
+}
+
+static inline uint32_t popc(uint32_t x) { return (uint32_t)__builtin_popcount(x); }
+
+uint32_t binary_run(int mode, const GenArgs& a, unsigned long long* best_parts) {
+  const uint32_t GS = group_size(a.chunks);
+  const uint64_t rw = a.row_words;
+  const uint32_t* cur = (const uint32_t*)a.cur;
+  uint32_t* nxt = (uint32_t*)a.next;
+  const uint32_t L = a.L, nchunks = a.chunks;
+  const bool gen = mode == MODE_GEN, cross = mode == MODE_CROSS;
+  const bool evaluates = a.objective != OBJ_NONE && (mode == MODE_GEN || mode == MODE_INIT || mode == MODE_EVAL);
+  const bool bitflip = (gen || mode == MODE_MUTATE) && a.mutation == MUT_BIT_FLIP && a.mut_rate > 0.f;
+  const bool reset_one = (gen || mode == MODE_MUTATE) && a.mutation == MUT_RESET_ONE;
+  const uint32_t mut_base = W_SEL + sel_words(a);
+
+  uint32_t elite0 = 0;
+  if (gen && a.n_elite > 0 && a.elite_idx == nullptr) elite0 = (uint32_t)best_index(reduce_best(a.best_cur, a.n_best_cur));
+
+  unsigned long long best = 0;
+  std::vector<uint32_t> seg((size_t)GS * 4);
+  for (uint64_t child = 0; child < a.S; ++child) {
+    float score = 0.f;
+    if (gen && child < a.n_elite) {
+      const uint32_t src = a.elite_idx ? a.elite_idx[child] : elite0;
+      std::memcpy(nxt + child * rw, cur + (uint64_t)src * rw, sizeof(uint32_t) * 4 * nchunks);
+      score = a.score_cur[src];
+    } else {
+      uint32_t pa = 0, pb = 0;
+      bool xo = false;
+      uint32_t blo = 0, bhi = 0;
+      if (gen || cross) {
+        select_parents(a, child, pa, pb);
+        xo = a.crossover != XO_NONE && do_crossover(a, pool_word(a.key, child, W_XOPROB));
+        if (a.crossover == XO_ONE_POINT) {
+          blo = word_to_index(pool_word(a.key, child, W_CUT1), L);
+          bhi = L;
+        } else if (a.crossover == XO_TWO_POINT) {
+          uint32_t c1 = word_to_index(pool_word(a.key, child, W_CUT1), L);
+          uint32_t c2 = word_to_index(pool_word(a.key, child, W_CUT2), L);
+          blo = std::min(c1, c2);
+          bhi = std::max(c1, c2);
+        }
+      }
+      uint32_t mpos = 0xFFFFFFFFu, mt = mut_base;
+      if (bitflip) mpos = geom_skip(pool_word(a.key, child, mt++), a.mut_thr, L, a.mut_inv_log2_1mp);
+      if (reset_one && pool_word(a.key, child, W_MUTIND) < a.mut_ind_thresh)
+        mpos = word_to_index(pool_word(a.key, child, mt), L);
+
+      // per-lane objective accumulators
+      uint32_t acc_u[64] = {0};
+      uint32_t first0[64];
+      float acc_v[64] = {0}, acc_w[64] = {0};
+      for (uint32_t q = 0; q < GS; ++q) first0[q] = 0xFFFFFFFFu;
+
+      for (uint32_t c0 = 0; c0 < nchunks; c0 += GS) {
+        for (uint32_t q = 0; q < GS; ++q) {
+          const uint32_t c = c0 + q;
+          uint32_t* v = &seg[q * 4];
+          v[0] = v[1] = v[2] = v[3] = 0;
+          if (c >= nchunks) continue;
+          if (mode == MODE_INIT) {
+            u32x4 r = draw(a.key, ST_INIT, child, c);
+            v[0] = r.x; v[1] = r.y; v[2] = r.z; v[3] = r.w;
+          } else if (mode == MODE_EVAL || mode == MODE_MUTATE) {
+            std::memcpy(v, cur + child * rw + 4 * c, 16);
+          } else {
+            const uint32_t* A = cur + (uint64_t)pa * rw + 4 * c;
+            if (xo) {
+              const uint32_t* B = cur + (uint64_t)pb * rw + 4 * c;
+              uint32_t m[4];
+              if (a.crossover == XO_UNIFORM) {
+                u32x4 r = draw(a.key, ST_XO, child, c);
+                m[0] = r.x; m[1] = r.y; m[2] = r.z; m[3] = r.w;
+              } else {
+                for (int j = 0; j < 4; ++j) m[j] = ~range_mask32(c * 128u + 32u * j, blo, bhi);
+              }
+              for (int j = 0; j < 4; ++j) v[j] = (A[j] & m[j]) | (B[j] & ~m[j]);
+            } else {
+              std::memcpy(v, A, 16);
+            }
+          }
+          if (c == nchunks - 1) {
+            v[0] &= a.last_mask.x; v[1] &= a.last_mask.y; v[2] &= a.last_mask.z; v[3] &= a.last_mask.w;
+          }
+        }
+        if (bitflip) {
+          const uint32_t seg_end = std::min((c0 + GS) * 128u, L);
+          while (mpos < seg_end) {
+            uint32_t c = mpos >> 7, b = mpos & 127u;
+            seg[(c - c0) * 4 + (b >> 5)] ^= 1u << (b & 31u);
+            mpos += 1u + geom_skip(pool_word(a.key, child, mt++), a.mut_thr, L, a.mut_inv_log2_1mp);
+          }
+        } else if (reset_one && mpos != 0xFFFFFFFFu && (mpos >> 7) >= c0 && (mpos >> 7) < c0 + GS) {
+          uint32_t c = mpos >> 7, b = mpos & 127u;
+          seg[(c - c0) * 4 + (b >> 5)] ^= 1u << (b & 31u);
+        }
+        for (uint32_t q = 0; q < GS; ++q) {
+          const uint32_t c = c0 + q;
+          if (c >= nchunks) continue;
+          const uint32_t* v = &seg[q * 4];
+          if (mode != MODE_EVAL) std::memcpy(nxt + child * rw + 4 * c, v, 16);
+          if (!evaluates) continue;
+          if (a.objective == OBJ_ONEMAX) {
+            acc_u[q] += popc(v[0]) + popc(v[1]) + popc(v[2]) + popc(v[3]);
+          } else if (a.objective == OBJ_KNAPSACK) {
+            for (int j = 0; j < 4; ++j) {
+              uint32_t bits = v[j];
+              const uint32_t base = c * 128u + 32u * j;
+              while (bits) {
+                uint32_t b = (uint32_t)__builtin_ctz(bits);
+                bits &= bits - 1;
+                acc_v[q] += a.obj_data[base + b];
+                acc_w[q] += a.obj_data[L + base + b];
+              }
+            }
+          } else if (a.objective == OBJ_TRAP) {
+            const uint32_t k = (uint32_t)a.obj_i;
+            const uint32_t km = k >= 32 ? 0xFFFFFFFFu : ((1u << k) - 1u);
+            for (int j = 0; j < 4; ++j) {
+              const uint32_t base = c * 128u + 32u * j;
+              for (uint32_t i = 0; i < 32u; i += k) {
+                if (base + i + k > L) break;
+                uint32_t ones = popc((v[j] >> i) & km);
+                acc_u[q] += ones == k ? k : (k - 1 - ones);
+              }
+            }
+          } else if (a.objective == OBJ_LEADING_ONES) {
+            for (int j = 0; j < 4; ++j) {
+              uint32_t inv = ~v[j];
+              if (inv) {
+                uint32_t p = c * 128u + 32u * j + (uint32_t)__builtin_ctz(inv);
+                first0[q] = std::min(first0[q], p);
+                break;
+              }
+            }
+          }
+        }
+      }
+      if (evaluates) {
+        if (a.objective == OBJ_ONEMAX || a.objective == OBJ_TRAP) {
+          uint32_t s = 0;
+          for (uint32_t q = 0; q < GS; ++q) s += acc_u[q];
+          score = (float)s;
+        } else if (a.objective == OBJ_KNAPSACK) {
+          float vv = butterfly_sum(acc_v, GS), ww = butterfly_sum(acc_w, GS);
+          score = ww <= a.obj_f0 ? vv : a.obj_f0 - ww;
+        } else if (a.objective == OBJ_LEADING_ONES) {
+          uint32_t m = 0xFFFFFFFFu;
+          for (uint32_t q = 0; q < GS; ++q) m = std::min(m, first0[q]);
+          score = (float)std::min(m, L);
+        }
+      }
+    }
+    if (evaluates) {
+      a.score_next[child] = score;
+      best = std::max(best, pack_best(score, child));
+    }
+  }
+  if (evaluates && best_parts) best_parts[0] = best;
+  return 1;
+}
+
+// ------------------------------------------------------------- utilities ---
+unsigned long long reduce_best(const unsigned long long* parts, uint32_t n) {
+  unsigned long long b = 0;
+  for (uint32_t i = 0; i < n; ++i) b = std::max(b, parts[i]);
+  return b;
+}
+
+unsigned long long best_of_scores(const float* scores, uint64_t S) {
+  unsigned long long b = 0;
+  for (uint64_t i = 0; i < S; ++i) b = std::max(b, pack_best(scores[i], i));
+  return b;
+}
+
+void score_stats(const float* s, uint64_t S, float* out) {
+  float mn = INFINITY, mx = -INFINITY;
+  double sm = 0;
+  for (uint64_t i = 0; i < S; ++i) {
+    mn = std::fmin(mn, s[i]);
+    mx = std::fmax(mx, s[i]);
+    sm += s[i];
+  }
+  out[0] = mn;
+  out[1] = mx;
+  out[2] = (float)sm;
+  out[3] = (float)S;
+}
+
+void roulette_prefix(const float* s, uint64_t S, float* cumfit) {
+  float st[4];
+  score_stats(s, S, st);
+  float acc = 0.f;
+  for (uint64_t i = 0; i < S; ++i) {
+    acc += std::fmax(s[i] - st[0], 0.f);
+    cumfit[i] = acc;
+  }
+}
+
+void topk(const float* scores, uint64_t S, uint32_t k, bool largest, uint32_t* idx_out) {
+  if (k > S) throw std::runtime_error("topk: k > S");
+  std::vector<uint32_t> idx(S);
+  std::iota(idx.begin(), idx.end(), 0u);
+  auto key = [&](uint32_t i) {
+    uint32_t kk = score_key(scores[i]);
+    return largest ? kk : ~kk;
+  };
+  std::partial_sort(idx.begin(), idx.begin() + k, idx.end(), [&](uint32_t x, uint32_t y) {
+    uint32_t kx = key(x), ky = key(y);
+    return kx != ky ? kx > ky : x < y;
+  });
+  std::memcpy(idx_out, idx.data(), 4ull * k);
+}
+
+void gather_rows(const void* rows, const float* scores, uint32_t row_words, const uint32_t* idx, uint32_t n,
+                 void* out_rows, float* out_scores) {
+  for (uint32_t r = 0; r < n; ++r) {
+    std::memcpy((uint32_t*)out_rows + (uint64_t)r * row_words, (const uint32_t*)rows + (uint64_t)idx[r] * row_words,
+                4ull * row_words);
+    if (scores && out_scores) out_scores[r] = scores[idx[r]];
+  }
+}
+
+void scatter_rows(void* rows, float* scores, uint32_t row_words, const uint32_t* idx, uint32_t n,
+                  const void* in_rows, const float* in_scores) {
+  for (uint32_t r = 0; r < n; ++r) {
+    std::memcpy((uint32_t*)rows + (uint64_t)idx[r] * row_words, (const uint32_t*)in_rows + (uint64_t)r * row_words,
+                4ull * row_words);
+    if (scores && in_scores) scores[idx[r]] = in_scores[r];
+  }
+}
+
+}  // namespace cpu
+}  // namespace pga

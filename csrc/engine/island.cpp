@@ -1,0 +1,420 @@
+// island.cpp — native GA runtime (see island.hpp).
+#include "pga/island.hpp"
+
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <stdexcept>
+
+#include "pga/cpu.hpp"
+#include "pga/ops.hpp"
+
+namespace pga {
+
+void row_geometry(int32_t encoding, uint32_t L, uint32_t* row_words, uint32_t* chunks) {
+  uint32_t c = 0;
+  switch (encoding) {
+    case ENC_BINARY: c = (L + 127) / 128; break;
+    case ENC_REAL: c = (L + 3) / 4; break;
+    case ENC_PERMUTATION: c = (L + 7) / 8; break;
+    default: throw std::invalid_argument("unknown encoding");
+  }
+  if (c == 0) c = 1;
+  *chunks = c;
+  *row_words = 4 * c;
+}
+
+namespace {
+bool per_individual_mutation(int32_t m) { return m == MUT_RESET_ONE || m == MUT_SWAP || m == MUT_INVERSION; }
+uint32_t prob_thresh(float p) {
+  double v = std::floor((double)p * 4294967296.0);
+  return v >= 4294967295.0 ? 0xFFFFFFFFu : (v <= 0 ? 0u : (uint32_t)v);
+}
+}  // namespace
+
+Island::Island(const Config& cfg, int device) : cfg_(cfg), device_(device) {
+  if (cfg_.S == 0) throw std::invalid_argument("population size must be > 0");
+  if (cfg_.S >= (1ull << 32)) throw std::invalid_argument("population size must be < 2^32");
+  if (cfg_.L == 0) throw std::invalid_argument("genome length must be > 0");
+  if (cfg_.encoding == ENC_PERMUTATION && cfg_.L > 65536) throw std::invalid_argument("permutation length > 65536");
+  if (cfg_.island >= 65536) throw std::invalid_argument("island id must be < 65536");
+  row_geometry(cfg_.encoding, cfg_.L, &row_words_, &chunks_);
+  if (on_gpu()) PGA_HIP_CHECK(hipSetDevice(device_));
+  const size_t rb = 4ull * row_words_ * cfg_.S;
+  for (int i = 0; i < 2; ++i) {
+    rows_[i] = alloc(rb);
+    scores_[i] = alloc(4ull * cfg_.S);
+    best_[i] = alloc(8ull * kMaxGrid);
+  }
+  out_best_ = alloc(64);
+  stats_ = alloc(4ull * (4 + 3 * 1024));
+  if (cfg_.encoding == ENC_BINARY) {
+    const uint32_t rem = cfg_.L - 128 * (chunks_ - 1);
+    uint32_t m[4];
+    for (uint32_t j = 0; j < 4; ++j) m[j] = range_mask32(32 * j, 0, rem);
+    last_mask_ = u32x4{m[0], m[1], m[2], m[3]};
+  } else {
+    last_mask_ = u32x4{~0u, ~0u, ~0u, ~0u};
+  }
+  set_operators(cfg_);
+}
+
+Island::~Island() {
+  Buffer* all[] = {&rows_[0],   &rows_[1],     &scores_[0],   &scores_[1],  &best_[0],  &best_[1],   &mut_thr_,
+                   &obj_data_[0], &obj_data_[1], &elite_idx_, &cumfit_, &cum_ws_, &topk_ws_, &stats_,
+                   &out_best_,  &scratch_};
+  for (Buffer* b : all) {
+    try {
+      release(*b);
+    } catch (...) {
+    }
+  }
+}
+
+Buffer Island::alloc(size_t bytes) {
+  Buffer b;
+  b.bytes = bytes;
+  if (bytes == 0) return b;
+  if (on_gpu()) {
+    PGA_HIP_CHECK(hipMalloc(&b.ptr, bytes));
+  } else {
+    b.ptr = std::aligned_alloc(64, (bytes + 63) & ~(size_t)63);
+    if (!b.ptr) throw std::bad_alloc();
+    std::memset(b.ptr, 0, bytes);
+  }
+  return b;
+}
+
+void Island::release(Buffer& b) {
+  if (!b.ptr) return;
+  if (on_gpu()) PGA_HIP_CHECK(hipFree(b.ptr));
+  else std::free(b.ptr);
+  b.ptr = nullptr;
+  b.bytes = 0;
+}
+
+void* Island::scratch(size_t bytes) {
+  if (scratch_.bytes < bytes) {
+    if (on_gpu() && scratch_.ptr) synchronize();
+    release(scratch_);
+    scratch_ = alloc(bytes);
+  }
+  return scratch_.ptr;
+}
+
+void Island::copy_to_host(void* dst, const void* src, size_t bytes) {
+  if (on_gpu()) {
+    PGA_HIP_CHECK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, stream));
+    PGA_HIP_CHECK(hipStreamSynchronize(stream));
+  } else {
+    std::memcpy(dst, src, bytes);
+  }
+}
+
+void Island::copy_to_device(void* dst, const void* src, size_t bytes) {
+  if (on_gpu()) {
+    PGA_HIP_CHECK(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, stream));
+    PGA_HIP_CHECK(hipStreamSynchronize(stream));
+  } else {
+    std::memcpy(dst, src, bytes);
+  }
+}
+
+void Island::synchronize() {
+  if (on_gpu()) PGA_HIP_CHECK(hipStreamSynchronize(stream));
+}
+
+void Island::rebuild_mut_table() {
+  const bool per_ind = per_individual_mutation(cfg_.mutation);
+  mut_rate_eff_ = cfg_.mut_rate >= 0.f ? cfg_.mut_rate : (per_ind ? 0.01f : 1.f / (float)cfg_.L);
+  if (mut_rate_eff_ > 1.f) mut_rate_eff_ = 1.f;
+  std::vector<uint32_t> thr(cfg_.L);
+  build_mut_table(per_ind ? 0.f : mut_rate_eff_, cfg_.L, thr.data(), &mut_inv_);
+  if (mut_thr_.bytes < 4ull * cfg_.L) {
+    if (on_gpu()) synchronize();
+    release(mut_thr_);
+    mut_thr_ = alloc(4ull * cfg_.L);
+  }
+  copy_to_device(mut_thr_.ptr, thr.data(), 4ull * cfg_.L);
+}
+
+void Island::set_operators(const Config& c) {
+  if (c.S != cfg_.S || c.L != cfg_.L || c.encoding != cfg_.encoding)
+    throw std::invalid_argument("set_operators cannot change S, L or encoding");
+  if (c.selection == SEL_TOURNAMENT && (c.tour_k < 1 || c.tour_k > 64))
+    throw std::invalid_argument("tournament size must be in [1, 64]");
+  if (c.n_elite > c.S) throw std::invalid_argument("elitism count exceeds population");
+  const float old_rate = cfg_.mut_rate;
+  const int32_t old_mut = cfg_.mutation;
+  cfg_ = c;
+  if (!mut_thr_.ptr || old_rate != c.mut_rate || old_mut != c.mutation) rebuild_mut_table();
+  if (cfg_.n_elite > 1 && elite_idx_.bytes < 4ull * cfg_.n_elite) {
+    release(elite_idx_);
+    elite_idx_ = alloc(4ull * cfg_.n_elite);
+  }
+  if (cfg_.selection == SEL_ROULETTE && !cumfit_.ptr) {
+    cumfit_ = alloc(4ull * cfg_.S);
+    cum_ws_ = alloc(4ull * (4 + 3 * 1024 + 1024));
+  }
+}
+
+void Island::set_objective_data(const float* host, size_t n, int which) {
+  if (which < 0 || which > 1) throw std::invalid_argument("objective data slot must be 0 or 1");
+  if (on_gpu()) synchronize();
+  release(obj_data_[which]);
+  obj_data_[which] = alloc(4ull * (n ? n : 1));
+  if (n) copy_to_device(obj_data_[which].ptr, host, 4ull * n);
+  obj_len_[which] = n;
+}
+
+GenArgs Island::make_args(int mode) {
+  GenArgs a;
+  std::memset(&a, 0, sizeof(a));
+  const int nx = cur_ ^ 1;
+  a.cur = rows_[cur_].ptr;
+  a.next = rows_[nx].ptr;
+  a.score_cur = (const float*)scores_[cur_].ptr;
+  a.score_next = (float*)scores_[nx].ptr;
+  if (mode == MODE_INIT || mode == MODE_EVAL) {
+    a.next = rows_[cur_].ptr;
+    a.score_next = (float*)scores_[cur_].ptr;
+  } else if (mode == MODE_MUTATE) {
+    a.cur = rows_[nx].ptr;
+    a.next = rows_[nx].ptr;
+  }
+  a.S = cfg_.S;
+  a.L = cfg_.L;
+  a.row_words = row_words_;
+  a.chunks = chunks_;
+  a.encoding = (uint32_t)cfg_.encoding;
+  a.key.k0 = (uint32_t)cfg_.seed;
+  a.key.k1 = (uint32_t)(cfg_.seed >> 32) ^ (epoch_ * 0x9E3779B9u);
+  a.key.gen = gen_;
+  a.key.island = cfg_.island;
+  a.selection = cfg_.selection;
+  a.tour_k = cfg_.tour_k;
+  a.cumfit = (const float*)cumfit_.ptr;
+  a.crossover = cfg_.crossover;
+  a.xo_always = cfg_.xo_prob >= 1.f ? 1u : 0u;
+  a.xo_thresh_hi = prob_thresh(cfg_.xo_prob);
+  a.blend_alpha = cfg_.blend_alpha;
+  a.mutation = cfg_.mutation;
+  a.mut_rate = mut_rate_eff_;
+  a.mut_ind_thresh = per_individual_mutation(cfg_.mutation) ? prob_thresh(mut_rate_eff_) : 0u;
+  a.mut_thr = (const uint32_t*)mut_thr_.ptr;
+  a.mut_inv_log2_1mp = mut_inv_;
+  a.sigma = cfg_.sigma;
+  a.lo = cfg_.lo;
+  a.hi = cfg_.hi;
+  a.objective = cfg_.objective;
+  a.obj_i = cfg_.obj_i;
+  a.obj_f0 = cfg_.obj_f0;
+  a.obj_f1 = cfg_.obj_f1;
+  a.obj_data = (const float*)obj_data_[0].ptr;
+  a.obj_data2 = (const float*)obj_data_[1].ptr;
+  a.user_fn = user_fn_;
+  a.n_elite = cfg_.n_elite;
+  a.elite_idx = cfg_.n_elite > 1 ? (const uint32_t*)elite_idx_.ptr : nullptr;
+  a.best_cur = (const unsigned long long*)best_[cur_].ptr;
+  a.n_best_cur = n_best_[cur_];
+  a.last_mask = last_mask_;
+  return a;
+}
+
+uint32_t Island::launch(int mode, const GenArgs& a, unsigned long long* parts) {
+  if (on_gpu()) return encoding_launch(mode, a, parts, stream);
+  return cpu::encoding_run(mode, a, parts);
+}
+
+void Island::initialize() {
+  GenArgs a = make_args(MODE_INIT);
+  n_best_[cur_] = launch(MODE_INIT, a, (unsigned long long*)best_[cur_].ptr);
+  if (cfg_.objective == OBJ_NONE) rebest();
+}
+
+void Island::evaluate() {
+  GenArgs a = make_args(MODE_EVAL);
+  n_best_[cur_] = launch(MODE_EVAL, a, (unsigned long long*)best_[cur_].ptr);
+}
+
+void Island::rebest() {
+  const float* sc = (const float*)scores_[cur_].ptr;
+  if (on_gpu()) {
+    n_best_[cur_] = best_of_scores_launch(sc, cfg_.S, (unsigned long long*)best_[cur_].ptr, stream);
+  } else {
+    ((unsigned long long*)best_[cur_].ptr)[0] = cpu::best_of_scores(sc, cfg_.S);
+    n_best_[cur_] = 1;
+  }
+}
+
+void Island::prepare_generation() {
+  if (cfg_.selection == SEL_ROULETTE) {
+    const float* sc = (const float*)scores_[cur_].ptr;
+    if (on_gpu()) roulette_prefix_launch(sc, cfg_.S, (float*)cumfit_.ptr, (float*)cum_ws_.ptr, stream);
+    else cpu::roulette_prefix(sc, cfg_.S, (float*)cumfit_.ptr);
+  }
+  if (cfg_.n_elite > 1) topk(cfg_.n_elite, true, (uint32_t*)elite_idx_.ptr);
+}
+
+void Island::run(uint32_t n) {
+  for (uint32_t i = 0; i < n; ++i) {
+    prepare_generation();
+    GenArgs a = make_args(MODE_GEN);
+    n_best_[cur_ ^ 1] = launch(MODE_GEN, a, (unsigned long long*)best_[cur_ ^ 1].ptr);
+    swap();
+  }
+}
+
+void Island::crossover_stage() {
+  prepare_generation();
+  GenArgs a = make_args(MODE_CROSS);
+  launch(MODE_CROSS, a, nullptr);
+}
+
+void Island::mutate_stage() {
+  GenArgs a = make_args(MODE_MUTATE);
+  launch(MODE_MUTATE, a, nullptr);
+}
+
+void Island::swap() {
+  cur_ ^= 1;
+  ++gen_;
+}
+
+unsigned long long Island::best_packed() {
+  unsigned long long r = 0;
+  if (on_gpu()) {
+    reduce_best_launch((const unsigned long long*)best_[cur_].ptr, n_best_[cur_], (unsigned long long*)out_best_.ptr,
+                       stream);
+    copy_to_host(&r, out_best_.ptr, 8);
+  } else {
+    r = cpu::reduce_best((const unsigned long long*)best_[cur_].ptr, n_best_[cur_]);
+  }
+  return r;
+}
+
+void Island::stats(float out[4]) {
+  const float* sc = (const float*)scores_[cur_].ptr;
+  if (on_gpu()) {
+    score_stats_launch(sc, cfg_.S, (float*)stats_.ptr, stream);
+    copy_to_host(out, stats_.ptr, 16);
+  } else {
+    cpu::score_stats(sc, cfg_.S, out);
+  }
+}
+
+void Island::topk(uint32_t k, bool largest, uint32_t* idx_out) {
+  if (k > cfg_.S) throw std::invalid_argument("k exceeds population size");
+  const float* sc = (const float*)scores_[cur_].ptr;
+  if (on_gpu()) {
+    size_t need = topk_workspace_bytes(cfg_.S, k);
+    if (topk_ws_.bytes < need) {
+      synchronize();
+      release(topk_ws_);
+      topk_ws_ = alloc(need);
+    }
+    topk_launch(sc, cfg_.S, k, largest, idx_out, topk_ws_.ptr, stream);
+  } else {
+    cpu::topk(sc, cfg_.S, k, largest, idx_out);
+  }
+}
+
+std::vector<uint32_t> Island::topk_host(uint32_t k, bool largest) {
+  std::vector<uint32_t> out(k);
+  if (k == 0) return out;
+  if (on_gpu()) {
+    uint32_t* d = (uint32_t*)scratch(4ull * k);
+    topk(k, largest, d);
+    copy_to_host(out.data(), d, 4ull * k);
+  } else {
+    topk(k, largest, out.data());
+  }
+  return out;
+}
+
+std::vector<uint32_t> Island::row_host(uint64_t i) {
+  if (i >= cfg_.S) throw std::out_of_range("individual index out of range");
+  std::vector<uint32_t> out(row_words_);
+  copy_to_host(out.data(), (const uint32_t*)rows_[cur_].ptr + i * row_words_, 4ull * row_words_);
+  return out;
+}
+
+void Island::gather(const uint32_t* idx, uint32_t n, void* out_rows, float* out_scores) {
+  if (on_gpu())
+    gather_rows_launch(rows_[cur_].ptr, (const float*)scores_[cur_].ptr, row_words_, idx, n, out_rows, out_scores,
+                       stream);
+  else
+    cpu::gather_rows(rows_[cur_].ptr, (const float*)scores_[cur_].ptr, row_words_, idx, n, out_rows, out_scores);
+}
+
+void Island::scatter(const uint32_t* idx, uint32_t n, const void* in_rows, const float* in_scores) {
+  if (on_gpu())
+    scatter_rows_launch(rows_[cur_].ptr, (float*)scores_[cur_].ptr, row_words_, idx, n, in_rows, in_scores, stream);
+  else
+    cpu::scatter_rows(rows_[cur_].ptr, (float*)scores_[cur_].ptr, row_words_, idx, n, in_rows, in_scores);
+}
+
+// ------------------------------------------------------------ checkpoint ---
+namespace {
+struct CkptHeader {
+  char magic[8];  // "PGACKPT1"
+  uint32_t version, encoding, L, row_words;
+  uint64_t S;
+  uint32_t gen, epoch, island, pad;
+  uint64_t seed;
+};
+}  // namespace
+
+void Island::save(const std::string& path) {
+  CkptHeader h;
+  std::memset(&h, 0, sizeof(h));
+  std::memcpy(h.magic, "PGACKPT1", 8);
+  h.version = 1;
+  h.encoding = (uint32_t)cfg_.encoding;
+  h.L = cfg_.L;
+  h.row_words = row_words_;
+  h.S = cfg_.S;
+  h.gen = gen_;
+  h.epoch = epoch_;
+  h.island = cfg_.island;
+  h.seed = cfg_.seed;
+  std::vector<char> rows(4ull * row_words_ * cfg_.S);
+  std::vector<float> sc(cfg_.S);
+  copy_to_host(rows.data(), rows_[cur_].ptr, rows.size());
+  copy_to_host(sc.data(), scores_[cur_].ptr, 4ull * cfg_.S);
+  FILE* f = std::fopen(path.c_str(), "wb");
+  if (!f) throw std::runtime_error("cannot open checkpoint for writing: " + path);
+  bool ok = std::fwrite(&h, sizeof(h), 1, f) == 1 && std::fwrite(rows.data(), 1, rows.size(), f) == rows.size() &&
+            std::fwrite(sc.data(), 4, cfg_.S, f) == cfg_.S;
+  ok = (std::fclose(f) == 0) && ok;
+  if (!ok) throw std::runtime_error("short write to checkpoint: " + path);
+}
+
+void Island::load(const std::string& path) {
+  FILE* f = std::fopen(path.c_str(), "rb");
+  if (!f) throw std::runtime_error("cannot open checkpoint: " + path);
+  CkptHeader h;
+  if (std::fread(&h, sizeof(h), 1, f) != 1 || std::memcmp(h.magic, "PGACKPT1", 8) != 0) {
+    std::fclose(f);
+    throw std::runtime_error("not a pga checkpoint: " + path);
+  }
+  if (h.S != cfg_.S || h.L != cfg_.L || h.encoding != (uint32_t)cfg_.encoding || h.row_words != row_words_) {
+    std::fclose(f);
+    throw std::runtime_error("checkpoint geometry does not match this population");
+  }
+  std::vector<char> rows(4ull * row_words_ * cfg_.S);
+  std::vector<float> sc(cfg_.S);
+  bool ok = std::fread(rows.data(), 1, rows.size(), f) == rows.size() && std::fread(sc.data(), 4, cfg_.S, f) == cfg_.S;
+  std::fclose(f);
+  if (!ok) throw std::runtime_error("truncated checkpoint: " + path);
+  copy_to_device(rows_[cur_].ptr, rows.data(), rows.size());
+  copy_to_device(scores_[cur_].ptr, sc.data(), 4ull * cfg_.S);
+  gen_ = h.gen;
+  epoch_ = h.epoch;
+  cfg_.seed = h.seed;
+  cfg_.island = h.island;
+  rebest();
+}
+
+}  // namespace pga

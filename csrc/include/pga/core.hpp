@@ -1,0 +1,287 @@
+// core.hpp — definitions shared by the gfx950 kernels, the CPU reference backend,
+// the C API runtime and the torch bindings.
+//
+// Everything random in the engine comes from ONE counter-based generator,
+// Philox4x32-10 (bit-identical to rocrand's `philox4x32_10_engine::ten_rounds`,
+// checked by tests/test_rng.py via tools/rng_check.cpp).  A draw is addressed by
+//   key     = 64-bit seed
+//   counter = {block | stream<<24, child_lo, child_hi | island<<16, generation}
+// so a value depends only on (seed, generation, island, individual, purpose,
+// block) and never on launch geometry.  This is what lets the CPU reference
+// backend reproduce a GPU generation bit for bit (BINARY / PERMUTATION) and
+// what makes checkpoints exactly resumable (the generation counter IS the
+// RNG state).
+//
+// Reference: the reference draws one process-global cuRAND XORWOW buffer of
+// S*L floats per generation (src/pga.cu:35, :99-101) and re-uses the same slice
+// for selection, crossover and mutation (src/pga.cu:298, :306-307, :341); see
+// SURVEY.md §5.2 for why that is replaced.
+#pragma once
+
+#include <stdint.h>
+
+#if defined(__HIPCC__)
+#include <hip/hip_runtime.h>
+#define PGA_HD __host__ __device__ __forceinline__
+#define PGA_DEVICE_COMPILE 1
+#else
+#define PGA_HD inline
+#endif
+
+namespace pga {
+
+// ---------------------------------------------------------------- enums ----
+// Values are part of the C ABI (pga_ext.h mirrors them) and of the python
+// bindings; append only.
+enum Encoding : int32_t {
+  ENC_BINARY = 0,       // bit-packed, 128-bit chunks, row stride multiple of 16 B
+  ENC_REAL = 1,         // f32 genes, 4-gene chunks
+  ENC_PERMUTATION = 2,  // u16 genes, each row a permutation of 0..L-1
+};
+
+enum Selection : int32_t {
+  SEL_TOURNAMENT = 0,  // k-way tournament, with replacement, first max wins
+  SEL_ROULETTE = 1,    // fitness proportional (scores shifted by the minimum)
+  SEL_RANDOM = 2,      // uniform parent choice (no pressure) — testing/baseline
+};
+
+enum Crossover : int32_t {
+  XO_UNIFORM = 0,     // per gene/bit: parent A with p=1/2 (reference default)
+  XO_ONE_POINT = 1,   // prefix from A, suffix from B
+  XO_TWO_POINT = 2,   // [a,b) from B, rest from A
+  XO_BLEND = 3,       // REAL: BLX-alpha
+  XO_ARITHMETIC = 4,  // REAL: child = A + u*(B-A), one u per child
+  XO_PMX = 5,         // PERMUTATION: partially mapped crossover
+  XO_OX = 6,          // PERMUTATION: ordered crossover (OX1)
+  XO_NONE = 7,        // child = copy of parent A
+};
+
+enum Mutation : int32_t {
+  MUT_BIT_FLIP = 0,     // BINARY: each bit flipped independently with rate p
+  MUT_GAUSSIAN = 1,     // REAL: each gene += sigma*N(0,1) with rate p (clamped)
+  MUT_UNIFORM = 2,      // REAL: each gene reset to U(lo,hi) with rate p
+  MUT_RESET_ONE = 3,    // reference default: with prob p per individual reset ONE gene
+  MUT_SWAP = 4,         // PERMUTATION: with prob p per individual swap two positions
+  MUT_INVERSION = 5,    // PERMUTATION: with prob p per individual reverse a segment (2-opt)
+  MUT_NONE = 6,
+};
+
+enum Objective : int32_t {
+  OBJ_NONE = 0,          // no fused evaluation (scores provided externally)
+  OBJ_ONEMAX = 1,        // BINARY: popcount
+  OBJ_KNAPSACK = 2,      // BINARY: 0/1 knapsack, data = [values L | weights L], p0 = capacity
+  OBJ_TRAP = 3,          // BINARY: concatenated deceptive trap, block size param_i (2,4,8)
+  OBJ_LEADING_ONES = 4,  // BINARY: number of leading one bits
+  OBJ_SPHERE = 16,       // REAL: -sum z^2
+  OBJ_RASTRIGIN = 17,    // REAL: -(10 D + sum z^2 - 10 cos(2 pi z))
+  OBJ_ROSENBROCK = 18,   // REAL: -sum 100 (z_{i+1} - z_i^2)^2 + (1 - z_i)^2
+  OBJ_ACKLEY = 19,       // REAL: -(ackley)
+  OBJ_GRIEWANK = 20,     // REAL
+  OBJ_SCHWEFEL = 21,     // REAL: -(418.9829 D - sum z sin(sqrt|z|))
+  OBJ_LINEAR = 22,       // REAL: w . x  (the float-gene sum of reference E1 when w = 1)
+  OBJ_KNAPSACK_REAL = 23,// REAL: reference E2 semantics: count=(int)(g*max_count)
+  OBJ_TSP_RANDOM_KEY = 24,// REAL: reference E3 semantics (decode (int)(g*L), dup penalty)
+  OBJ_TSP = 32,          // PERMUTATION: -(closed tour length), data = L*L distance matrix
+  OBJ_TSP_OPEN = 33,     // PERMUTATION: -(open path length) (reference E3 metric)
+  OBJ_USER_FNPTR = 64,   // REAL: reference-ABI device function pointer obj_f
+};
+
+// Philox streams (purpose tags, high byte of counter word 0)
+enum Stream : uint32_t {
+  ST_INIT = 1,     // initial population
+  ST_XO = 2,       // crossover masks / per-gene crossover values
+  ST_CHILD = 3,    // per-child word pool (see word layout below)
+  ST_MUTX = 4,     // extra per-gene mutation values (gaussian etc.)
+  ST_MIGRATE = 5,  // migration pairing / victim choice
+  ST_COMPAT = 6,   // reference-ABI rand slices handed to user callbacks
+  ST_PERM = 7,     // permutation crossover helpers
+};
+
+// Child word-pool layout (word t = philox(ST_CHILD, block t/4)[t%4]):
+//   0      crossover-probability test
+//   1, 2   cut points / blend parameter
+//   3      per-individual mutation test (RESET_ONE / SWAP / INVERSION)
+//   4..    selection words (2k for tournament-k, 2 otherwise)
+//   then   mutation draws, consumed sequentially
+constexpr uint32_t W_XOPROB = 0, W_CUT1 = 1, W_CUT2 = 2, W_MUTIND = 3, W_SEL = 4;
+
+// ---------------------------------------------------------------- Philox ---
+struct u32x4 {
+  uint32_t x, y, z, w;
+};
+
+PGA_HD void mulhilo32(uint32_t a, uint32_t b, uint32_t& hi, uint32_t& lo) {
+  uint64_t p = (uint64_t)a * (uint64_t)b;
+  hi = (uint32_t)(p >> 32);
+  lo = (uint32_t)p;
+}
+
+PGA_HD u32x4 philox4x32_10(u32x4 c, uint32_t k0, uint32_t k1) {
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    uint32_t hi0, lo0, hi1, lo1;
+    mulhilo32(0xD2511F53u, c.x, hi0, lo0);
+    mulhilo32(0xCD9E8D57u, c.z, hi1, lo1);
+    c = u32x4{hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0};
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+  return c;
+}
+
+struct RngKey {
+  uint32_t k0, k1;     // seed
+  uint32_t gen;        // generation counter
+  uint32_t island;     // island id (< 65536)
+};
+
+PGA_HD u32x4 draw(const RngKey& key, uint32_t stream, uint64_t ind, uint32_t block) {
+  u32x4 c{(block & 0x00FFFFFFu) | (stream << 24), (uint32_t)ind,
+          (uint32_t)(ind >> 32) | (key.island << 16), key.gen};
+  return philox4x32_10(c, key.k0, key.k1);
+}
+
+PGA_HD uint32_t sel4(const u32x4& v, uint32_t i) {
+  return i == 0 ? v.x : (i == 1 ? v.y : (i == 2 ? v.z : v.w));
+}
+
+// uniform index in [0, n) from a 32-bit word (n < 2^32)
+PGA_HD uint32_t word_to_index(uint32_t w, uint32_t n) {
+  return (uint32_t)(((uint64_t)w * (uint64_t)n) >> 32);
+}
+
+// uniform float in (0, 1], exactly representable, identical on host and device
+PGA_HD float word_to_unit(uint32_t w) {
+  return (float)((w >> 8) + 1u) * (1.0f / 16777216.0f);
+}
+
+// ------------------------------------------------------- geometric skips ---
+// Bernoulli(p)-per-position mutation is simulated by geometric skips.  The skip
+// distribution is inverted EXACTLY with an integer threshold table
+//   thr[m] = floor((1-p)^m * 2^32)  for m = 1..cap   (thr[0] = 2^32 implied)
+//   skip(r) = #{ m in [1,cap] : r < thr[m] }
+// P(skip >= m) = thr[m]/2^32 = (1-p)^m.  A float log estimate seeds the
+// search and two integer correction loops make the result exact, so device
+// and host agree bit for bit.
+PGA_HD uint32_t geom_skip(uint32_t r, const uint32_t* thr, uint32_t cap, float inv_log2_1mp) {
+  // thr is 1-indexed: thr[m-1] holds thr[m]
+  if (cap == 0) return 0;
+  if (r >= thr[0]) return 0;  // flip at the very next position
+  float est = __builtin_log2f(((float)r + 0.5f) * (1.0f / 4294967296.0f)) * inv_log2_1mp;
+  uint32_t m = est <= 0.f ? 0u : (est >= (float)cap ? cap : (uint32_t)est);
+  while (m < cap && r < thr[m]) ++m;         // thr[m] == threshold for m+1
+  while (m > 0 && !(r < thr[m - 1])) --m;    // thr[m-1] == threshold for m
+  return m;
+}
+
+// ------------------------------------------------------------ arguments ----
+// One POD for every encoding.  Passed by value to kernels (fits the 4 KB
+// kernarg segment) and by const-ref to the CPU reference.
+struct GenArgs {
+  // population buffers (current generation read, next generation written)
+  const void* cur;
+  void* next;
+  const float* score_cur;
+  float* score_next;
+  unsigned long long* best_next;  // packed (orderable score << 32 | ~index), reset by launcher
+
+  uint64_t S;          // individuals
+  uint32_t L;          // genes (bits for BINARY)
+  uint32_t row_words;  // row stride in 32-bit words (multiple of 4)
+  uint32_t chunks;     // 16-byte chunks per row that hold genes
+  uint32_t encoding;
+
+  RngKey key;
+
+  // selection
+  int32_t selection;
+  uint32_t tour_k;
+  const float* cumfit;  // roulette: inclusive prefix sums of shifted scores (S)
+
+  // crossover
+  int32_t crossover;
+  uint32_t xo_thresh_hi;  // crossover happens iff word < xo_thresh (xo_thresh = p_c * 2^32,
+  uint32_t xo_always;     //  xo_always = 1 when p_c >= 1)
+  float blend_alpha;
+
+  // mutation
+  int32_t mutation;
+  float mut_rate;            // per gene (BIT_FLIP/GAUSSIAN/UNIFORM) or per individual
+  uint32_t mut_ind_thresh;   // per-individual threshold (RESET_ONE/SWAP/INVERSION)
+  const uint32_t* mut_thr;   // geometric skip thresholds (cap = L entries)
+  float mut_inv_log2_1mp;    // 1/log2(1-p)
+  float sigma;               // gaussian sigma
+  float lo, hi;              // REAL gene bounds
+
+  // objective
+  int32_t objective;
+  int32_t obj_i;         // integer parameter (trap order, rotated flag, ...)
+  float obj_f0, obj_f1;  // float parameters (capacity, max count, ...)
+  const float* obj_data; // problem data (weights, distance matrix, rotation, shift)
+  const float* obj_data2;
+  void* user_fn;         // reference-ABI device function pointer (OBJ_USER_FNPTR)
+
+  // elitism: children [0, n_elite) copy elite_idx[i] (E==1 may use best_cur)
+  uint32_t n_elite;
+  const uint32_t* elite_idx;
+  const unsigned long long* best_cur;  // per-block packed bests of the current generation
+  uint32_t n_best_cur;
+
+  // padding mask for the last chunk (BINARY)
+  u32x4 last_mask;
+};
+
+PGA_HD uint32_t sel_words(const GenArgs& a) {
+  return a.selection == SEL_TOURNAMENT ? 2u * a.tour_k : 2u;
+}
+
+PGA_HD bool do_crossover(const GenArgs& a, uint32_t w0) { return a.xo_always || w0 < a.xo_thresh_hi; }
+
+// bits of the 32-bit word starting at bit `base` that fall in [lo, hi)
+PGA_HD uint32_t range_mask32(uint32_t base, uint32_t lo, uint32_t hi) {
+  uint32_t l = lo <= base ? 0u : (lo - base >= 32u ? 32u : lo - base);
+  uint32_t h = hi <= base ? 0u : (hi - base >= 32u ? 32u : hi - base);
+  uint32_t mh = h >= 32u ? 0xFFFFFFFFu : ((1u << h) - 1u);
+  uint32_t ml = l >= 32u ? 0xFFFFFFFFu : ((1u << l) - 1u);
+  return mh & ~ml;
+}
+
+// Lanes cooperating on one individual: the smallest power of two >= chunks,
+// capped at one wave.  Part of the SEMANTICS (it fixes the float summation
+// order of group reductions), so the CPU reference uses it too.
+PGA_HD uint32_t group_size(uint32_t chunks) {
+  uint32_t g = 1;
+  while (g < chunks && g < 64) g <<= 1;
+  return g;
+}
+
+// Kernel modes
+enum Mode : int32_t {
+  MODE_GEN = 0,     // select + crossover + mutate + evaluate (fused generation)
+  MODE_INIT = 1,    // random init + evaluate
+  MODE_EVAL = 2,    // evaluate current rows
+  MODE_CROSS = 3,   // select + crossover only (reference pga_crossover)
+  MODE_MUTATE = 4,  // mutate rows in place (reference pga_mutate)
+};
+
+// orderable encoding of a float score (monotone, -NaN < -inf < ... < +inf)
+PGA_HD uint32_t score_key(float s) {
+  uint32_t u;
+  __builtin_memcpy(&u, &s, 4);
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+PGA_HD float key_score(uint32_t k) {
+  uint32_t u = (k & 0x80000000u) ? (k & 0x7FFFFFFFu) : ~k;
+  float s;
+  __builtin_memcpy(&s, &u, 4);
+  return s;
+}
+// packed best: larger is better; ties resolved to the LOWER index (reference
+// pga_get_best keeps the first max, src/pga.cu:221-229)
+PGA_HD unsigned long long pack_best(float s, uint64_t idx) {
+  return ((unsigned long long)score_key(s) << 32) | (0xFFFFFFFFull - (uint32_t)idx);
+}
+PGA_HD uint64_t best_index(unsigned long long p) { return 0xFFFFFFFFull - (uint32_t)p; }
+PGA_HD float best_score(unsigned long long p) { return key_score((uint32_t)(p >> 32)); }
+
+}  // namespace pga

@@ -1,0 +1,51 @@
+// cpu.hpp — CPU reference backend.
+//
+// Same operator semantics as the gfx950 kernels, evaluated one individual at a
+// time on host memory.  Because every random draw is addressed by
+// (seed, generation, island, individual, purpose, block) and group
+// reductions follow the same lane butterfly, BINARY and PERMUTATION
+// generations are bit-identical to the GPU; REAL generations match up to
+// transcendental-function ulps.  This is the oracle of the test-suite and the
+// "CPU reference path" config of BASELINE.json.
+#pragma once
+
+#include "pga/core.hpp"
+
+namespace pga {
+namespace cpu {
+
+// returns number of best parts written (always 1)
+uint32_t encoding_run(int mode, const GenArgs& a, unsigned long long* best_parts);
+uint32_t binary_run(int mode, const GenArgs& a, unsigned long long* best_parts);
+uint32_t real_run(int mode, const GenArgs& a, unsigned long long* best_parts);
+uint32_t perm_run(int mode, const GenArgs& a, unsigned long long* best_parts);
+
+unsigned long long reduce_best(const unsigned long long* parts, uint32_t n);
+unsigned long long best_of_scores(const float* scores, uint64_t S);
+void score_stats(const float* scores, uint64_t S, float* out4);
+void roulette_prefix(const float* scores, uint64_t S, float* cumfit);
+void topk(const float* scores, uint64_t S, uint32_t k, bool largest, uint32_t* idx_out);
+void gather_rows(const void* rows, const float* scores, uint32_t row_words, const uint32_t* idx, uint32_t n,
+                 void* out_rows, float* out_scores);
+void scatter_rows(void* rows, float* scores, uint32_t row_words, const uint32_t* idx, uint32_t n,
+                  const void* in_rows, const float* in_scores);
+
+// CPU emulation of a GS-lane butterfly sum (lane 0's result)
+inline float butterfly_sum(float* v, uint32_t GS) {
+  float t[64];
+  for (uint32_t o = GS / 2; o > 0; o >>= 1) {
+    for (uint32_t q = 0; q < GS; ++q) t[q] = v[q] + v[q ^ o];
+    for (uint32_t q = 0; q < GS; ++q) v[q] = t[q];
+  }
+  return v[0];
+}
+
+// word t of a child's ST_CHILD pool
+inline uint32_t pool_word(const RngKey& key, uint64_t child, uint32_t t) {
+  return sel4(draw(key, ST_CHILD, child, t >> 2), t & 3u);
+}
+
+void select_parents(const GenArgs& a, uint64_t child, uint32_t& pa, uint32_t& pb);
+
+}  // namespace cpu
+}  // namespace pga

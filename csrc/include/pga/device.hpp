@@ -1,0 +1,137 @@
+// device.hpp — wave64 helpers shared by the encoding kernels (gfx950 only).
+#pragma once
+#include "pga/core.hpp"
+
+namespace pga {
+namespace dev {
+
+constexpr int kBlock = 256;  // 4 waves; every kernel uses this block size
+
+__device__ __forceinline__ uint32_t lane_id() { return threadIdx.x & 63u; }
+
+// reduction over an aligned group of GS lanes (GS power of two <= 64)
+template <int GS>
+__device__ __forceinline__ float group_sum(float v) {
+#pragma unroll
+  for (int o = GS / 2; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+template <int GS>
+__device__ __forceinline__ uint32_t group_sum_u(uint32_t v) {
+#pragma unroll
+  for (int o = GS / 2; o > 0; o >>= 1) v += (uint32_t)__shfl_xor((int)v, o, 64);
+  return v;
+}
+template <int GS>
+__device__ __forceinline__ uint32_t group_min_u(uint32_t v) {
+#pragma unroll
+  for (int o = GS / 2; o > 0; o >>= 1) {
+    uint32_t w = (uint32_t)__shfl_xor((int)v, o, 64);
+    v = w < v ? w : v;
+  }
+  return v;
+}
+
+__device__ __forceinline__ unsigned long long shfl_xor_u64(unsigned long long v, int o) {
+  uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)v, o, 64);
+  uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(v >> 32), o, 64);
+  return ((unsigned long long)hi << 32) | lo;
+}
+
+// block-wide max of a packed best, result valid in every thread
+__device__ __forceinline__ unsigned long long block_max_u64(unsigned long long v, unsigned long long* lds4) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    unsigned long long w = shfl_xor_u64(v, o);
+    v = w > v ? w : v;
+  }
+  __syncthreads();
+  if (lane_id() == 0) lds4[threadIdx.x >> 6] = v;
+  __syncthreads();
+  unsigned long long r = lds4[0];
+#pragma unroll
+  for (int i = 1; i < kBlock / 64; ++i) r = lds4[i] > r ? lds4[i] : r;
+  return r;
+}
+
+// reduce an array of packed bests with the whole block
+__device__ __forceinline__ unsigned long long block_reduce_parts(const unsigned long long* parts, uint32_t n,
+                                                                 unsigned long long* lds4) {
+  unsigned long long v = 0;
+  for (uint32_t i = threadIdx.x; i < n; i += kBlock) v = parts[i] > v ? parts[i] : v;
+  return block_max_u64(v, lds4);
+}
+
+// Child word pool: lane q of a GS-lane group holds block q of the child's
+// ST_CHILD stream; word t < 4*GS is fetched from its owner lane with one
+// ds_bpermute, later words are computed on demand.  t must be group-uniform.
+template <int GS>
+struct Pool {
+  u32x4 w;
+  uint32_t gbase;
+  __device__ __forceinline__ uint32_t get(uint32_t t, const RngKey& key, uint64_t child) const {
+    if (t < 4u * GS) {
+      uint32_t v = sel4(w, t & 3u);
+      if (GS == 1) return v;
+      return (uint32_t)__shfl((int)v, (int)(gbase + (t >> 2)), 64);
+    }
+    return sel4(draw(key, ST_CHILD, child, t >> 2), t & 3u);
+  }
+};
+
+// fitness-proportional pick: smallest i with cumfit[i] > target (cumfit inclusive)
+__device__ __forceinline__ uint32_t roulette_pick(const float* cumfit, uint32_t S, uint32_t w) {
+  float total = cumfit[S - 1];
+  if (!(total > 0.f)) return word_to_index(w, S);  // all weights zero: uniform
+  float target = word_to_unit(w) * total;
+  uint32_t lo = 0, hi = S - 1;
+  while (lo < hi) {
+    uint32_t mid = (lo + hi) >> 1;
+    if (cumfit[mid] < target) lo = mid + 1; else hi = mid;
+  }
+  return lo;
+}
+
+// Pick two parents.  All selection words are group-uniform.
+template <int GS>
+__device__ __forceinline__ void select_parents(const GenArgs& a, const Pool<GS>& pool, uint64_t child,
+                                               uint32_t& pa, uint32_t& pb) {
+  const uint32_t S = (uint32_t)a.S;
+  if (a.selection == SEL_TOURNAMENT) {
+    const uint32_t k = a.tour_k;
+    if (k == 2) {
+      // issue all four score loads before any compare (memory-level parallelism)
+      uint32_t i0 = word_to_index(pool.get(W_SEL + 0, a.key, child), S);
+      uint32_t i1 = word_to_index(pool.get(W_SEL + 1, a.key, child), S);
+      uint32_t i2 = word_to_index(pool.get(W_SEL + 2, a.key, child), S);
+      uint32_t i3 = word_to_index(pool.get(W_SEL + 3, a.key, child), S);
+      float s0 = a.score_cur[i0], s1 = a.score_cur[i1], s2 = a.score_cur[i2], s3 = a.score_cur[i3];
+      pa = (s0 < s1) ? i1 : i0;
+      pb = (s2 < s3) ? i3 : i2;
+    } else {
+      uint32_t best[2];
+#pragma unroll
+      for (int p = 0; p < 2; ++p) {
+        uint32_t b = word_to_index(pool.get(W_SEL + p * k, a.key, child), S);
+        float bs = a.score_cur[b];
+        for (uint32_t j = 1; j < k; ++j) {
+          uint32_t c = word_to_index(pool.get(W_SEL + p * k + j, a.key, child), S);
+          float cs = a.score_cur[c];
+          if (bs < cs) { bs = cs; b = c; }
+        }
+        best[p] = b;
+      }
+      pa = best[0];
+      pb = best[1];
+    }
+  } else if (a.selection == SEL_ROULETTE) {
+    pa = roulette_pick(a.cumfit, S, pool.get(W_SEL + 0, a.key, child));
+    pb = roulette_pick(a.cumfit, S, pool.get(W_SEL + 1, a.key, child));
+  } else {
+    pa = word_to_index(pool.get(W_SEL + 0, a.key, child), S);
+    pb = word_to_index(pool.get(W_SEL + 1, a.key, child), S);
+  }
+}
+
+}  // namespace dev
+}  // namespace pga

@@ -1,0 +1,143 @@
+// island.hpp — the native GA runtime: one population (an "island") resident on
+// one device (or on the host for the CPU reference backend).
+//
+// An Island owns its memory (double-buffered rows + scores, per-block best
+// partials, mutation tables, objective data, top-k/roulette workspaces) and
+// enqueues every stage on ONE stream without host synchronisation, so a run
+// of n generations is n back-to-back fused kernel launches.  It is the
+// engine behind both the reference-compatible C API (csrc/capi/pga.cpp,
+// include/pga.h) and the torch bindings (csrc/python/bindings.cpp).
+//
+// Reference counterparts: struct population / struct pga (src/pga.cu:37-56),
+// __fill_population (:107-118), pga_run (:376-391), pga_get_best (:218-236).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "pga/core.hpp"
+
+namespace pga {
+
+struct Config {
+  int32_t encoding = ENC_BINARY;
+  uint64_t S = 0;
+  uint32_t L = 0;
+  int32_t selection = SEL_TOURNAMENT;
+  uint32_t tour_k = 2;
+  int32_t crossover = XO_UNIFORM;
+  float xo_prob = 1.f;
+  float blend_alpha = 0.5f;
+  int32_t mutation = MUT_BIT_FLIP;
+  float mut_rate = -1.f;  // < 0: 1/L per gene (BIT_FLIP/GAUSSIAN/UNIFORM), 0.01 per individual (RESET_ONE...)
+  float sigma = 0.1f;
+  float lo = 0.f, hi = 1.f;
+  int32_t objective = OBJ_ONEMAX;
+  int32_t obj_i = 0;
+  float obj_f0 = 0.f, obj_f1 = 0.f;
+  uint32_t n_elite = 0;
+  uint64_t seed = 0;
+  uint32_t island = 0;
+};
+
+// words per row and gene chunks for an encoding
+void row_geometry(int32_t encoding, uint32_t L, uint32_t* row_words, uint32_t* chunks);
+
+struct Buffer {
+  void* ptr = nullptr;
+  size_t bytes = 0;
+};
+
+class Island {
+ public:
+  // device >= 0: GPU ordinal; device < 0: CPU reference backend
+  Island(const Config& cfg, int device);
+  ~Island();
+  Island(const Island&) = delete;
+  Island& operator=(const Island&) = delete;
+
+  const Config& config() const { return cfg_; }
+  bool on_gpu() const { return device_ >= 0; }
+  int device() const { return device_; }
+  uint32_t row_words() const { return row_words_; }
+  uint32_t chunks() const { return chunks_; }
+  uint32_t generation() const { return gen_; }
+  void set_generation(uint32_t g) { gen_ = g; }
+  uint32_t epoch() const { return epoch_; }
+  void bump_epoch() { ++epoch_; }
+
+  hipStream_t stream = nullptr;
+
+  // ---- configuration (may be changed between generations) ----
+  void set_operators(const Config& c);  // selection/crossover/mutation/objective scalars
+  void set_objective_data(const float* host, size_t n, int which);  // which = 0 or 1
+  void set_user_fn(void* f) { user_fn_ = f; }
+
+  // ---- stages ----
+  void initialize();          // random population + evaluation (generation 0)
+  void evaluate();            // scores(cur) <- objective(rows(cur))
+  void run(uint32_t n);       // n fused generations
+  void crossover_stage();     // next <- crossover(select(cur))  (no mutation / evaluation)
+  void mutate_stage();        // mutate next in place
+  void swap();                // cur <-> next, generation++
+  void rebest();              // recompute best partials of cur from its scores
+
+  // ---- queries (synchronise the stream) ----
+  unsigned long long best_packed();
+  float best_score() { return pga::best_score(best_packed()); }
+  uint64_t best_index() { return pga::best_index(best_packed()); }
+  void stats(float out4[4]);  // min, max, sum, count of current scores
+  std::vector<uint32_t> topk_host(uint32_t k, bool largest);
+  std::vector<uint32_t> row_host(uint64_t i);
+
+  // ---- device-side building blocks (no sync) ----
+  void topk(uint32_t k, bool largest, uint32_t* idx_out);  // idx_out: device (or host for CPU) memory
+  void gather(const uint32_t* idx, uint32_t n, void* out_rows, float* out_scores);
+  void scatter(const uint32_t* idx, uint32_t n, const void* in_rows, const float* in_scores);
+
+  // raw buffers (cur = current generation)
+  void* rows(int which) { return rows_[which ^ cur_].ptr; }
+  float* scores(int which) { return (float*)scores_[which ^ cur_].ptr; }
+  unsigned long long* best_parts() { return (unsigned long long*)best_[cur_].ptr; }
+  uint32_t n_best() const { return n_best_[cur_]; }
+  void set_n_best(uint32_t n) { n_best_[cur_] = n; }
+  size_t row_bytes() const { return 4ull * row_words_; }
+
+  // scratch buffers for callers (migration staging)
+  void* scratch(size_t bytes);
+
+  // checkpoint: header + current rows + scores
+  void save(const std::string& path);
+  void load(const std::string& path);
+
+  void synchronize();
+  void copy_to_host(void* dst, const void* src, size_t bytes);
+  void copy_to_device(void* dst, const void* src, size_t bytes);
+
+ private:
+  GenArgs make_args(int mode);
+  uint32_t launch(int mode, const GenArgs& a, unsigned long long* parts);
+  void prepare_generation();  // elitism indices, roulette prefix
+  Buffer alloc(size_t bytes);
+  void release(Buffer& b);
+  void rebuild_mut_table();
+
+  Config cfg_;
+  int device_;
+  uint32_t row_words_ = 0, chunks_ = 0;
+  int cur_ = 0;
+  uint32_t gen_ = 0, epoch_ = 0;
+  Buffer rows_[2], scores_[2], best_[2];
+  uint32_t n_best_[2] = {0, 0};
+  Buffer mut_thr_, obj_data_[2], elite_idx_, cumfit_, cum_ws_, topk_ws_, stats_, out_best_, scratch_;
+  size_t obj_len_[2] = {0, 0};
+  float mut_inv_ = 0.f;
+  float mut_rate_eff_ = 0.f;
+  void* user_fn_ = nullptr;
+  u32x4 last_mask_{0, 0, 0, 0};
+};
+
+}  // namespace pga

@@ -1,0 +1,72 @@
+// ops.hpp — host-side launcher API of the engine's device operators.
+//
+// Every operator takes raw device pointers and a HIP stream, allocates
+// nothing and never synchronises, so callers can capture sequences of them
+// into a hipGraph.  The same entry points back the C API runtime
+// (csrc/capi) and the torch bindings (csrc/python); the CPU reference
+// backend (csrc/cpu) implements identical semantics on host memory.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <stdexcept>
+#include <string>
+
+#include "pga/core.hpp"
+
+#define PGA_HIP_CHECK(expr)                                                                  \
+  do {                                                                                       \
+    hipError_t _e = (expr);                                                                  \
+    if (_e != hipSuccess)                                                                    \
+      throw std::runtime_error(std::string("HIP error: ") + hipGetErrorString(_e) + " at " + \
+                               __FILE__ + ":" + std::to_string(__LINE__));                   \
+  } while (0)
+
+namespace pga {
+
+// Max blocks of a persistent grid-stride launch; per-block best arrays must
+// hold at least this many entries.
+constexpr uint32_t kMaxGrid = 8192;
+
+// grid for `S` work items processed `per_block` at a time: min(ceil, 8*CUs)
+uint32_t launch_grid(uint64_t S, uint32_t per_block);
+int device_cu_count();
+
+// ---- encodings: one launch per call, returns the grid used (= number of
+// valid entries written to best_parts, when the mode evaluates) ----
+uint32_t binary_launch(int mode, const GenArgs& a, unsigned long long* best_parts, hipStream_t s);
+uint32_t real_launch(int mode, const GenArgs& a, unsigned long long* best_parts, hipStream_t s);
+uint32_t perm_launch(int mode, const GenArgs& a, unsigned long long* best_parts, hipStream_t s);
+
+inline uint32_t encoding_launch(int mode, const GenArgs& a, unsigned long long* best_parts, hipStream_t s) {
+  switch (a.encoding) {
+    case ENC_BINARY: return binary_launch(mode, a, best_parts, s);
+    case ENC_REAL: return real_launch(mode, a, best_parts, s);
+    default: return perm_launch(mode, a, best_parts, s);
+  }
+}
+
+// ---- reductions / selection helpers (util.hip) ----
+// out[0] = max over parts[0..n)
+void reduce_best_launch(const unsigned long long* parts, uint32_t n, unsigned long long* out, hipStream_t s);
+// per-block best over arbitrary scores (for externally evaluated populations)
+uint32_t best_of_scores_launch(const float* scores, uint64_t S, unsigned long long* parts, hipStream_t s);
+// stats[0..3] = {min, max, sum, count} of scores (count as float)
+void score_stats_launch(const float* scores, uint64_t S, float* stats, hipStream_t s);
+// roulette: cumfit = inclusive prefix sum of max(score - min, 0); workspace >= 2*kMaxGrid floats
+void roulette_prefix_launch(const float* scores, uint64_t S, float* cumfit, float* workspace, hipStream_t s);
+// top-k by score (descending, ties -> lower index); idx_out[k]; workspace: topk_workspace_bytes(S)
+size_t topk_workspace_bytes(uint64_t S, uint32_t k);
+void topk_launch(const float* scores, uint64_t S, uint32_t k, bool largest, uint32_t* idx_out, void* workspace,
+                 hipStream_t s);
+// rows: out[i] = rows[idx[i]] (row_words 32-bit words per row), optional scores
+void gather_rows_launch(const void* rows, const float* scores, uint32_t row_words, const uint32_t* idx, uint32_t n,
+                        void* out_rows, float* out_scores, hipStream_t s);
+// rows[idx[i]] = in[i]
+void scatter_rows_launch(void* rows, float* scores, uint32_t row_words, const uint32_t* idx, uint32_t n,
+                         const void* in_rows, const float* in_scores, hipStream_t s);
+
+// mutation threshold table for geometric skips: thr[m-1] = floor((1-p)^m 2^32), m = 1..L
+void build_mut_table(float p, uint32_t L, uint32_t* host_out, float* inv_log2_1mp);
+
+}  // namespace pga

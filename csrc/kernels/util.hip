@@ -1,0 +1,468 @@
+// util.hip — population-wide reductions, roulette prefix sums, radix-select
+// top-k, and row gather/scatter (elitism, migration, best queries).
+//
+// Replaces the reference's host-side argmax over a D2H copy of every score
+// (pga_get_best, src/pga.cu:218-236) and implements its stubbed top-N /
+// migration entry points (src/pga.cu:238-248, :368-374) on the device.
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+
+#include <cmath>
+#include <mutex>
+
+#include "pga/device.hpp"
+#include "pga/ops.hpp"
+
+namespace pga {
+
+int device_cu_count() {
+  static int counts[64] = {0};
+  int dev = 0;
+  PGA_HIP_CHECK(hipGetDevice(&dev));
+  if (dev < 0 || dev >= 64) dev = 0;
+  if (counts[dev] == 0) {
+    int n = 0;
+    PGA_HIP_CHECK(hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev));
+    counts[dev] = n > 0 ? n : 256;
+  }
+  return counts[dev];
+}
+
+uint32_t launch_grid(uint64_t S, uint32_t per_block) {
+  uint64_t need = (S + per_block - 1) / per_block;
+  uint64_t cap = (uint64_t)device_cu_count() * 8;
+  if (cap > kMaxGrid) cap = kMaxGrid;
+  uint64_t g = need < cap ? need : cap;
+  return (uint32_t)(g == 0 ? 1 : g);
+}
+
+void build_mut_table(float p, uint32_t L, uint32_t* out, float* inv_log2_1mp) {
+  const double q = 1.0 - (double)p;
+  double t = 1.0;
+  for (uint32_t m = 1; m <= L; ++m) {
+    t *= q;
+    double v = std::floor(t * 4294967296.0);
+    out[m - 1] = v >= 4294967295.0 ? 0xFFFFFFFFu : (v <= 0.0 ? 0u : (uint32_t)v);
+  }
+  if (p <= 0.f) *inv_log2_1mp = 0.f;
+  else if (p >= 1.f) *inv_log2_1mp = 0.f;
+  else *inv_log2_1mp = (float)(1.0 / std::log2(q));
+}
+
+namespace {
+using namespace dev;
+
+__global__ __launch_bounds__(kBlock) void reduce_best_kernel(const unsigned long long* parts, uint32_t n,
+                                                             unsigned long long* out) {
+  __shared__ unsigned long long lds[kBlock / 64];
+  unsigned long long b = block_reduce_parts(parts, n, lds);
+  if (threadIdx.x == 0) out[0] = b;
+}
+
+__global__ __launch_bounds__(kBlock) void best_of_scores_kernel(const float* scores, uint64_t S,
+                                                                unsigned long long* parts) {
+  __shared__ unsigned long long lds[kBlock / 64];
+  unsigned long long b = 0;
+  for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < S; i += (uint64_t)gridDim.x * kBlock) {
+    unsigned long long p = pack_best(scores[i], i);
+    b = p > b ? p : b;
+  }
+  b = block_max_u64(b, lds);
+  if (threadIdx.x == 0) parts[blockIdx.x] = b;
+}
+
+template <typename T, typename Op>
+__device__ __forceinline__ T block_reduce(T v, T* lds, Op op) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = op(v, __shfl_xor(v, o, 64));
+  __syncthreads();
+  if (lane_id() == 0) lds[threadIdx.x >> 6] = v;
+  __syncthreads();
+  T r = lds[0];
+#pragma unroll
+  for (int i = 1; i < kBlock / 64; ++i) r = op(r, lds[i]);
+  return r;
+}
+
+struct FMin { __device__ float operator()(float a, float b) const { return fminf(a, b); } };
+struct FMax { __device__ float operator()(float a, float b) const { return fmaxf(a, b); } };
+struct FAdd { __device__ float operator()(float a, float b) const { return a + b; } };
+
+// stage 1: per-block {min, max, sum}
+__global__ __launch_bounds__(kBlock) void stats_part_kernel(const float* s, uint64_t S, float* parts) {
+  __shared__ float lds[kBlock / 64];
+  float mn = INFINITY, mx = -INFINITY, sm = 0.f;
+  for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < S; i += (uint64_t)gridDim.x * kBlock) {
+    float v = s[i];
+    mn = fminf(mn, v);
+    mx = fmaxf(mx, v);
+    sm += v;
+  }
+  mn = block_reduce(mn, lds, FMin());
+  mx = block_reduce(mx, lds, FMax());
+  sm = block_reduce(sm, lds, FAdd());
+  if (threadIdx.x == 0) {
+    parts[3 * blockIdx.x + 0] = mn;
+    parts[3 * blockIdx.x + 1] = mx;
+    parts[3 * blockIdx.x + 2] = sm;
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void stats_final_kernel(const float* parts, uint32_t n, uint64_t S,
+                                                             float* out) {
+  __shared__ float lds[kBlock / 64];
+  float mn = INFINITY, mx = -INFINITY, sm = 0.f;
+  for (uint32_t i = threadIdx.x; i < n; i += kBlock) {
+    mn = fminf(mn, parts[3 * i]);
+    mx = fmaxf(mx, parts[3 * i + 1]);
+    sm += parts[3 * i + 2];
+  }
+  mn = block_reduce(mn, lds, FMin());
+  mx = block_reduce(mx, lds, FMax());
+  sm = block_reduce(sm, lds, FAdd());
+  if (threadIdx.x == 0) {
+    out[0] = mn;
+    out[1] = mx;
+    out[2] = sm;
+    out[3] = (float)S;
+  }
+}
+
+// roulette: contiguous range per block, weights = max(s - min, 0)
+__device__ __forceinline__ float block_excl_scan(float v, float* lds, float& total) {
+  // inclusive wave scan
+  const uint32_t lane = lane_id();
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    float t = __shfl_up(v, o, 64);
+    if (lane >= (uint32_t)o) v += t;
+  }
+  __syncthreads();
+  if (lane == 63) lds[threadIdx.x >> 6] = v;
+  __syncthreads();
+  float off = 0.f;
+  total = 0.f;
+  for (int i = 0; i < kBlock / 64; ++i) {
+    if (i < (int)(threadIdx.x >> 6)) off += lds[i];
+    total += lds[i];
+  }
+  return off + v;  // inclusive
+}
+
+__global__ __launch_bounds__(kBlock) void prefix_part_kernel(const float* s, uint64_t S, uint64_t per_block,
+                                                             const float* stats, float* block_sums) {
+  __shared__ float lds[kBlock / 64];
+  const float mn = stats[0];
+  const uint64_t b0 = (uint64_t)blockIdx.x * per_block;
+  const uint64_t b1 = b0 + per_block < S ? b0 + per_block : S;
+  float sm = 0.f;
+  for (uint64_t i = b0 + threadIdx.x; i < b1; i += kBlock) sm += fmaxf(s[i] - mn, 0.f);
+  sm = block_reduce(sm, lds, FAdd());
+  if (threadIdx.x == 0) block_sums[blockIdx.x] = sm;
+}
+
+__global__ __launch_bounds__(kBlock) void prefix_blocks_kernel(float* block_sums, uint32_t n) {
+  // exclusive scan of n block sums, single block, sequential tiles
+  __shared__ float lds[kBlock / 64];
+  float carry = 0.f;
+  for (uint32_t t0 = 0; t0 < n; t0 += kBlock) {
+    uint32_t i = t0 + threadIdx.x;
+    float v = i < n ? block_sums[i] : 0.f;
+    float total;
+    float inc = block_excl_scan(v, lds, total);
+    if (i < n) block_sums[i] = carry + inc - v;
+    carry += total;
+    __syncthreads();
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void prefix_final_kernel(const float* s, uint64_t S, uint64_t per_block,
+                                                              const float* stats, const float* block_off,
+                                                              float* cumfit) {
+  __shared__ float lds[kBlock / 64];
+  const float mn = stats[0];
+  const uint64_t b0 = (uint64_t)blockIdx.x * per_block;
+  const uint64_t b1 = b0 + per_block < S ? b0 + per_block : S;
+  float carry = block_off[blockIdx.x];
+  for (uint64_t t0 = b0; t0 < b1; t0 += kBlock) {
+    uint64_t i = t0 + threadIdx.x;
+    float v = i < b1 ? fmaxf(s[i] - mn, 0.f) : 0.f;
+    float total;
+    float inc = block_excl_scan(v, lds, total);
+    if (i < b1) cumfit[i] = carry + inc;
+    carry += total;
+    __syncthreads();
+  }
+}
+
+// ---------------- radix-select top-k ----------------
+struct TopkState {
+  uint32_t prefix, mask, remaining, pad;
+  uint32_t hist[256];
+};
+
+__device__ __forceinline__ uint32_t topk_key(float s, bool largest) {
+  uint32_t k = score_key(s);
+  return largest ? k : ~k;
+}
+
+__global__ __launch_bounds__(kBlock) void topk_init_kernel(TopkState* st, uint32_t k) {
+  if (threadIdx.x == 0) {
+    st->prefix = 0;
+    st->mask = 0;
+    st->remaining = k;
+  }
+  st->hist[threadIdx.x] = 0;
+}
+
+__global__ __launch_bounds__(kBlock) void topk_hist_kernel(const float* s, uint64_t S, bool largest, uint32_t shift,
+                                                           TopkState* st) {
+  __shared__ uint32_t h[256];
+  h[threadIdx.x] = 0;
+  __syncthreads();
+  const uint32_t prefix = st->prefix, mask = st->mask;
+  for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < S; i += (uint64_t)gridDim.x * kBlock) {
+    uint32_t key = topk_key(s[i], largest);
+    if ((key & mask) == prefix) atomicAdd(&h[(key >> shift) & 255u], 1u);
+  }
+  __syncthreads();
+  if (h[threadIdx.x]) atomicAdd(&st->hist[threadIdx.x], h[threadIdx.x]);
+}
+
+__global__ __launch_bounds__(kBlock) void topk_digit_kernel(TopkState* st, uint32_t shift) {
+  if (threadIdx.x == 0) {
+    uint32_t rem = st->remaining;
+    uint32_t d = 255;
+    for (;; --d) {
+      uint32_t c = st->hist[d];
+      if (c >= rem || d == 0) break;
+      rem -= c;
+    }
+    st->remaining = rem;
+    st->prefix |= d << shift;
+    st->mask |= 255u << shift;
+  }
+  __syncthreads();
+  st->hist[threadIdx.x] = 0;
+}
+
+// ordered compaction: contiguous range per block
+__global__ __launch_bounds__(kBlock) void topk_count_kernel(const float* s, uint64_t S, uint64_t per_block,
+                                                            bool largest, const TopkState* st, uint32_t* cnt) {
+  __shared__ uint32_t lds[kBlock / 64];
+  const uint32_t T = st->prefix;
+  const uint64_t b0 = (uint64_t)blockIdx.x * per_block;
+  const uint64_t b1 = b0 + per_block < S ? b0 + per_block : S;
+  uint32_t gt = 0, eq = 0;
+  for (uint64_t i = b0 + threadIdx.x; i < b1; i += kBlock) {
+    uint32_t key = topk_key(s[i], largest);
+    gt += key > T;
+    eq += key == T;
+  }
+  auto add = [](uint32_t a, uint32_t b) { return a + b; };
+  gt = block_reduce(gt, lds, add);
+  eq = block_reduce(eq, lds, add);
+  if (threadIdx.x == 0) {
+    cnt[2 * blockIdx.x] = gt;
+    cnt[2 * blockIdx.x + 1] = eq;
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void topk_offsets_kernel(uint32_t* cnt, uint32_t n) {
+  if (threadIdx.x == 0) {
+    uint32_t g = 0, e = 0;
+    for (uint32_t i = 0; i < n; ++i) {
+      uint32_t cg = cnt[2 * i], ce = cnt[2 * i + 1];
+      cnt[2 * i] = g;
+      cnt[2 * i + 1] = e;
+      g += cg;
+      e += ce;
+    }
+    cnt[2 * n] = g;  // total strictly greater
+  }
+}
+
+__device__ __forceinline__ uint32_t block_excl_scan_u(uint32_t v, uint32_t* lds, uint32_t& total) {
+  const uint32_t lane = lane_id();
+  uint32_t inc = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    uint32_t t = (uint32_t)__shfl_up((int)inc, o, 64);
+    if (lane >= (uint32_t)o) inc += t;
+  }
+  __syncthreads();
+  if (lane == 63) lds[threadIdx.x >> 6] = inc;
+  __syncthreads();
+  uint32_t off = 0;
+  total = 0;
+  for (int i = 0; i < kBlock / 64; ++i) {
+    if (i < (int)(threadIdx.x >> 6)) off += lds[i];
+    total += lds[i];
+  }
+  return off + inc - v;
+}
+
+__global__ __launch_bounds__(kBlock) void topk_write_kernel(const float* s, uint64_t S, uint64_t per_block,
+                                                            bool largest, const TopkState* st, const uint32_t* cnt,
+                                                            uint32_t nblocks, uint32_t* keys_out, uint32_t* idx_out) {
+  __shared__ uint32_t lds[kBlock / 64];
+  const uint32_t T = st->prefix;
+  const uint32_t need_eq = st->remaining;
+  const uint32_t gt_total = cnt[2 * nblocks];
+  uint32_t gpos = cnt[2 * blockIdx.x], epos = cnt[2 * blockIdx.x + 1];
+  const uint64_t b0 = (uint64_t)blockIdx.x * per_block;
+  const uint64_t b1 = b0 + per_block < S ? b0 + per_block : S;
+  for (uint64_t t0 = b0; t0 < b1; t0 += kBlock) {
+    uint64_t i = t0 + threadIdx.x;
+    uint32_t key = i < b1 ? topk_key(s[i], largest) : 0u;
+    uint32_t isg = (i < b1 && key > T) ? 1u : 0u;
+    uint32_t ise = (i < b1 && key == T) ? 1u : 0u;
+    uint32_t tg, te;
+    uint32_t rg = block_excl_scan_u(isg, lds, tg);
+    __syncthreads();
+    uint32_t re = block_excl_scan_u(ise, lds, te);
+    if (isg) {
+      keys_out[gpos + rg] = key;
+      idx_out[gpos + rg] = (uint32_t)i;
+    }
+    if (ise && epos + re < need_eq) {
+      keys_out[gt_total + epos + re] = key;
+      idx_out[gt_total + epos + re] = (uint32_t)i;
+    }
+    gpos += tg;
+    epos += te;
+    __syncthreads();
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void gather_rows_kernel(const uint4* rows, const float* scores, uint32_t rw16,
+                                                             const uint32_t* idx, uint32_t n, uint4* out,
+                                                             float* out_scores) {
+  const uint64_t total = (uint64_t)n * rw16;
+  for (uint64_t t = (uint64_t)blockIdx.x * kBlock + threadIdx.x; t < total; t += (uint64_t)gridDim.x * kBlock) {
+    uint64_t r = t / rw16, c = t % rw16;
+    uint64_t src = idx[r];
+    out[t] = rows[src * rw16 + c];
+    if (c == 0 && scores && out_scores) out_scores[r] = scores[src];
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void scatter_rows_kernel(uint4* rows, float* scores, uint32_t rw16,
+                                                              const uint32_t* idx, uint32_t n, const uint4* in,
+                                                              const float* in_scores) {
+  const uint64_t total = (uint64_t)n * rw16;
+  for (uint64_t t = (uint64_t)blockIdx.x * kBlock + threadIdx.x; t < total; t += (uint64_t)gridDim.x * kBlock) {
+    uint64_t r = t / rw16, c = t % rw16;
+    uint64_t dst = idx[r];
+    rows[dst * rw16 + c] = in[t];
+    if (c == 0 && scores && in_scores) scores[dst] = in_scores[r];
+  }
+}
+
+inline size_t align_up(size_t x) { return (x + 255) & ~(size_t)255; }
+
+}  // namespace
+
+void reduce_best_launch(const unsigned long long* parts, uint32_t n, unsigned long long* out, hipStream_t s) {
+  hipLaunchKernelGGL(reduce_best_kernel, 1, kBlock, 0, s, parts, n, out);
+  PGA_HIP_CHECK(hipGetLastError());
+}
+
+uint32_t best_of_scores_launch(const float* scores, uint64_t S, unsigned long long* parts, hipStream_t s) {
+  uint32_t grid = launch_grid(S, kBlock * 4);
+  hipLaunchKernelGGL(best_of_scores_kernel, grid, kBlock, 0, s, scores, S, parts);
+  PGA_HIP_CHECK(hipGetLastError());
+  return grid;
+}
+
+void score_stats_launch(const float* scores, uint64_t S, float* stats, hipStream_t s) {
+  // stats buffer layout: [0..4) result, [4..) 3*grid partials
+  uint32_t grid = launch_grid(S, kBlock * 4);
+  if (grid > 1024) grid = 1024;
+  hipLaunchKernelGGL(stats_part_kernel, grid, kBlock, 0, s, scores, S, stats + 4);
+  hipLaunchKernelGGL(stats_final_kernel, 1, kBlock, 0, s, stats + 4, grid, S, stats);
+  PGA_HIP_CHECK(hipGetLastError());
+}
+
+void roulette_prefix_launch(const float* scores, uint64_t S, float* cumfit, float* ws, hipStream_t s) {
+  // ws layout: [0..4) stats, [4 .. 4+3*1024) stats partials, then block sums
+  score_stats_launch(scores, S, ws, s);
+  uint32_t grid = launch_grid(S, kBlock * 4);
+  if (grid > 1024) grid = 1024;
+  const uint64_t per_block = (S + grid - 1) / grid;
+  float* block_sums = ws + 4 + 3 * 1024;
+  hipLaunchKernelGGL(prefix_part_kernel, grid, kBlock, 0, s, scores, S, per_block, ws, block_sums);
+  hipLaunchKernelGGL(prefix_blocks_kernel, 1, kBlock, 0, s, block_sums, grid);
+  hipLaunchKernelGGL(prefix_final_kernel, grid, kBlock, 0, s, scores, S, per_block, ws, block_sums, cumfit);
+  PGA_HIP_CHECK(hipGetLastError());
+}
+
+size_t topk_workspace_bytes(uint64_t S, uint32_t k) {
+  size_t cub_bytes = 0;
+  PGA_HIP_CHECK(hipcub::DeviceRadixSort::SortPairsDescending(nullptr, cub_bytes, (uint32_t*)nullptr,
+                                                             (uint32_t*)nullptr, (uint32_t*)nullptr,
+                                                             (uint32_t*)nullptr, (int)k));
+  (void)S;
+  return align_up(sizeof(TopkState)) + align_up(sizeof(uint32_t) * (2 * 1024 + 1)) + 3 * align_up(4ull * k) +
+         align_up(cub_bytes);
+}
+
+void topk_launch(const float* scores, uint64_t S, uint32_t k, bool largest, uint32_t* idx_out, void* ws,
+                 hipStream_t s) {
+  if (k == 0) return;
+  if (k > S) throw std::runtime_error("topk: k > S");
+  char* p = (char*)ws;
+  TopkState* st = (TopkState*)p;
+  p += align_up(sizeof(TopkState));
+  uint32_t* cnt = (uint32_t*)p;
+  p += align_up(sizeof(uint32_t) * (2 * 1024 + 1));
+  uint32_t* keys = (uint32_t*)p;
+  p += align_up(4ull * k);
+  uint32_t* keys_sorted = (uint32_t*)p;
+  p += align_up(4ull * k);
+  uint32_t* idx = (uint32_t*)p;
+  p += align_up(4ull * k);
+  size_t cub_bytes = 0;
+  PGA_HIP_CHECK(hipcub::DeviceRadixSort::SortPairsDescending(nullptr, cub_bytes, keys, keys_sorted, idx, idx_out,
+                                                             (int)k));
+
+  uint32_t grid = launch_grid(S, kBlock * 4);
+  hipLaunchKernelGGL(topk_init_kernel, 1, kBlock, 0, s, st, k);
+  for (int d = 0; d < 4; ++d) {
+    const uint32_t shift = 24 - 8 * d;
+    hipLaunchKernelGGL(topk_hist_kernel, grid, kBlock, 0, s, scores, S, largest, shift, st);
+    hipLaunchKernelGGL(topk_digit_kernel, 1, kBlock, 0, s, st, shift);
+  }
+  uint32_t cgrid = grid > 1024 ? 1024 : grid;
+  const uint64_t per_block = (S + cgrid - 1) / cgrid;
+  hipLaunchKernelGGL(topk_count_kernel, cgrid, kBlock, 0, s, scores, S, per_block, largest, st, cnt);
+  hipLaunchKernelGGL(topk_offsets_kernel, 1, 64, 0, s, cnt, cgrid);
+  hipLaunchKernelGGL(topk_write_kernel, cgrid, kBlock, 0, s, scores, S, per_block, largest, st, cnt, cgrid, keys,
+                     idx);
+  PGA_HIP_CHECK(hipGetLastError());
+  // stable descending sort keeps equal keys in ascending index order
+  PGA_HIP_CHECK(hipcub::DeviceRadixSort::SortPairsDescending(p, cub_bytes, keys, keys_sorted, idx, idx_out, (int)k,
+                                                             0, 32, s));
+}
+
+void gather_rows_launch(const void* rows, const float* scores, uint32_t row_words, const uint32_t* idx, uint32_t n,
+                        void* out_rows, float* out_scores, hipStream_t s) {
+  if (n == 0) return;
+  const uint32_t rw16 = row_words / 4;
+  uint32_t grid = launch_grid((uint64_t)n * rw16, kBlock);
+  hipLaunchKernelGGL(gather_rows_kernel, grid, kBlock, 0, s, (const uint4*)rows, scores, rw16, idx, n,
+                     (uint4*)out_rows, out_scores);
+  PGA_HIP_CHECK(hipGetLastError());
+}
+
+void scatter_rows_launch(void* rows, float* scores, uint32_t row_words, const uint32_t* idx, uint32_t n,
+                         const void* in_rows, const float* in_scores, hipStream_t s) {
+  if (n == 0) return;
+  const uint32_t rw16 = row_words / 4;
+  uint32_t grid = launch_grid((uint64_t)n * rw16, kBlock);
+  hipLaunchKernelGGL(scatter_rows_kernel, grid, kBlock, 0, s, (uint4*)rows, scores, rw16, idx, n,
+                     (const uint4*)in_rows, in_scores);
+  PGA_HIP_CHECK(hipGetLastError());
+}
+
+}  // namespace pga

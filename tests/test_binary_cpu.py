@@ -1,0 +1,175 @@
+"""BINARY encoding on the CPU reference backend (runs without a GPU)."""
+import math
+
+import pytest
+import torch
+
+import libpga_amd as pga
+from libpga_amd import _C
+
+
+def make(problem, S=256, seed=3, **kw):
+    return pga.GeneticAlgorithm(problem, S, seed=seed, device="cpu", **kw)
+
+
+@pytest.mark.parametrize("L", [1, 31, 64, 100, 128, 129, 1000, 1024, 9000])
+def test_init_scores_match_oracle(L):
+    ga = make(pga.models.OneMax(L), S=97)
+    g = ga.genomes()
+    assert g.shape == (97, L)
+    assert torch.equal(ga.problem.reference_fitness(g), ga.scores)
+    # padding bits are zero
+    rw = ga.rows.shape[1]
+    assert rw % 4 == 0
+    full = pga.ops.decode(ga.rows, "binary", rw * 32)
+    assert int(full[:, L:].sum()) == 0
+    # roughly half the bits set
+    assert abs(g.float().mean().item() - 0.5) < 0.1 + 2.0 / math.sqrt(97 * L)
+
+
+def test_codec_roundtrip():
+    g = torch.randint(0, 2, (13, 77), dtype=torch.uint8)
+    rows = pga.ops.encode(g, "binary", 77, 4)
+    assert torch.equal(pga.ops.decode(rows, "binary", 77), g)
+
+
+@pytest.mark.parametrize("prob", ["onemax", "trap", "leading", "knapsack"])
+@pytest.mark.parametrize("xo", ["uniform", "one_point", "two_point"])
+def test_generation_scores_match_oracle(prob, xo):
+    p = {
+        "onemax": pga.models.OneMax(300),
+        "trap": pga.models.Trap(256, 4),
+        "leading": pga.models.LeadingOnes(200),
+        "knapsack": pga.models.Knapsack01.random(150, seed=1),
+    }[prob]
+    ga = make(p, S=128, crossover=xo, elitism=1)
+    ga.run(7)
+    assert ga.generation == 7
+    assert torch.allclose(p.reference_fitness(ga.genomes()), ga.scores, rtol=0, atol=1e-3)
+
+
+def test_onemax_converges():
+    ga = make(pga.models.OneMax(64), S=1024, elitism=1)
+    s0 = ga.best_score()
+    ga.run(60)
+    assert ga.best_score() == 64.0 > s0
+
+
+def test_elitism_monotone():
+    ga = make(pga.models.Trap(128, 4), S=128, elitism=1)
+    prev = ga.best_score()
+    for _ in range(20):
+        ga.run(1)
+        cur = ga.best_score()
+        assert cur >= prev
+        prev = cur
+
+
+def test_elitism_k_preserves_top():
+    ga = make(pga.models.OneMax(200), S=300, elitism=5)
+    top_scores, top_genomes = ga.top(5)
+    ga.run(1)
+    new = ga.genomes()[:5]
+    assert torch.equal(new, top_genomes)
+    assert torch.equal(ga.scores[:5], top_scores)
+
+
+def test_determinism_and_seed():
+    a = make(pga.models.OneMax(500), seed=11)
+    b = make(pga.models.OneMax(500), seed=11)
+    c = make(pga.models.OneMax(500), seed=12)
+    for x in (a, b, c):
+        x.run(5)
+    assert torch.equal(a.rows, b.rows)
+    assert not torch.equal(a.rows, c.rows)
+
+
+def test_staged_equals_fused():
+    """crossover_stage + mutate_stage + swap + evaluate == one fused generation
+    (reference pga_run stage order, src/pga.cu:381-390)."""
+    a = make(pga.models.OneMax(777), seed=5)
+    b = make(pga.models.OneMax(777), seed=5)
+    a.run(1)
+    isl = b.island
+    isl.crossover_stage()
+    isl.mutate_stage()
+    isl.swap()
+    isl.evaluate()
+    assert torch.equal(a.rows, b.rows)
+    assert torch.equal(a.scores, b.scores)
+
+
+def test_mutation_rate_statistics():
+    """Bit-flip at rate p: with crossover=none and random selection, a child
+    differs from its parent in Binomial(L, p) bits."""
+    L, S, p = 512, 4096, 0.01
+    ga = make(pga.models.OneMax(L), S=S, selection="random", crossover="none", mutation_rate=p)
+    parents = ga.genomes().clone()
+    ga.run(1)
+    kids = ga.genomes()
+    # parent A of child i is word W_SEL=4 of its ST_CHILD pool (block 1, word 0)
+    seed = 3
+    idx = torch.tensor([(_C.philox(1 | (3 << 24), i, 0, 0, seed, 0)[0] * S) >> 32 for i in range(S)])
+    nflip = (kids != parents[idx]).sum(-1).float()
+    mean = nflip.mean().item()
+    assert abs(mean - L * p) < 4 * math.sqrt(L * p * (1 - p) / S)
+    var = nflip.var().item()
+    assert abs(var - L * p * (1 - p)) < 0.25 * L * p
+
+
+def test_topk_and_stats():
+    ga = make(pga.models.OneMax(100), S=500)
+    sc = ga.scores.clone()
+    idx = ga.island.topk(17, True).long()
+    ref = sorted(range(500), key=lambda i: (-sc[i].item(), i))[:17]
+    assert idx.tolist() == ref
+    low = ga.island.topk(9, False).long()
+    ref = sorted(range(500), key=lambda i: (sc[i].item(), i))[:9]
+    assert low.tolist() == ref
+    st = ga.stats()
+    assert st["max"] == sc.max().item() and st["min"] == sc.min().item()
+    assert abs(st["mean"] - sc.mean().item()) < 1e-3
+
+
+def test_roulette_runs_and_improves():
+    ga = make(pga.models.OneMax(64), S=512, selection="roulette")
+    m0 = ga.stats()["mean"]
+    ga.run(30)
+    assert ga.stats()["mean"] > m0 + 3
+
+
+def test_tournament_k():
+    ga = make(pga.models.OneMax(64), S=512, tournament_k=5)
+    m0 = ga.stats()["mean"]
+    ga.run(5)
+    assert ga.stats()["mean"] > m0 + 5
+
+
+def test_torch_objective():
+    fn = lambda g: (g[:, ::2].float().sum(-1) - g[:, 1::2].float().sum(-1))  # noqa: E731
+    p = pga.models.BinaryTorchObjective(64, fn, optimum=32)
+    ga = make(p, S=512, elitism=1)
+    ga.run(40)
+    assert torch.equal(fn(ga.genomes()).float(), ga.scores)
+    assert ga.best_score() >= 28
+
+
+def test_checkpoint_resume_exact(tmp_path):
+    a = make(pga.models.OneMax(300), seed=9)
+    a.run(4)
+    a.save(str(tmp_path / "c.ckpt"))
+    a.run(6)
+    b = make(pga.models.OneMax(300), seed=0)
+    b.load(str(tmp_path / "c.ckpt"))
+    assert b.generation == 4
+    b.run(6)
+    assert torch.equal(a.rows, b.rows) and torch.equal(a.scores, b.scores)
+
+
+def test_philox_known_answer():
+    # Random123 known-answer vector for philox4x32-10 (counter=0, key=0)
+    assert _C.philox(0, 0, 0, 0, 0, 0) == (0x6627E8D5, 0xE169C58D, 0xBC57AC4C, 0x9B00DBD8)
+    assert _C.philox(0xFFFFFFFF, 0xFFFFFFFF, 0xFFFFFFFF, 0xFFFFFFFF, 0xFFFFFFFF, 0xFFFFFFFF) == (
+        0x408F276D, 0x41C83B0E, 0xA20BC7C6, 0x6D5451FD)
+    assert _C.philox(0x243F6A88, 0x85A308D3, 0x13198A2E, 0x03707344, 0xA4093822, 0x299F31D0) == (
+        0xD16CFE09, 0x94FDCCEB, 0x5001E420, 0x24126EA1)

@@ -1,0 +1,137 @@
+"""gfx950 BINARY kernels vs the CPU reference backend (bit-exact) and the
+plain-PyTorch fp32 fitness oracle."""
+import pytest
+import torch
+
+import libpga_amd as pga
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+
+
+def pair(problem, S, seed=21, **kw):
+    g = pga.GeneticAlgorithm(problem, S, seed=seed, device=DEV, **kw)
+    c = pga.GeneticAlgorithm(problem, S, seed=seed, device="cpu", **kw)
+    return g, c
+
+
+def same(g, c):
+    torch.cuda.synchronize()
+    assert torch.equal(g.rows.cpu(), c.rows), "rows differ"
+    assert torch.equal(g.scores.cpu(), c.scores), "scores differ"
+
+
+def test_extension_is_native():
+    import libpga_amd._C as C
+
+    assert C.__file__.endswith("_C.so")
+    ga = pga.GeneticAlgorithm(pga.models.OneMax(64), 64, device=DEV)
+    assert ga.island.on_gpu
+
+
+@pytest.mark.parametrize("L", [1, 64, 100, 128, 1000, 1024, 4096, 9000])
+@pytest.mark.parametrize("S", [1, 77, 4096])
+def test_init_bitexact(L, S):
+    g, c = pair(pga.models.OneMax(L), S)
+    same(g, c)
+
+
+@pytest.mark.parametrize("L", [64, 1024, 3000, 9000])
+@pytest.mark.parametrize("xo", ["uniform", "one_point", "two_point", "none"])
+@pytest.mark.parametrize("elitism", [0, 1, 3])
+def test_generations_bitexact(L, xo, elitism):
+    g, c = pair(pga.models.OneMax(L), 1000, crossover=xo, elitism=elitism, crossover_prob=0.8)
+    g.run(3)
+    c.run(3)
+    same(g, c)
+    assert g.best_score() == c.best_score()
+
+
+@pytest.mark.parametrize("prob", ["trap", "leading", "knapsack"])
+def test_objectives_bitexact(prob):
+    p = {
+        "trap": pga.models.Trap(512, 8),
+        "leading": pga.models.LeadingOnes(300),
+        "knapsack": pga.models.Knapsack01.random(700, seed=2),
+    }[prob]
+    g, c = pair(p, 513, elitism=1, tournament_k=3)
+    g.run(4)
+    c.run(4)
+    same(g, c)
+    ref = p.reference_fitness(g.genomes().cpu())
+    assert torch.allclose(ref, g.scores.cpu(), rtol=0, atol=1e-2)
+
+
+@pytest.mark.parametrize("mut", [("bit_flip", 0.0), ("bit_flip", 0.05), ("bit_flip", 1.0), ("reset_one", 0.3)])
+def test_mutation_modes_bitexact(mut):
+    name, rate = mut
+    g, c = pair(pga.models.OneMax(300), 400, mutation=name, mutation_rate=rate)
+    g.run(2)
+    c.run(2)
+    same(g, c)
+
+
+def test_staged_equals_fused_gpu():
+    a = pga.GeneticAlgorithm(pga.models.OneMax(1024), 2048, seed=4, device=DEV)
+    b = pga.GeneticAlgorithm(pga.models.OneMax(1024), 2048, seed=4, device=DEV)
+    a.run(1)
+    isl = b.island
+    isl.crossover_stage()
+    isl.mutate_stage()
+    isl.swap()
+    isl.evaluate()
+    torch.cuda.synchronize()
+    assert torch.equal(a.rows, b.rows) and torch.equal(a.scores, b.scores)
+
+
+@pytest.mark.parametrize("S,k", [(1000, 1), (1000, 10), (100000, 1000), (1 << 20, 10486)])
+def test_topk_matches_cpu(S, k):
+    ga = pga.GeneticAlgorithm(pga.models.OneMax(64), S, seed=1, device=DEV)
+    sc = ga.scores.cpu()
+    for largest in (True, False):
+        idx = ga.island.topk(k, largest).cpu().long()
+        key = -sc if largest else sc
+        order = torch.from_numpy(__import__("numpy").lexsort((torch.arange(S).numpy(), key.numpy())))
+        assert torch.equal(idx, order[:k])
+
+
+def test_stats_and_best():
+    ga = pga.GeneticAlgorithm(pga.models.OneMax(1024), 100000, seed=2, device=DEV)
+    sc = ga.scores.cpu()
+    st = ga.stats()
+    assert st["max"] == sc.max().item() and st["min"] == sc.min().item()
+    assert abs(st["mean"] - sc.double().mean().item()) < 1e-2
+    s, i = ga.island.best()
+    assert s == sc.max().item() and i == int((sc == sc.max()).nonzero()[0])
+
+
+def test_roulette_gpu_improves():
+    ga = pga.GeneticAlgorithm(pga.models.OneMax(256), 65536, seed=2, device=DEV, selection="roulette")
+    m0 = ga.stats()["mean"]
+    ga.run(20)
+    assert ga.stats()["mean"] > m0 + 5
+
+
+def test_gather_scatter_gpu():
+    ga = pga.GeneticAlgorithm(pga.models.OneMax(1024), 5000, seed=2, device=DEV)
+    isl = ga.island
+    idx = torch.tensor([5, 17, 4999, 0], dtype=torch.int32, device=DEV)
+    rows = torch.empty(4 * isl.row_words, dtype=torch.int32, device=DEV)
+    sc = torch.empty(4, dtype=torch.float32, device=DEV)
+    isl.gather(idx, rows, sc)
+    assert torch.equal(rows.view(4, -1), ga.rows[idx.long()])
+    assert torch.equal(sc, ga.scores[idx.long()])
+    dst = torch.tensor([1, 2, 3, 4], dtype=torch.int32, device=DEV)
+    isl.scatter(dst, rows, sc)
+    assert torch.equal(ga.rows[1:5], rows.view(4, -1))
+
+
+def test_headline_config_converges():
+    """1M x 1024-bit OneMax: fused kernel scores == popcount oracle."""
+    ga = pga.GeneticAlgorithm(pga.models.OneMax(1024), 1 << 20, seed=3, device=DEV, elitism=1)
+    b0 = ga.best_score()
+    ga.run(50)
+    torch.cuda.synchronize()
+    ref = ga.problem.reference_fitness(ga.genomes())
+    assert torch.equal(ref, ga.scores)
+    assert ga.best_score() > b0 + 20
