@@ -71,7 +71,6 @@ uint32_t binary_run(int mode, const GenArgs& a, unsigned long long* best_parts) 
   const bool evaluates = a.objective != OBJ_NONE && (mode == MODE_GEN || mode == MODE_INIT || mode == MODE_EVAL);
   const bool bitflip = (gen || mode == MODE_MUTATE) && a.mutation == MUT_BIT_FLIP && a.mut_rate > 0.f;
   const bool reset_one = (gen || mode == MODE_MUTATE) && a.mutation == MUT_RESET_ONE;
-  const uint32_t mut_base = W_SEL + sel_words(a);
 
   uint32_t elite0 = 0;
   if (gen && a.n_elite > 0 && a.elite_idx == nullptr) elite0 = (uint32_t)best_index(reduce_best(a.best_cur, a.n_best_cur));
@@ -101,10 +100,9 @@ uint32_t binary_run(int mode, const GenArgs& a, unsigned long long* best_parts) 
           bhi = std::max(c1, c2);
         }
       }
-      uint32_t mpos = 0xFFFFFFFFu, mt = mut_base;
-      if (bitflip) mpos = geom_skip(pool_word(a.key, child, mt++), a.mut_thr, L, a.mut_inv_log2_1mp);
+      uint32_t rpos = 0xFFFFFFFFu;  // RESET_ONE: the one flipped bit
       if (reset_one && pool_word(a.key, child, W_MUTIND) < a.mut_ind_thresh)
-        mpos = word_to_index(pool_word(a.key, child, mt), L);
+        rpos = word_to_index(pool_word(a.key, child, W_MUTPOS), L);
 
       // per-lane objective accumulators
       uint32_t acc_u[64] = {0};
@@ -143,16 +141,17 @@ uint32_t binary_run(int mode, const GenArgs& a, unsigned long long* best_parts) 
             v[0] &= a.last_mask.x; v[1] &= a.last_mask.y; v[2] &= a.last_mask.z; v[3] &= a.last_mask.w;
           }
         }
-        if (bitflip) {
-          const uint32_t seg_end = std::min((c0 + GS) * 128u, L);
-          while (mpos < seg_end) {
-            uint32_t c = mpos >> 7, b = mpos & 127u;
-            seg[(c - c0) * 4 + (b >> 5)] ^= 1u << (b & 31u);
-            mpos += 1u + geom_skip(pool_word(a.key, child, mt++), a.mut_thr, L, a.mut_inv_log2_1mp);
+        for (uint32_t q = 0; q < GS; ++q) {
+          const uint32_t c = c0 + q;
+          if (c >= nchunks) continue;
+          uint32_t* v = &seg[q * 4];
+          if (bitflip) {
+            const uint32_t clen = std::min(128u, L - c * 128u);
+            u32x4 m = chunk_flip_mask(a, child, c, clen, chunk_mut_word(a.key, child, c), a.mut_thr);
+            v[0] ^= m.x; v[1] ^= m.y; v[2] ^= m.z; v[3] ^= m.w;
+          } else if (reset_one && (rpos >> 7) == c) {
+            v[(rpos & 127u) >> 5] ^= 1u << (rpos & 31u);
           }
-        } else if (reset_one && mpos != 0xFFFFFFFFu && (mpos >> 7) >= c0 && (mpos >> 7) < c0 + GS) {
-          uint32_t c = mpos >> 7, b = mpos & 127u;
-          seg[(c - c0) * 4 + (b >> 5)] ^= 1u << (b & 31u);
         }
         for (uint32_t q = 0; q < GS; ++q) {
           const uint32_t c = c0 + q;

@@ -129,14 +129,11 @@ void Island::rebuild_mut_table() {
   const bool per_ind = per_individual_mutation(cfg_.mutation);
   mut_rate_eff_ = cfg_.mut_rate >= 0.f ? cfg_.mut_rate : (per_ind ? 0.01f : 1.f / (float)cfg_.L);
   if (mut_rate_eff_ > 1.f) mut_rate_eff_ = 1.f;
-  std::vector<uint32_t> thr(cfg_.L);
-  build_mut_table(per_ind ? 0.f : mut_rate_eff_, cfg_.L, thr.data(), &mut_inv_);
-  if (mut_thr_.bytes < 4ull * cfg_.L) {
-    if (on_gpu()) synchronize();
-    release(mut_thr_);
-    mut_thr_ = alloc(4ull * cfg_.L);
-  }
-  copy_to_device(mut_thr_.ptr, thr.data(), 4ull * cfg_.L);
+  std::vector<uint32_t> thr(kMutCap);
+  build_mut_table(per_ind ? 0.f : mut_rate_eff_, kMutCap, thr.data(), &mut_inv_);
+  if (!mut_thr_.ptr) mut_thr_ = alloc(4ull * kMutCap);
+  if (on_gpu()) synchronize();
+  copy_to_device(mut_thr_.ptr, thr.data(), 4ull * kMutCap);
 }
 
 void Island::set_operators(const Config& c) {

@@ -97,13 +97,21 @@ enum Stream : uint32_t {
   ST_PERM = 7,     // permutation crossover helpers
 };
 
-// Child word-pool layout (word t = philox(ST_CHILD, block t/4)[t%4]):
+// Per-child randomness (stream ST_CHILD, one Philox block b per index):
+//   child words  t = 0,1,2,...  = register (t % 3) of block (t / 3)   [.x .y .z]
+//   mutation word of chunk c    = register .w of block c
+// so the lane that owns chunk c of an individual holds that chunk's first
+// mutation draw in its own register, and child words are fetched with one
+// group-uniform ds_bpermute.  Child-word layout:
 //   0      crossover-probability test
 //   1, 2   cut points / blend parameter
 //   3      per-individual mutation test (RESET_ONE / SWAP / INVERSION)
-//   4..    selection words (2k for tournament-k, 2 otherwise)
-//   then   mutation draws, consumed sequentially
-constexpr uint32_t W_XOPROB = 0, W_CUT1 = 1, W_CUT2 = 2, W_MUTIND = 3, W_SEL = 4;
+//   4      per-individual mutation position
+//   5..    selection words (2k for tournament-k, 2 otherwise)
+// Further draws of one chunk's mutation come from stream ST_MUTX, block
+// (chunk << 6) | (n >> 2), register n & 3 for the n-th extra draw.
+constexpr uint32_t W_XOPROB = 0, W_CUT1 = 1, W_CUT2 = 2, W_MUTIND = 3, W_MUTPOS = 4, W_SEL = 5;
+constexpr uint32_t kMutCap = 128;  // geometric-skip table length (one BINARY chunk)
 
 // ---------------------------------------------------------------- Philox ---
 struct u32x4 {
@@ -144,10 +152,33 @@ PGA_HD u32x4 draw(const RngKey& key, uint32_t stream, uint64_t ind, uint32_t blo
 PGA_HD uint32_t sel4(const u32x4& v, uint32_t i) {
   return i == 0 ? v.x : (i == 1 ? v.y : (i == 2 ? v.z : v.w));
 }
+PGA_HD uint32_t sel3(const u32x4& v, uint32_t i) { return i == 0 ? v.x : (i == 1 ? v.y : v.z); }
+
+// child word t (reference definition; kernels fetch it from the owner lane)
+PGA_HD uint32_t child_word(const RngKey& key, uint64_t child, uint32_t t) {
+  return sel3(draw(key, ST_CHILD, child, t / 3u), t % 3u);
+}
+// first mutation draw of chunk c
+PGA_HD uint32_t chunk_mut_word(const RngKey& key, uint64_t child, uint32_t c) {
+  return draw(key, ST_CHILD, child, c).w;
+}
+// n-th extra mutation draw of chunk c
+PGA_HD uint32_t chunk_mut_extra(const RngKey& key, uint64_t child, uint32_t c, uint32_t n) {
+  return sel4(draw(key, ST_MUTX, child, (c << 6) | (n >> 2)), n & 3u);
+}
 
 // uniform index in [0, n) from a 32-bit word (n < 2^32)
 PGA_HD uint32_t word_to_index(uint32_t w, uint32_t n) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  // One v_mul_hi_u32.  The empty asm makes the result opaque: otherwise hipcc
+  // folds zext(mulhi)*4 into a 64-bit shift of a register PAIR whose low half
+  // may be an in-flight load destination, which forces s_waitcnt vmcnt(0).
+  uint32_t r = __umulhi(w, n);
+  asm("" : "+v"(r));
+  return r;
+#else
   return (uint32_t)(((uint64_t)w * (uint64_t)n) >> 32);
+#endif
 }
 
 // uniform float in (0, 1], exactly representable, identical on host and device
@@ -233,6 +264,28 @@ struct GenArgs {
 
 PGA_HD uint32_t sel_words(const GenArgs& a) {
   return a.selection == SEL_TOURNAMENT ? 2u * a.tour_k : 2u;
+}
+
+// Bernoulli(p) flips over positions [0, clen) of chunk c (clen <= kMutCap):
+// first draw r0 = chunk_mut_word, then geometric skips.  Returns the flip
+// positions as a 128-bit mask.
+PGA_HD u32x4 chunk_flip_mask(const GenArgs& a, uint64_t child, uint32_t c, uint32_t clen, uint32_t r0,
+                             const uint32_t* thr) {
+  u32x4 m{0, 0, 0, 0};
+  if (r0 < thr[kMutCap - 1]) return m;  // no flip in 128 positions: the common case
+  uint32_t pos = geom_skip(r0, thr, kMutCap, a.mut_inv_log2_1mp);
+  uint32_t n = 0;
+  while (pos < clen) {
+    const uint32_t bit = 1u << (pos & 31u);
+    switch (pos >> 5) {
+      case 0: m.x ^= bit; break;
+      case 1: m.y ^= bit; break;
+      case 2: m.z ^= bit; break;
+      default: m.w ^= bit; break;
+    }
+    pos += 1u + geom_skip(chunk_mut_extra(a.key, child, c, n++), thr, kMutCap, a.mut_inv_log2_1mp);
+  }
+  return m;
 }
 
 PGA_HD bool do_crossover(const GenArgs& a, uint32_t w0) { return a.xo_always || w0 < a.xo_thresh_hi; }

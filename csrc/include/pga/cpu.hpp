@@ -40,10 +40,8 @@ inline float butterfly_sum(float* v, uint32_t GS) {
   return v[0];
 }
 
-// word t of a child's ST_CHILD pool
-inline uint32_t pool_word(const RngKey& key, uint64_t child, uint32_t t) {
-  return sel4(draw(key, ST_CHILD, child, t >> 2), t & 3u);
-}
+// child word t (see core.hpp for the layout)
+inline uint32_t pool_word(const RngKey& key, uint64_t child, uint32_t t) { return child_word(key, child, t); }
 
 void select_parents(const GenArgs& a, uint64_t child, uint32_t& pa, uint32_t& pb);
 

@@ -62,20 +62,22 @@ __device__ __forceinline__ unsigned long long block_reduce_parts(const unsigned 
   return block_max_u64(v, lds4);
 }
 
-// Child word pool: lane q of a GS-lane group holds block q of the child's
-// ST_CHILD stream; word t < 4*GS is fetched from its owner lane with one
-// ds_bpermute, later words are computed on demand.  t must be group-uniform.
+// Child word pool: lane q of a GS-lane group holds Philox block q of the
+// child's ST_CHILD stream.  Child word t < 3*GS lives in register t%3 of lane
+// t/3 and is fetched with one ds_bpermute (t must be group-uniform); later
+// words are computed on demand.  Register .w of lane q's block is the first
+// mutation draw of chunk q (see core.hpp).
 template <int GS>
 struct Pool {
   u32x4 w;
   uint32_t gbase;
   __device__ __forceinline__ uint32_t get(uint32_t t, const RngKey& key, uint64_t child) const {
-    if (t < 4u * GS) {
-      uint32_t v = sel4(w, t & 3u);
+    if (t < 3u * GS) {
+      const uint32_t v = sel3(w, t % 3u);
       if (GS == 1) return v;
-      return (uint32_t)__shfl((int)v, (int)(gbase + (t >> 2)), 64);
+      return (uint32_t)__shfl((int)v, (int)(gbase + t / 3u), 64);
     }
-    return sel4(draw(key, ST_CHILD, child, t >> 2), t & 3u);
+    return child_word(key, child, t);
   }
 };
 

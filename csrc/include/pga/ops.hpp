@@ -30,6 +30,10 @@ constexpr uint32_t kMaxGrid = 8192;
 
 // grid for `S` work items processed `per_block` at a time: min(ceil, 8*CUs)
 uint32_t launch_grid(uint64_t S, uint32_t per_block);
+// same, capped at the kernel's resident blocks per CU (hipOccupancy...) so a
+// persistent grid-stride launch never leaves a partial second wave
+uint32_t launch_grid_occ(uint64_t S, uint32_t per_block, const void* kernel);
+uint32_t occupancy_blocks(const void* kernel, int block);
 int device_cu_count();
 
 // ---- encodings: one launch per call, returns the grid used (= number of

@@ -9,6 +9,7 @@
 
 #include <cmath>
 #include <mutex>
+#include <unordered_map>
 
 #include "pga/device.hpp"
 #include "pga/ops.hpp"
@@ -31,6 +32,29 @@ int device_cu_count() {
 uint32_t launch_grid(uint64_t S, uint32_t per_block) {
   uint64_t need = (S + per_block - 1) / per_block;
   uint64_t cap = (uint64_t)device_cu_count() * 8;
+  if (cap > kMaxGrid) cap = kMaxGrid;
+  uint64_t g = need < cap ? need : cap;
+  return (uint32_t)(g == 0 ? 1 : g);
+}
+
+uint32_t occupancy_blocks(const void* kernel, int block) {
+  static std::mutex mu;
+  static std::unordered_map<uint64_t, int> cache;
+  int dev = 0;
+  PGA_HIP_CHECK(hipGetDevice(&dev));
+  const uint64_t key = (uint64_t)(uintptr_t)kernel * 64 + (uint64_t)dev;
+  std::lock_guard<std::mutex> g(mu);
+  auto it = cache.find(key);
+  if (it != cache.end()) return (uint32_t)it->second;
+  int n = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, kernel, block, 0) != hipSuccess || n <= 0) n = 1;
+  cache[key] = n;
+  return (uint32_t)n;
+}
+
+uint32_t launch_grid_occ(uint64_t S, uint32_t per_block, const void* kernel) {
+  uint64_t need = (S + per_block - 1) / per_block;
+  uint64_t cap = (uint64_t)device_cu_count() * occupancy_blocks(kernel, dev::kBlock);
   if (cap > kMaxGrid) cap = kMaxGrid;
   uint64_t g = need < cap ? need : cap;
   return (uint32_t)(g == 0 ? 1 : g);

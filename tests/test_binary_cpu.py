@@ -107,9 +107,9 @@ def test_mutation_rate_statistics():
     parents = ga.genomes().clone()
     ga.run(1)
     kids = ga.genomes()
-    # parent A of child i is word W_SEL=4 of its ST_CHILD pool (block 1, word 0)
+    # parent A of child i is child word W_SEL=5: ST_CHILD block 1, register .z
     seed = 3
-    idx = torch.tensor([(_C.philox(1 | (3 << 24), i, 0, 0, seed, 0)[0] * S) >> 32 for i in range(S)])
+    idx = torch.tensor([(_C.philox(1 | (3 << 24), i, 0, 0, seed, 0)[2] * S) >> 32 for i in range(S)])
     nflip = (kids != parents[idx]).sum(-1).float()
     mean = nflip.mean().item()
     assert abs(mean - L * p) < 4 * math.sqrt(L * p * (1 - p) / S)

@@ -1,0 +1,26 @@
+#!/bin/bash
+# One gpurun session: GPU tests, smoke, short bench, rocprofv3 kernel stats.
+# Every GPU step has its own time limit and the chain stops at the first failure.
+set -o pipefail
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+cd "$R"
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+STEP=${1:-all}
+if [ "$STEP" = "all" ] || [ "$STEP" = "tests" ]; then
+  timeout -k 10 ${PYTEST_TIMEOUT:-900} python -m pytest tests -m gpu -q --maxfail=10 ${PYTEST_ARGS:-} > gpurun_out/pytest_gpu.log 2>&1
+  rc=$?; tail -5 gpurun_out/pytest_gpu.log; [ $rc -ne 0 ] && exit $rc
+fi
+if [ "$STEP" = "all" ] || [ "$STEP" = "smoke" ]; then
+  timeout -k 10 300 python __graft_entry__.py smoke > gpurun_out/smoke.log 2>&1 || { cat gpurun_out/smoke.log; exit 1; }
+  cat gpurun_out/smoke.log
+fi
+if [ "$STEP" = "all" ] || [ "$STEP" = "bench" ]; then
+  timeout -k 10 300 python bench.py --steps ${BENCH_STEPS:-500} --warmup 50 > gpurun_out/bench.log 2>&1 || { cat gpurun_out/bench.log; exit 1; }
+  cat gpurun_out/bench.log
+fi
+if [ "$STEP" = "all" ] || [ "$STEP" = "prof" ]; then
+  cd /tmp
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/prof" -o run -- python3 "$R/bench.py" --steps 100 --warmup 10 > "$R/gpurun_out/prof.log" 2>&1 || { tail -30 "$R/gpurun_out/prof.log"; exit 1; }
+  find "$R/gpurun_out/prof" -name "*kernel_stats.csv" | head -3
+fi
