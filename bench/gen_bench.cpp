@@ -1,0 +1,58 @@
+// gen_bench.cpp — native (no python) generation benchmark of the Island runtime.
+//
+//   gen_bench [--pop N] [--length L] [--gens G] [--warmup W] [--xo uniform|one|two]
+//             [--elitism E] [--encoding binary|real|perm] [--objective N]
+// Prints one JSON line: us per generation measured with hipEvents around G
+// back-to-back fused generations on the null stream.
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+
+#include "pga/island.hpp"
+#include "pga/ops.hpp"
+
+int main(int argc, char** argv) {
+  pga::Config c;
+  c.S = 1u << 20;
+  c.L = 1024;
+  c.objective = pga::OBJ_ONEMAX;
+  c.n_elite = 1;
+  c.seed = 1234;
+  int gens = 300, warm = 30;
+  for (int i = 1; i + 1 < argc; i += 2) {
+    std::string k = argv[i], v = argv[i + 1];
+    if (k == "--pop") c.S = std::strtoull(v.c_str(), nullptr, 10);
+    else if (k == "--length") c.L = (uint32_t)std::atoi(v.c_str());
+    else if (k == "--gens") gens = std::atoi(v.c_str());
+    else if (k == "--warmup") warm = std::atoi(v.c_str());
+    else if (k == "--elitism") c.n_elite = (uint32_t)std::atoi(v.c_str());
+    else if (k == "--objective") c.objective = std::atoi(v.c_str());
+    else if (k == "--xo") c.crossover = v == "one" ? pga::XO_ONE_POINT : (v == "two" ? pga::XO_TWO_POINT : pga::XO_UNIFORM);
+    else if (k == "--encoding") {
+      c.encoding = v == "real" ? pga::ENC_REAL : (v == "perm" ? pga::ENC_PERMUTATION : pga::ENC_BINARY);
+      if (c.encoding == pga::ENC_REAL) { c.mutation = pga::MUT_GAUSSIAN; c.lo = -5.12f; c.hi = 5.12f; }
+      if (c.encoding == pga::ENC_PERMUTATION) { c.mutation = pga::MUT_SWAP; c.crossover = pga::XO_OX; }
+    }
+  }
+  pga::Island isl(c, 0);
+  isl.initialize();
+  isl.run(warm);
+  PGA_HIP_CHECK(hipDeviceSynchronize());
+  hipEvent_t e0, e1;
+  PGA_HIP_CHECK(hipEventCreate(&e0));
+  PGA_HIP_CHECK(hipEventCreate(&e1));
+  PGA_HIP_CHECK(hipEventRecord(e0, nullptr));
+  isl.run(gens);
+  PGA_HIP_CHECK(hipEventRecord(e1, nullptr));
+  PGA_HIP_CHECK(hipEventSynchronize(e1));
+  float ms = 0.f;
+  PGA_HIP_CHECK(hipEventElapsedTime(&ms, e0, e1));
+  const double us = 1000.0 * ms / gens;
+  std::printf("{\"pop\": %llu, \"length\": %u, \"gens\": %d, \"us_per_gen\": %.2f, \"gens_per_sec\": %.1f, "
+              "\"evals_per_sec\": %.4e, \"best\": %.1f}\n",
+              (unsigned long long)c.S, c.L, gens, us, 1e6 / us, 1e6 / us * (double)c.S, isl.best_score());
+  return 0;
+}

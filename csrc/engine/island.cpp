@@ -46,6 +46,7 @@ Island::Island(const Config& cfg, int device) : cfg_(cfg), device_(device) {
     rows_[i] = alloc(rb);
     scores_[i] = alloc(4ull * cfg_.S);
     best_[i] = alloc(8ull * kMaxGrid);
+    keys_[i] = alloc(2ull * cfg_.S);
   }
   out_best_ = alloc(64);
   stats_ = alloc(4ull * (4 + 3 * 1024));
@@ -62,7 +63,7 @@ Island::Island(const Config& cfg, int device) : cfg_(cfg), device_(device) {
 
 Island::~Island() {
   Buffer* all[] = {&rows_[0],   &rows_[1],     &scores_[0],   &scores_[1],  &best_[0],  &best_[1],   &mut_thr_,
-                   &obj_data_[0], &obj_data_[1], &elite_idx_, &cumfit_, &cum_ws_, &topk_ws_, &stats_,
+                   &obj_data_[0], &obj_data_[1], &keys_[0], &keys_[1], &elite_idx_, &cumfit_, &cum_ws_, &topk_ws_, &stats_,
                    &out_best_,  &scratch_};
   for (Buffer* b : all) {
     try {
@@ -216,6 +217,11 @@ GenArgs Island::make_args(int mode) {
   a.best_cur = (const unsigned long long*)best_[cur_].ptr;
   a.n_best_cur = n_best_[cur_];
   a.last_mask = last_mask_;
+  if (integer_objective(cfg_.objective, cfg_.L)) {
+    a.key_cur = (const uint16_t*)keys_[cur_].ptr;
+    a.key_next = (uint16_t*)keys_[nx].ptr;
+    if (mode == MODE_INIT || mode == MODE_EVAL) a.key_next = (uint16_t*)keys_[cur_].ptr;
+  }
   return a;
 }
 
@@ -239,6 +245,7 @@ void Island::rebest() {
   const float* sc = (const float*)scores_[cur_].ptr;
   if (on_gpu()) {
     n_best_[cur_] = best_of_scores_launch(sc, cfg_.S, (unsigned long long*)best_[cur_].ptr, stream);
+    if (integer_objective(cfg_.objective, cfg_.L)) scores_to_keys_launch(sc, cfg_.S, (uint16_t*)keys_[cur_].ptr, stream);
   } else {
     ((unsigned long long*)best_[cur_].ptr)[0] = cpu::best_of_scores(sc, cfg_.S);
     n_best_[cur_] = 1;
@@ -350,6 +357,7 @@ void Island::scatter(const uint32_t* idx, uint32_t n, const void* in_rows, const
     scatter_rows_launch(rows_[cur_].ptr, (float*)scores_[cur_].ptr, row_words_, idx, n, in_rows, in_scores, stream);
   else
     cpu::scatter_rows(rows_[cur_].ptr, (float*)scores_[cur_].ptr, row_words_, idx, n, in_rows, in_scores);
+  rebest();  // best partials and tournament keys follow the new scores
 }
 
 // ------------------------------------------------------------ checkpoint ---

@@ -258,6 +258,14 @@ struct GenArgs {
   const unsigned long long* best_cur;  // per-block packed bests of the current generation
   uint32_t n_best_cur;
 
+  // Tournament keys: for integer-valued objectives with scores in [0, 65535]
+  // (OneMax, LeadingOnes, Trap) every individual also carries key = score as
+  // u16.  The 2 MiB key array of a 1M population stays L2-resident, the 4 MiB
+  // f32 array does not, and tournament reads are random; comparisons are
+  // unchanged because the key is exact.  nullptr when disabled.
+  const uint16_t* key_cur;
+  uint16_t* key_next;
+
   // padding mask for the last chunk (BINARY)
   u32x4 last_mask;
 };
@@ -316,6 +324,11 @@ enum Mode : int32_t {
   MODE_CROSS = 3,   // select + crossover only (reference pga_crossover)
   MODE_MUTATE = 4,  // mutate rows in place (reference pga_mutate)
 };
+
+// objectives whose scores are exact integers in [0, L] (u16 tournament keys)
+PGA_HD bool integer_objective(int32_t obj, uint32_t L) {
+  return (obj == OBJ_ONEMAX || obj == OBJ_LEADING_ONES || obj == OBJ_TRAP) && L <= 65535u;
+}
 
 // orderable encoding of a float score (monotone, -NaN < -inf < ... < +inf)
 PGA_HD uint32_t score_key(float s) {

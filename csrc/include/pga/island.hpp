@@ -83,7 +83,7 @@ class Island {
   void crossover_stage();     // next <- crossover(select(cur))  (no mutation / evaluation)
   void mutate_stage();        // mutate next in place
   void swap();                // cur <-> next, generation++
-  void rebest();              // recompute best partials of cur from its scores
+  void rebest();              // recompute best partials (and tournament keys) of cur from its scores
 
   // ---- queries (synchronise the stream) ----
   unsigned long long best_packed();
@@ -130,7 +130,7 @@ class Island {
   uint32_t row_words_ = 0, chunks_ = 0;
   int cur_ = 0;
   uint32_t gen_ = 0, epoch_ = 0;
-  Buffer rows_[2], scores_[2], best_[2];
+  Buffer rows_[2], scores_[2], best_[2], keys_[2];
   uint32_t n_best_[2] = {0, 0};
   Buffer mut_thr_, obj_data_[2], elite_idx_, cumfit_, cum_ws_, topk_ws_, stats_, out_best_, scratch_;
   size_t obj_len_[2] = {0, 0};

@@ -55,6 +55,8 @@ inline uint32_t encoding_launch(int mode, const GenArgs& a, unsigned long long* 
 void reduce_best_launch(const unsigned long long* parts, uint32_t n, unsigned long long* out, hipStream_t s);
 // per-block best over arbitrary scores (for externally evaluated populations)
 uint32_t best_of_scores_launch(const float* scores, uint64_t S, unsigned long long* parts, hipStream_t s);
+// keys[i] = (uint16)scores[i] (integer objectives' tournament keys)
+void scores_to_keys_launch(const float* scores, uint64_t S, uint16_t* keys, hipStream_t s);
 // stats[0..3] = {min, max, sum, count} of scores (count as float)
 void score_stats_launch(const float* scores, uint64_t S, float* stats, hipStream_t s);
 // roulette: cumfit = inclusive prefix sum of max(score - min, 0); workspace >= 2*kMaxGrid floats

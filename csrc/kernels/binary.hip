@@ -227,6 +227,7 @@ __global__ __launch_bounds__(kBlock) void binary_kernel(GenArgs a, unsigned long
     }
     if (EVALS && q == 0) {
       a.score_next[child] = score;
+      if (a.key_next) a.key_next[child] = (uint16_t)score;
       const unsigned long long pb = pack_best(score, child);
       my_best = pb > my_best ? pb : my_best;
     }
@@ -256,7 +257,33 @@ __global__ __launch_bounds__(kBlock) void binary_kernel(GenArgs a, unsigned long
 // ---------------------------------------------------------------------------
 constexpr int XOK_UNIFORM = 0, XOK_RANGE = 1;  // crossover kind template values
 
-template <int GS, int OBJ, int XOK>
+// Diagnostic ablation switches (bench/micro/ablate builds only, see
+// bench/micro/README.md; the shipped build defines none of them).
+#ifndef PGA_ABL
+#define PGA_ABL 0
+#endif
+constexpr int kAblXoRng = 1, kAblPoolRng = 2, kAblMut = 4, kAblGather = 8;
+#ifndef PGA_CACHE
+#define PGA_CACHE 0  // 1: non-temporal child stores, 2: non-temporal parent loads
+#endif
+typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void store_row(uint4* p, uint4 v) {
+  if (PGA_CACHE & 1) {
+    v4u x = {v.x, v.y, v.z, v.w};
+    __builtin_nontemporal_store(x, (v4u*)p);
+  } else {
+    *p = v;
+  }
+}
+__device__ __forceinline__ uint4 load_row(const uint4* p) {
+  if (PGA_CACHE & 2) {
+    v4u x = __builtin_nontemporal_load((const v4u*)p);
+    return make_uint4(x[0], x[1], x[2], x[3]);
+  }
+  return *p;
+}
+
+template <int GS, int OBJ, int XOK, bool KEY>
 __global__ __launch_bounds__(kBlock) void binary_gen_pipe(GenArgs a, unsigned long long* best_parts) {
   __shared__ unsigned long long lds_red[kBlock / 64];
   __shared__ uint32_t lds_elite;
@@ -299,6 +326,7 @@ __global__ __launch_bounds__(kBlock) void binary_gen_pipe(GenArgs a, unsigned lo
     const float sc = a.score_cur[src];
     if (q == 0) {
       a.score_next[c0] = sc;
+      if (KEY) a.key_next[c0] = (uint16_t)sc;
       const unsigned long long pb = pack_best(sc, c0);
       my_best = pb > my_best ? pb : my_best;
     }
@@ -328,16 +356,28 @@ __global__ __launch_bounds__(kBlock) void binary_gen_pipe(GenArgs a, unsigned lo
 #define PGA_STAGE1(c, P)                                                   \
   {                                                                        \
     const uint64_t cc_ = (c) < a.S ? (c) : a.S - 1;                        \
-    P##w = draw(a.key, ST_CHILD, cc_, q);                                  \
+    if (PGA_ABL & kAblPoolRng) {                                           \
+      const uint32_t h_ = (uint32_t)cc_ * 0x9E3779B9u + q * 0x85EBCA6Bu;   \
+      P##w = u32x4{h_, h_ * 0xC2B2AE35u, h_ ^ 0x27D4EB2Fu, h_ * 3u};        \
+    } else {                                                               \
+      P##w = draw(a.key, ST_CHILD, cc_, q);                                \
+    }                                                                      \
     Pool<GS> pool_{P##w, gbase};                                           \
     P##i0 = word_to_index(pool_.get(W_SEL + 0, a.key, cc_), S);            \
     P##i1 = word_to_index(pool_.get(W_SEL + 1, a.key, cc_), S);            \
     P##i2 = word_to_index(pool_.get(W_SEL + 2, a.key, cc_), S);            \
     P##i3 = word_to_index(pool_.get(W_SEL + 3, a.key, cc_), S);            \
-    P##t0 = a.score_cur[P##i0];                                            \
-    P##t1 = a.score_cur[P##i1];                                            \
-    P##t2 = a.score_cur[P##i2];                                            \
-    P##t3 = a.score_cur[P##i3];                                            \
+    if (KEY) { /* exact u16 keys: L2-resident, same comparisons */        \
+      P##t0 = (float)a.key_cur[P##i0];                                     \
+      P##t1 = (float)a.key_cur[P##i1];                                     \
+      P##t2 = (float)a.key_cur[P##i2];                                     \
+      P##t3 = (float)a.key_cur[P##i3];                                     \
+    } else {                                                               \
+      P##t0 = a.score_cur[P##i0];                                          \
+      P##t1 = a.score_cur[P##i1];                                          \
+      P##t2 = a.score_cur[P##i2];                                          \
+      P##t3 = a.score_cur[P##i3];                                          \
+    }                                                                      \
   }
 
   // stage 2: tournament winners (branch-free select), crossover plan, row loads
@@ -366,8 +406,12 @@ __global__ __launch_bounds__(kBlock) void binary_gen_pipe(GenArgs a, unsigned lo
       }                                                                                     \
     }                                                                                       \
     pb_ = P##xo ? pb_ : pa_;                                                                \
-    P##A = cur[(uint64_t)pa_ * rs + qq];                                                    \
-    P##B = cur[(uint64_t)pb_ * rs + qq];                                                    \
+    if (PGA_ABL & kAblGather) {                                                             \
+      pa_ = (uint32_t)cc_;                                                                  \
+      pb_ = (uint32_t)cc_;                                                                  \
+    }                                                                                       \
+    P##A = load_row(cur + (uint64_t)pa_ * rs + qq);                                         \
+    P##B = load_row(cur + (uint64_t)pb_ * rs + qq);                                         \
   }
 
   // stage 3: crossover, mutation (own-register first draw, LDS thresholds),
@@ -376,12 +420,13 @@ __global__ __launch_bounds__(kBlock) void binary_gen_pipe(GenArgs a, unsigned lo
   if ((c) < a.S) {                                                                           \
     /* branch-free: a phi between the loaded row and the mixed row would be a   */          \
     /* register copy of an in-flight load (= s_waitcnt vmcnt(0))                 */          \
-    const uint4 mx_ = XOK == XOK_UNIFORM ? u4(draw(a.key, ST_XO, (c), q)) : range_keep_a(q, P##lo, P##hi); \
+    const uint4 mx_ = (PGA_ABL & kAblXoRng) ? make_uint4(P##w.x, P##w.y, ~P##w.x, ~P##w.y)               \
+                      : (XOK == XOK_UNIFORM ? u4(draw(a.key, ST_XO, (c), q)) : range_keep_a(q, P##lo, P##hi)); \
     const uint32_t keep_ = P##xo ? 0u : 0xFFFFFFFFu;                                         \
     const uint4 m_ = make_uint4(mx_.x | keep_, mx_.y | keep_, mx_.z | keep_, mx_.w | keep_); \
     uint4 v_ = mix4(P##A, P##B, m_);                                                         \
     if (last) v_ = and4(v_, lmask);                                                          \
-    if (bitflip) {                                                                           \
+    if (bitflip && !(PGA_ABL & kAblMut)) {                                                   \
       v_ = xor4(v_, u4(chunk_flip_mask(a, (c), q, clen, P##w.w, lds_thr)));                  \
     } else if (reset_one) {                                                                  \
       Pool<GS> pool_{P##w, gbase};                                                           \
@@ -392,12 +437,13 @@ __global__ __launch_bounds__(kBlock) void binary_gen_pipe(GenArgs a, unsigned lo
     }                                                                                        \
     BinObj<OBJ> acc_;                                                                        \
     if (have) {                                                                              \
-      nxt[(c) * rs + q] = v_;                                                                \
+      store_row(nxt + (c) * rs + q, v_);                                                     \
       acc_.add(a, v_, q);                                                                    \
     }                                                                                        \
     const float sc_ = acc_.template finish<GS>(a);                                           \
     if (q == 0) {                                                                            \
       a.score_next[(c)] = sc_;                                                               \
+      if (KEY) a.key_next[(c)] = (uint16_t)sc_;                                              \
       const unsigned long long pb_ = pack_best(sc_, (c));                                    \
       my_best = pb_ > my_best ? pb_ : my_best;                                               \
     }                                                                                        \
@@ -449,10 +495,15 @@ uint32_t launch_mode(int mode, const GenArgs& a, unsigned long long* parts, hipS
                         ((a.selection == SEL_TOURNAMENT && a.tour_k == 2) || a.selection == SEL_RANDOM) &&
                         !(a.n_elite > 1 && a.elite_idx == nullptr) && getenv_pipeline();
       if (pipe) {
-        if (a.crossover == XO_ONE_POINT || a.crossover == XO_TWO_POINT)
-          return go(binary_gen_pipe<GS, OBJ, XOK_RANGE>, a, parts, gpb, s);
-        if (a.crossover == XO_UNIFORM || a.crossover == XO_NONE)
-          return go(binary_gen_pipe<GS, OBJ, XOK_UNIFORM>, a, parts, gpb, s);
+        constexpr bool INT_OBJ = OBJ == OBJ_ONEMAX || OBJ == OBJ_LEADING_ONES || OBJ == OBJ_TRAP;
+        const bool key = INT_OBJ && a.key_cur != nullptr;
+        const bool range = a.crossover == XO_ONE_POINT || a.crossover == XO_TWO_POINT;
+        if (key) {
+          return range ? go(binary_gen_pipe<GS, OBJ, XOK_RANGE, INT_OBJ>, a, parts, gpb, s)
+                       : go(binary_gen_pipe<GS, OBJ, XOK_UNIFORM, INT_OBJ>, a, parts, gpb, s);
+        }
+        return range ? go(binary_gen_pipe<GS, OBJ, XOK_RANGE, false>, a, parts, gpb, s)
+                     : go(binary_gen_pipe<GS, OBJ, XOK_UNIFORM, false>, a, parts, gpb, s);
       }
       return go(binary_kernel<GS, OBJ, MODE_GEN>, a, parts, gpb, s);
     }

@@ -383,6 +383,13 @@ __global__ __launch_bounds__(kBlock) void scatter_rows_kernel(uint4* rows, float
   }
 }
 
+__global__ __launch_bounds__(kBlock) void scores_to_keys_kernel(const float* s, uint64_t S, uint16_t* k) {
+  for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < S; i += (uint64_t)gridDim.x * kBlock) {
+    const float v = s[i];
+    k[i] = (uint16_t)(v <= 0.f ? 0.f : (v >= 65535.f ? 65535.f : v));
+  }
+}
+
 inline size_t align_up(size_t x) { return (x + 255) & ~(size_t)255; }
 
 }  // namespace
@@ -397,6 +404,12 @@ uint32_t best_of_scores_launch(const float* scores, uint64_t S, unsigned long lo
   hipLaunchKernelGGL(best_of_scores_kernel, grid, kBlock, 0, s, scores, S, parts);
   PGA_HIP_CHECK(hipGetLastError());
   return grid;
+}
+
+void scores_to_keys_launch(const float* scores, uint64_t S, uint16_t* keys, hipStream_t s) {
+  uint32_t grid = launch_grid(S, kBlock * 4);
+  hipLaunchKernelGGL(scores_to_keys_kernel, grid, kBlock, 0, s, scores, S, keys);
+  PGA_HIP_CHECK(hipGetLastError());
 }
 
 void score_stats_launch(const float* scores, uint64_t S, float* stats, hipStream_t s) {

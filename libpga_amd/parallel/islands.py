@@ -174,8 +174,7 @@ class IslandModel:
         else:
             rows, scores = self._views(self.recv)
         victims = isl.topk(self.k, False)
-        isl.scatter(victims, rows.contiguous(), scores.contiguous())
-        isl.rebest()
+        isl.scatter(victims, rows.contiguous(), scores.contiguous())  # also refreshes best + keys
         self.migrations += 1
 
     # ----------------------------------------------------------------- run --
