@@ -1,6 +1,151 @@
+// cpu_real.cpp — CPU reference backend for the REAL encoding; mirrors
+// csrc/kernels/real.hip (same per-gene semantics from real_ops.hpp, same
+// GS-lane butterfly reductions, rotation as a k-ordered fma chain = the MFMA
+// result).  Transcendental functions differ from the device by a few ulps, so
+// REAL generations agree with the GPU to within float tolerance rather than
+// bit for bit.
+#include <algorithm>
+#include <cmath>
+#include <cstring>
 #include <stdexcept>
+#include <vector>
+
 #include "pga/cpu.hpp"
-namespace pga { namespace cpu {
-uint32_t real_run(int, const GenArgs&, unsigned long long*) { throw std::runtime_error("REAL encoding: not built yet"); }
-uint32_t perm_run(int, const GenArgs&, unsigned long long*) { throw std::runtime_error("PERMUTATION encoding: not built yet"); }
-}}
+#include "pga/real_ops.hpp"
+
+namespace pga {
+namespace cpu {
+
+static float butterfly_prod(float* v, uint32_t GS) {
+  float t[64];
+  for (uint32_t o = GS / 2; o > 0; o >>= 1) {
+    for (uint32_t q = 0; q < GS; ++q) t[q] = v[q] * v[q ^ o];
+    for (uint32_t q = 0; q < GS; ++q) v[q] = t[q];
+  }
+  return v[0];
+}
+
+uint32_t real_run(int mode, const GenArgs& a, unsigned long long* best_parts) {
+  if (a.chunks > 64) throw std::invalid_argument("REAL encoding supports at most 256 genes");
+  const uint32_t GS = group_size(a.chunks);
+  const uint64_t rw = a.row_words;
+  const float* cur = (const float*)a.cur;
+  float* nxt = (float*)a.next;
+  const uint32_t L = a.L, nchunks = a.chunks;
+  const bool gen = mode == MODE_GEN, cross = mode == MODE_CROSS, mutm = mode == MODE_MUTATE;
+  const bool evals = a.objective != OBJ_NONE && (gen || mode == MODE_INIT || mode == MODE_EVAL);
+  const bool per_gene_mut = (gen || mutm) && (a.mutation == MUT_GAUSSIAN || a.mutation == MUT_UNIFORM) && a.mut_rate > 0.f;
+  const bool reset_one = (gen || mutm) && a.mutation == MUT_RESET_ONE;
+  const bool rot = (a.obj_i & 2) && a.obj_data && real_obj_rotatable(a.objective);
+  const bool shift = (a.obj_i & 1) && a.obj_data2 && real_obj_rotatable(a.objective);
+  if (rot && L > 128) throw std::invalid_argument("rotated objectives support at most 128 dimensions");
+  const uint32_t dp = ((4 * nchunks + 15) / 16) * 16;
+  if (evals && a.objective == OBJ_USER_FNPTR)
+    throw std::invalid_argument("device function-pointer objectives need the GPU backend");
+
+  uint32_t elite0 = 0;
+  if (gen && a.n_elite > 0 && a.elite_idx == nullptr) elite0 = (uint32_t)best_index(reduce_best(a.best_cur, a.n_best_cur));
+
+  unsigned long long best = 0;
+  std::vector<float> v(4 * GS), x(std::max<uint32_t>(4 * GS, dp) + 4), z(std::max<uint32_t>(4 * GS, dp) + 4);
+  for (uint64_t child = 0; child < a.S; ++child) {
+    std::fill(v.begin(), v.end(), 0.f);
+    bool elite = false;
+    float score = 0.f;
+    if (gen && child < a.n_elite) {
+      elite = true;
+      const uint32_t src = a.elite_idx ? a.elite_idx[child] : elite0;
+      std::memcpy(v.data(), cur + (uint64_t)src * rw, 16ull * nchunks);
+      score = a.score_cur[src];
+    } else if (mode == MODE_INIT) {
+      for (uint32_t q = 0; q < nchunks; ++q) real_init_chunk(a, child, q, &v[4 * q]);
+    } else if (mode == MODE_EVAL || mutm) {
+      std::memcpy(v.data(), cur + child * rw, 16ull * nchunks);
+    }
+    if (!elite && (gen || cross || mutm)) {
+      if (gen || cross) {
+        uint32_t pa, pb;
+        select_parents(a, child, pa, pb);
+        const bool xo = a.crossover != XO_NONE && do_crossover(a, pool_word(a.key, child, W_XOPROB));
+        uint32_t blo = 0, bhi = 0;
+        float ua = 0.f;
+        if (a.crossover == XO_ONE_POINT) {
+          blo = word_to_index(pool_word(a.key, child, W_CUT1), L);
+          bhi = L;
+        } else if (a.crossover == XO_TWO_POINT) {
+          const uint32_t c1 = word_to_index(pool_word(a.key, child, W_CUT1), L);
+          const uint32_t c2 = word_to_index(pool_word(a.key, child, W_CUT2), L);
+          blo = std::min(c1, c2);
+          bhi = std::max(c1, c2);
+        } else if (a.crossover == XO_ARITHMETIC) {
+          ua = word_to_unit(pool_word(a.key, child, W_CUT1));
+        }
+        for (uint32_t q = 0; q < nchunks; ++q)
+          real_cross_chunk(a, child, q, cur + (uint64_t)pa * rw + 4 * q, cur + (uint64_t)pb * rw + 4 * q, xo, blo, bhi,
+                           ua, &v[4 * q]);
+      }
+      if (per_gene_mut) {
+        for (uint32_t q = 0; q < nchunks; ++q) {
+          const uint32_t clen = std::min(4u, L - 4 * q);
+          real_mutate_chunk(a, child, q, clen, chunk_mut_word(a.key, child, q), a.mut_thr, &v[4 * q]);
+        }
+      } else if (reset_one && pool_word(a.key, child, W_MUTIND) < a.mut_ind_thresh) {
+        const uint32_t pos = word_to_index(pool_word(a.key, child, W_MUTPOS), L);
+        v[pos] = real_reset_value(a, pool_word(a.key, child, W_SEL + sel_words(a)));
+      }
+    }
+    for (uint32_t d = L; d < 4 * nchunks; ++d) v[d] = 0.f;
+    if (mode != MODE_EVAL) std::memcpy(nxt + child * rw, v.data(), 16ull * nchunks);
+
+    if (evals && !elite) {
+      std::fill(x.begin(), x.end(), 0.f);
+      for (uint32_t d = 0; d < L; ++d) x[d] = shift ? v[d] - a.obj_data2[d] : v[d];
+      if (rot) {
+        std::fill(z.begin(), z.end(), 0.f);
+        for (uint32_t n = 0; n < L; ++n) {
+          float acc = 0.f;
+          for (uint32_t k = 0; k < dp; ++k) acc = std::fmaf(x[k], k < L ? a.obj_data[n * L + k] : 0.f, acc);
+          z[n] = acc;
+        }
+      } else {
+        z = x;
+      }
+      if (a.objective == OBJ_TSP_RANDOM_KEY) {
+        float lane[64] = {0};
+        for (uint32_t i = 0; i < L; ++i) {
+          const uint32_t ci = random_key_city(x[i], L);
+          if (i > 0) lane[i / 4] += a.obj_data[random_key_city(x[i - 1], L) * L + ci];
+          uint32_t dups = 0;
+          for (uint32_t k = 0; k < L; ++k) dups += (k != i && random_key_city(x[k], L) == ci) ? 1u : 0u;
+          lane[i / 4] += 10000.f * (float)dups;
+        }
+        score = -butterfly_sum(lane, GS);
+      } else {
+        float s0[64] = {0}, s1[64] = {0}, s2[64];
+        for (uint32_t q = 0; q < GS; ++q) s2[q] = 1.f;
+        for (uint32_t d = 0; d < L; ++d) {
+          RealAcc acc{s0[d / 4], s1[d / 4], s2[d / 4]};
+          real_obj_term(a, d, z[d], z[d + 1], v[d], acc);
+          s0[d / 4] = acc.s0;
+          s1[d / 4] = acc.s1;
+          s2[d / 4] = acc.s2;
+        }
+        RealAcc t{butterfly_sum(s0, GS), butterfly_sum(s1, GS), butterfly_prod(s2, GS)};
+        score = real_obj_finish(a, t);
+      }
+    }
+    if (evals) {
+      a.score_next[child] = score;
+      best = std::max(best, pack_best(score, child));
+    }
+  }
+  if (evals && best_parts) best_parts[0] = best;
+  return 1;
+}
+
+uint32_t perm_run(int, const GenArgs&, unsigned long long*) {
+  throw std::runtime_error("PERMUTATION encoding: not built yet");
+}
+
+}  // namespace cpu
+}  // namespace pga

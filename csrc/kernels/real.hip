@@ -1,7 +1,329 @@
-// real.hip — f32 REAL encoding (placeholder until the REAL kernels land).
+// real.hip — f32 REAL encoding on gfx950, including MFMA-batched rotated
+// objectives.
+//
+// Geometry: one individual = `chunks` 16-byte chunks of 4 genes; a group of
+// GS = group_size(chunks) lanes owns one individual (lane q holds genes
+// 4q..4q+3), GPB = 256/GS individuals per block iteration.  Genomes up to 256
+// genes (GS <= 64).  Per iteration every child's genes are also staged in an
+// LDS tile X[GPB][TW] (TW = max(4 GS, 16) + 1: the +1 breaks the 16-way bank
+// conflict of the MFMA A-operand column reads).
+//
+// Rotated objectives (CEC-style f(M (x - o)), the "MFMA batched fitness" of
+// BASELINE config 3) multiply the whole child tile by M^T with
+// v_mfma_f32_16x16x4_f32: 16 children x 16 dims per wave tile, K = 4 per
+// instruction, exact f32 (bit-for-bit a k-ordered fma chain, so the CPU
+// reference reproduces it), M staged once per block in LDS.  For the 30-D
+// Rastrigin config a block iteration is 32 children x 32 dims = 4 tiles, one
+// per wave, 8 MFMAs each.
+//
+// Reference parity: float genes, user objective via device function pointer
+// (OBJ_USER_FNPTR, include/pga.h:46 obj_f), E1 sum / E2 knapsack / E3 random-key
+// TSP objectives (test*/test.cu) are built in.
+#include <hip/hip_runtime.h>
+
+#include "pga/device.hpp"
 #include "pga/ops.hpp"
+#include "pga/real_ops.hpp"
+
 namespace pga {
-uint32_t real_launch(int, const GenArgs&, unsigned long long*, hipStream_t) {
-  throw std::runtime_error("REAL encoding: not built yet");
+namespace {
+
+using namespace dev;
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+typedef float (*obj_fn_t)(float*, unsigned);
+
+template <int GS>
+__device__ __forceinline__ float group_prod(float v) {
+#pragma unroll
+  for (int o = GS / 2; o > 0; o >>= 1) v *= __shfl_xor(v, o, 64);
+  return v;
 }
+
+struct RealGeom {
+  uint32_t tw;   // X/Z tile row stride (floats)
+  uint32_t xr;   // tile rows (>= 16 for MFMA)
+  uint32_t dp;   // padded dims for MFMA (multiple of 16)
+};
+
+__host__ __device__ inline RealGeom real_geom(uint32_t GS, uint32_t chunks) {
+  RealGeom g;
+  const uint32_t w = 4 * GS > 16 ? 4 * GS : 16;
+  g.tw = w + 1;
+  const uint32_t gpb = 256 / GS;
+  g.xr = gpb > 16 ? gpb : 16;
+  g.dp = ((4 * chunks + 15) / 16) * 16;
+  return g;
+}
+
+// dynamic LDS layout (floats): [hdr 144][X xr*tw][Z xr*tw (rotation)][M dp*(dp+1) (rotation)]
+constexpr uint32_t kHdr = 144;  // thr[128] u32 | red[4] u64 (8) | elite u32 | pad  (576 B, 16-aligned)
+
+__host__ __device__ inline size_t real_lds_floats(uint32_t GS, uint32_t chunks, bool rot) {
+  RealGeom g = real_geom(GS, chunks);
+  size_t n = kHdr + (size_t)g.xr * g.tw;
+  if (rot) n += (size_t)g.xr * g.tw + (size_t)g.dp * (g.dp + 1);
+  return n;
+}
+
+template <int GS, int MODE, bool ROT>
+__global__ __launch_bounds__(kBlock) void real_kernel(GenArgs a, unsigned long long* best_parts) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  uint32_t* lds_thr = (uint32_t*)smem;
+  unsigned long long* lds_red = (unsigned long long*)(smem + 128);
+  uint32_t* lds_elite = (uint32_t*)(smem + 136);
+  const RealGeom G = real_geom(GS, a.chunks);
+  float* X = smem + kHdr;
+  float* Z = X + G.xr * G.tw;
+  float* MS = Z + G.xr * G.tw;
+
+  const uint32_t lane = lane_id();
+  const uint32_t q = lane & (GS - 1);
+  const uint32_t gbase = lane & ~(uint32_t)(GS - 1);
+  constexpr uint32_t GPB = kBlock / GS;
+  const uint32_t g = threadIdx.x / GS;
+  const uint64_t rs = a.row_words >> 2;
+  const float4* cur = (const float4*)a.cur;
+  float4* nxt = (float4*)a.next;
+  const uint32_t L = a.L;
+  const bool have = q < a.chunks;
+  const uint32_t clen = have ? (L - 4 * q >= 4 ? 4u : L - 4 * q) : 0u;
+  constexpr bool MUTATES = MODE == MODE_GEN || MODE == MODE_MUTATE;
+  constexpr bool EVALS = MODE == MODE_GEN || MODE == MODE_INIT || MODE == MODE_EVAL;
+  const bool evals = EVALS && a.objective != OBJ_NONE;
+  const bool per_gene_mut = MUTATES && (a.mutation == MUT_GAUSSIAN || a.mutation == MUT_UNIFORM) && a.mut_rate > 0.f;
+  const bool reset_one = MUTATES && a.mutation == MUT_RESET_ONE;
+  const bool shift = (a.obj_i & 1) && a.obj_data2 && real_obj_rotatable(a.objective);
+  const bool tile_needed = ROT || a.objective == OBJ_TSP_RANDOM_KEY || a.objective == OBJ_USER_FNPTR ||
+                           a.objective == OBJ_ROSENBROCK;
+
+  // ---- per-block setup ----
+  if (MODE == MODE_GEN && a.n_elite > 0 && a.elite_idx == nullptr && blockIdx.x == 0) {
+    unsigned long long b = block_reduce_parts(a.best_cur, a.n_best_cur, lds_red);
+    if (threadIdx.x == 0) *lds_elite = (uint32_t)best_index(b);
+  }
+  if (per_gene_mut)
+    for (uint32_t i = threadIdx.x; i < kMutCap; i += kBlock) lds_thr[i] = a.mut_thr[i];
+  for (uint32_t i = threadIdx.x; i < G.xr * G.tw; i += kBlock) X[i] = 0.f;
+  if (ROT) {
+    for (uint32_t i = threadIdx.x; i < G.xr * G.tw; i += kBlock) Z[i] = 0.f;
+    for (uint32_t i = threadIdx.x; i < G.dp * (G.dp + 1); i += kBlock) {
+      const uint32_t n = i / (G.dp + 1), k = i % (G.dp + 1);
+      MS[i] = (n < L && k < L) ? a.obj_data[n * L + k] : 0.f;  // MS[n][k] = M[n][k]
+    }
+  }
+  __syncthreads();
+
+  unsigned long long my_best = 0;
+  for (uint64_t base = (uint64_t)blockIdx.x * GPB; base < a.S; base += (uint64_t)gridDim.x * GPB) {  // block-uniform
+    const uint64_t child = base + g;
+    const bool valid = child < a.S;  // group-uniform
+    float v[4] = {0.f, 0.f, 0.f, 0.f};
+    bool elite = false;
+    float score = 0.f;
+    if (valid) {
+      if (MODE == MODE_GEN && child < a.n_elite) {
+        elite = true;
+        const uint32_t src = a.elite_idx ? a.elite_idx[child] : *lds_elite;
+        if (have) {
+          const float4 e = cur[(uint64_t)src * rs + q];
+          v[0] = e.x; v[1] = e.y; v[2] = e.z; v[3] = e.w;
+        }
+        score = a.score_cur[src];
+      } else if (MODE == MODE_INIT) {
+        if (have) real_init_chunk(a, child, q, v);
+      } else if (MODE == MODE_EVAL || MODE == MODE_MUTATE) {
+        if (have) {
+          const float4 e = cur[child * rs + q];
+          v[0] = e.x; v[1] = e.y; v[2] = e.z; v[3] = e.w;
+        }
+      }
+      if (!elite && (MODE == MODE_GEN || MODE == MODE_CROSS || MODE == MODE_MUTATE)) {
+        Pool<GS> pool{draw(a.key, ST_CHILD, child, q), gbase};
+        if (MODE == MODE_GEN || MODE == MODE_CROSS) {
+          uint32_t pa, pb;
+          select_parents<GS>(a, pool, child, pa, pb);
+          const bool xo = a.crossover != XO_NONE && do_crossover(a, pool.get(W_XOPROB, a.key, child));
+          uint32_t blo = 0, bhi = 0;
+          float ua = 0.f;
+          if (a.crossover == XO_ONE_POINT) {
+            blo = word_to_index(pool.get(W_CUT1, a.key, child), L);
+            bhi = L;
+          } else if (a.crossover == XO_TWO_POINT) {
+            const uint32_t c1 = word_to_index(pool.get(W_CUT1, a.key, child), L);
+            const uint32_t c2 = word_to_index(pool.get(W_CUT2, a.key, child), L);
+            blo = c1 < c2 ? c1 : c2;
+            bhi = c1 < c2 ? c2 : c1;
+          } else if (a.crossover == XO_ARITHMETIC) {
+            ua = word_to_unit(pool.get(W_CUT1, a.key, child));
+          }
+          if (have) {
+            const float4 A4 = cur[(uint64_t)pa * rs + q], B4 = cur[(uint64_t)pb * rs + q];
+            const float A[4] = {A4.x, A4.y, A4.z, A4.w}, B[4] = {B4.x, B4.y, B4.z, B4.w};
+            real_cross_chunk(a, child, q, A, B, xo, blo, bhi, ua, v);
+          }
+        }
+        if (per_gene_mut && have) {
+          real_mutate_chunk(a, child, q, clen, pool.w.w, lds_thr, v);
+        } else if (reset_one && pool.get(W_MUTIND, a.key, child) < a.mut_ind_thresh) {
+          const uint32_t pos = word_to_index(pool.get(W_MUTPOS, a.key, child), L);
+          const float x = real_reset_value(a, pool.get(W_SEL + sel_words(a), a.key, child));
+          if ((pos >> 2) == q) {
+            const uint32_t j = pos & 3u;
+            v[0] = j == 0 ? x : v[0];
+            v[1] = j == 1 ? x : v[1];
+            v[2] = j == 2 ? x : v[2];
+            v[3] = j == 3 ? x : v[3];
+          }
+        }
+      }
+      // padding genes of the last chunk stay zero
+      for (uint32_t j = clen; j < 4; ++j) v[j] = 0.f;
+      if (MODE != MODE_EVAL && have) nxt[child * rs + q] = make_float4(v[0], v[1], v[2], v[3]);
+    }
+
+    if (evals) {
+      // x (shifted) -> LDS tile row
+      float x[4];
+      for (int j = 0; j < 4; ++j) {
+        const uint32_t d = 4 * q + j;
+        x[j] = (shift && d < L) ? v[j] - a.obj_data2[d] : v[j];
+        if (d >= L) x[j] = 0.f;
+      }
+      if (tile_needed) {
+        float* row = X + g * G.tw + 4 * q;
+        row[0] = x[0]; row[1] = x[1]; row[2] = x[2]; row[3] = x[3];
+      }
+      float z[4] = {x[0], x[1], x[2], x[3]};
+      if (ROT) {
+        __syncthreads();
+        // Z = X M^T on MFMA: tile (rt, ct) = rows 16rt.., dims 16ct..; B[k][n] = M[n][k]
+        const uint32_t w = threadIdx.x >> 6;
+        const uint32_t nrt = (GPB + 15) / 16, nct = G.dp / 16;
+        for (uint32_t t = w; t < nrt * nct; t += kBlock / 64) {
+          const uint32_t rt = t / nct, ct = t % nct;
+          floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+          const float* xa = X + (rt * 16 + (lane & 15)) * G.tw + (lane >> 4);
+          const float* mb = MS + (ct * 16 + (lane & 15)) * (G.dp + 1) + (lane >> 4);
+          for (uint32_t k0 = 0; k0 < G.dp; k0 += 4)
+            acc = __builtin_amdgcn_mfma_f32_16x16x4f32(xa[k0], mb[k0], acc, 0, 0, 0);
+          float* zo = Z + (rt * 16 + (lane >> 4) * 4) * G.tw + ct * 16 + (lane & 15);
+          zo[0] = acc[0];
+          zo[G.tw] = acc[1];
+          zo[2 * G.tw] = acc[2];
+          zo[3 * G.tw] = acc[3];
+        }
+        __syncthreads();
+        const float* zr = Z + g * G.tw + 4 * q;
+        z[0] = zr[0]; z[1] = zr[1]; z[2] = zr[2]; z[3] = zr[3];
+      } else if (tile_needed) {
+        __syncthreads();
+      }
+      if (valid && !elite) {
+        if (a.objective == OBJ_USER_FNPTR) {
+          // reference ABI: obj_f(gene*, unsigned) on the child's genome (LDS row)
+          float s = 0.f;
+          if (q == 0) s = ((obj_fn_t)a.user_fn)(X + g * G.tw, L);
+          score = __shfl(s, (int)gbase, 64);
+        } else if (a.objective == OBJ_TSP_RANDOM_KEY) {
+          // reference E3: path over consecutive decoded cities + 10000 per duplicate pair
+          const float* row = X + g * G.tw;
+          float len = 0.f;
+          for (uint32_t j = 0; j < 4; ++j) {
+            const uint32_t i = 4 * q + j;
+            if (i >= L) break;
+            const uint32_t ci = random_key_city(row[i], L);
+            if (i > 0) len += a.obj_data[random_key_city(row[i - 1], L) * L + ci];
+            uint32_t dups = 0;
+            for (uint32_t k = 0; k < L; ++k) dups += (k != i && random_key_city(row[k], L) == ci) ? 1u : 0u;
+            len += 10000.f * (float)dups;
+          }
+          score = -group_sum<GS>(len);
+        } else {
+          RealAcc acc{0.f, 0.f, 1.f};
+          const float* zrow = (ROT ? Z : X) + g * G.tw + 4 * q;
+          for (uint32_t j = 0; j < 4; ++j) {
+            const uint32_t d = 4 * q + j;
+            if (d < L) {
+              const float zn = (j < 3) ? z[j + 1] : zrow[4];
+              real_obj_term(a, d, z[j], zn, v[j], acc);
+            }
+          }
+          acc.s0 = group_sum<GS>(acc.s0);
+          acc.s1 = group_sum<GS>(acc.s1);
+          acc.s2 = group_prod<GS>(acc.s2);
+          score = real_obj_finish(a, acc);
+        }
+      }
+      if (valid && q == 0) {
+        a.score_next[child] = score;
+        const unsigned long long pb = pack_best(score, child);
+        my_best = pb > my_best ? pb : my_best;
+      }
+      if (tile_needed) __syncthreads();  // tiles are rewritten next iteration
+    }
+  }
+  if (evals && best_parts) {
+    unsigned long long b = block_max_u64(my_best, lds_red);
+    if (threadIdx.x == 0) best_parts[blockIdx.x] = b;
+  }
+}
+
+template <int GS, int MODE, bool ROT>
+uint32_t go(const GenArgs& a, unsigned long long* parts, hipStream_t s) {
+  const size_t lds = real_lds_floats(GS, a.chunks, ROT) * sizeof(float);
+  auto k = real_kernel<GS, MODE, ROT>;
+  static bool configured = false;  // one per instantiation
+  if (!configured) {
+    PGA_HIP_CHECK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    configured = true;
+  }
+  const uint32_t gpb = kBlock / GS;
+  uint64_t need = (a.S + gpb - 1) / gpb;
+  int per_cu = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)k, kBlock, lds) != hipSuccess || per_cu <= 0)
+    per_cu = 1;
+  uint64_t cap = (uint64_t)device_cu_count() * per_cu;
+  if (cap > kMaxGrid) cap = kMaxGrid;
+  const uint32_t grid = (uint32_t)(need < cap ? need : cap);
+  hipLaunchKernelGGL(k, grid, kBlock, lds, s, a, parts);
+  return grid;
+}
+
+template <int GS, bool ROT>
+uint32_t launch_mode(int mode, const GenArgs& a, unsigned long long* parts, hipStream_t s) {
+  switch (mode) {
+    case MODE_GEN: return go<GS, MODE_GEN, ROT>(a, parts, s);
+    case MODE_INIT: return go<GS, MODE_INIT, ROT>(a, parts, s);
+    case MODE_EVAL: return go<GS, MODE_EVAL, ROT>(a, parts, s);
+    case MODE_CROSS: return go<GS, MODE_CROSS, false>(a, parts, s);
+    default: return go<GS, MODE_MUTATE, false>(a, parts, s);
+  }
+}
+
+template <int GS>
+uint32_t launch_rot(int mode, const GenArgs& a, unsigned long long* parts, hipStream_t s) {
+  const bool rot = (a.obj_i & 2) && a.obj_data && real_obj_rotatable(a.objective);
+  return rot ? launch_mode<GS, true>(mode, a, parts, s) : launch_mode<GS, false>(mode, a, parts, s);
+}
+
+}  // namespace
+
+uint32_t real_launch(int mode, const GenArgs& a, unsigned long long* best_parts, hipStream_t s) {
+  if (a.chunks > 64) throw std::invalid_argument("REAL encoding supports at most 256 genes");
+  const bool rot = (a.obj_i & 2) && real_obj_rotatable(a.objective);
+  if (rot && a.L > 128) throw std::invalid_argument("rotated objectives support at most 128 dimensions");
+  uint32_t grid = 0;
+  switch (group_size(a.chunks)) {
+    case 1: grid = launch_rot<1>(mode, a, best_parts, s); break;
+    case 2: grid = launch_rot<2>(mode, a, best_parts, s); break;
+    case 4: grid = launch_rot<4>(mode, a, best_parts, s); break;
+    case 8: grid = launch_rot<8>(mode, a, best_parts, s); break;
+    case 16: grid = launch_rot<16>(mode, a, best_parts, s); break;
+    case 32: grid = launch_rot<32>(mode, a, best_parts, s); break;
+    default: grid = launch_rot<64>(mode, a, best_parts, s); break;
+  }
+  PGA_HIP_CHECK(hipGetLastError());
+  return grid;
+}
+
 }  // namespace pga

@@ -1,0 +1,103 @@
+"""REAL encoding: CPU reference vs torch oracle (CPU) and gfx950 kernels vs
+CPU reference / torch oracle (GPU, incl. the MFMA rotated objectives)."""
+import pytest
+import torch
+
+import libpga_amd as pga
+
+M = pga.models
+
+PROBLEMS = {
+    "sphere": lambda: M.Sphere(30),
+    "rastrigin": lambda: M.Rastrigin(30),
+    "rastrigin_rot": lambda: M.Rastrigin(30, rotate=True, shift=True, seed=3),
+    "rosenbrock": lambda: M.Rosenbrock(17),
+    "rosenbrock_rot": lambda: M.Rosenbrock(64, rotate=True, seed=1),
+    "ackley": lambda: M.Ackley(20),
+    "griewank": lambda: M.Griewank(9),
+    "schwefel": lambda: M.Schwefel(12, rotate=True),
+    "sum": lambda: M.SumGenes(100),
+    "knap": lambda: M.ReferenceKnapsack(),
+    "tsp_rk": lambda: M.RandomKeyTSP.planted(40),
+    "sphere_d3": lambda: M.Sphere(3, rotate=True),
+    "sphere_d128": lambda: M.Sphere(128, rotate=True),
+}
+
+
+def close(a, b, rel=2e-4, abs_=2e-3):
+    return torch.allclose(a, b, rtol=rel, atol=abs_)
+
+
+@pytest.mark.parametrize("name", list(PROBLEMS))
+def test_cpu_scores_match_oracle(name):
+    p = PROBLEMS[name]()
+    ga = pga.GeneticAlgorithm(p, 200, seed=5, device="cpu", elitism=2)
+    assert close(p.reference_fitness(ga.genomes()), ga.scores)
+    ga.run(5)
+    assert close(p.reference_fitness(ga.genomes()), ga.scores)
+    g = ga.genomes()
+    tol = 1e-5 * max(abs(p.lo), abs(p.hi), 1.0)
+    assert float(g.min()) >= p.lo - tol and float(g.max()) <= p.hi + tol
+
+
+@pytest.mark.parametrize("xo", ["uniform", "blend", "arithmetic", "one_point", "two_point"])
+@pytest.mark.parametrize("mut", ["gaussian", "uniform", "reset_one"])
+def test_cpu_operators(xo, mut):
+    p = M.Sphere(24)
+    ga = pga.GeneticAlgorithm(p, 300, seed=1, device="cpu", crossover=xo, mutation=mut, elitism=1)
+    s0 = ga.best_score()
+    ga.run(25)
+    assert ga.best_score() >= s0
+    assert close(p.reference_fitness(ga.genomes()), ga.scores)
+
+
+def test_reference_knapsack_optimum():
+    """Reference E2 expects 285 = items 2 and 3 (test2/test.cu)."""
+    p = M.ReferenceKnapsack()
+    ga = pga.GeneticAlgorithm(p, 100, seed=2, device="cpu")
+    ga.run(5)
+    s, g = ga.best()
+    assert s == 285.0
+    assert p.counts(g.unsqueeze(0))[0].tolist() == [0, 0, 1, 1, 0, 0]
+
+
+def test_sum_genes_improves():
+    ga = pga.GeneticAlgorithm(M.SumGenes(100), 4000, seed=2, device="cpu")
+    s0 = ga.best_score()
+    ga.run(30)
+    assert ga.best_score() > s0 + 10
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", list(PROBLEMS))
+def test_gpu_matches_cpu(name):
+    p = PROBLEMS[name]()
+    g = pga.GeneticAlgorithm(p, 1000, seed=9, device="cuda:0", elitism=1)
+    c = pga.GeneticAlgorithm(p, 1000, seed=9, device="cpu", elitism=1)
+    torch.cuda.synchronize()
+    assert torch.equal(g.rows.cpu(), c.rows), "init rows differ"
+    assert close(g.scores.cpu(), c.scores)
+    assert close(p.reference_fitness(g.genomes().cpu()), g.scores.cpu())
+    # one generation from the SAME population: selection identical unless two
+    # scores are within an ulp; compare children gene-wise with tolerance
+    g.run(1)
+    c.run(1)
+    torch.cuda.synchronize()
+    gg, cg = g.genomes().cpu(), c.genomes()
+    same_rows = torch.isclose(gg, cg, rtol=1e-4, atol=1e-4).all(-1).float().mean().item()
+    assert same_rows > 0.99
+    assert close(p.reference_fitness(gg), g.scores.cpu())
+
+
+@pytest.mark.gpu
+def test_gpu_rastrigin30_rotated_mfma_1m():
+    """BASELINE config 3 shape: Rastrigin-30D rotated, pop = 1M, MFMA scores."""
+    p = M.Rastrigin(30, rotate=True, shift=True, seed=4)
+    ga = pga.GeneticAlgorithm(p, 1 << 20, seed=1, device="cuda:0", elitism=1)
+    b0 = ga.best_score()
+    ga.run(20)
+    torch.cuda.synchronize()
+    idx = torch.randint(0, 1 << 20, (4096,), device="cuda:0")
+    ref = p.reference_fitness(ga.genomes()[idx])
+    assert close(ref, ga.scores[idx], rel=1e-4, abs_=5e-3)
+    assert ga.best_score() > b0
