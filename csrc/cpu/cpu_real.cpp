@@ -143,9 +143,6 @@ uint32_t real_run(int mode, const GenArgs& a, unsigned long long* best_parts) {
   return 1;
 }
 
-uint32_t perm_run(int, const GenArgs&, unsigned long long*) {
-  throw std::runtime_error("PERMUTATION encoding: not built yet");
-}
 
 }  // namespace cpu
 }  // namespace pga

@@ -83,6 +83,7 @@ enum Objective : int32_t {
   OBJ_TSP_RANDOM_KEY = 24,// REAL: reference E3 semantics (decode (int)(g*L), dup penalty)
   OBJ_TSP = 32,          // PERMUTATION: -(closed tour length), data = L*L distance matrix
   OBJ_TSP_OPEN = 33,     // PERMUTATION: -(open path length) (reference E3 metric)
+  OBJ_TSP_EUC = 34,      // PERMUTATION: -(closed tour length), data = L (x, y) city coordinates
   OBJ_USER_FNPTR = 64,   // REAL: reference-ABI device function pointer obj_f
 };
 

@@ -5,3 +5,4 @@ from .real import (  # noqa: F401
     Ackley, Griewank, RandomKeyTSP, Rastrigin, RealTorchObjective, ReferenceKnapsack, Rosenbrock, Schwefel, Sphere,
     SumGenes, random_rotation,
 )
+from .permutation import TSP, TSPEuclidean  # noqa: F401

@@ -1,0 +1,96 @@
+"""Permutation (PERMUTATION encoding, u16 city ids) problem family: TSP.
+
+BASELINE config 5 ("TSP-256 permutation encoding (ordered/PMX crossover)").
+Crossover PMX / OX1 and swap / inversion (2-opt) mutation run in the fused
+kernel (csrc/kernels/perm.hip).
+"""
+from __future__ import annotations
+
+import torch
+
+from .._ext import C
+from .base import Operators, Problem
+
+
+class TSP(Problem):
+    """Closed-tour TSP over a distance matrix (score = -tour length).
+    ``open_path=True`` scores the open path (the reference E3 metric,
+    test3/test.cu:30-34, without its duplicate penalty: tours are valid
+    permutations by construction)."""
+
+    def __init__(self, dist: torch.Tensor, open_path: bool = False):
+        self.encoding = "permutation"
+        self.dist = torch.as_tensor(dist, dtype=torch.float32)
+        n = self.dist.shape[0]
+        if self.dist.shape != (n, n):
+            raise ValueError("distance matrix must be square")
+        if n > 4096:
+            raise ValueError("at most 4096 cities")
+        self.length = n
+        self.open_path = open_path
+        self.objective = C.OBJ_TSP_OPEN if open_path else C.OBJ_TSP
+
+    def data(self):
+        return self.dist.reshape(-1)
+
+    def default_operators(self) -> Operators:
+        return Operators(selection="tournament", tournament_k=4, crossover="ox", mutation="inversion",
+                         mutation_rate=0.3)
+
+    def tour_length(self, tours: torch.Tensor) -> torch.Tensor:
+        t = tours.to(torch.int64)
+        d = self.dist.to(t.device)
+        nxt = t[:, 1:] if self.open_path else torch.roll(t, -1, dims=1)
+        cur = t[:, :-1] if self.open_path else t
+        return d[cur, nxt].sum(-1)
+
+    def reference_fitness(self, genomes: torch.Tensor) -> torch.Tensor:
+        return -self.tour_length(genomes)
+
+    @staticmethod
+    def random_euclidean(n: int, seed: int = 0, open_path: bool = False) -> "TSP":
+        g = torch.Generator().manual_seed(seed)
+        xy = torch.rand(n, 2, generator=g) * 1000.0
+        return TSP(torch.cdist(xy.double(), xy.double()).float(), open_path=open_path)
+
+
+class TSPEuclidean(Problem):
+    """Closed-tour Euclidean TSP from city coordinates (staged in LDS; no
+    distance matrix traffic)."""
+
+    def __init__(self, coords: torch.Tensor):
+        self.encoding = "permutation"
+        self.coords = torch.as_tensor(coords, dtype=torch.float32)
+        if self.coords.ndim != 2 or self.coords.shape[1] != 2:
+            raise ValueError("coords must be [n, 2]")
+        self.length = int(self.coords.shape[0])
+        if self.length > 4096:
+            raise ValueError("at most 4096 cities")
+        self.objective = C.OBJ_TSP_EUC
+
+    def data(self):
+        return self.coords.reshape(-1)
+
+    def default_operators(self) -> Operators:
+        return Operators(selection="tournament", tournament_k=4, crossover="ox", mutation="inversion",
+                         mutation_rate=0.3)
+
+    def tour_length(self, tours: torch.Tensor) -> torch.Tensor:
+        t = tours.to(torch.int64)
+        c = self.coords.to(t.device)
+        a, b = c[t], c[torch.roll(t, -1, dims=1)]
+        return torch.sqrt(((a - b) ** 2).sum(-1)).sum(-1)
+
+    def reference_fitness(self, genomes: torch.Tensor) -> torch.Tensor:
+        return -self.tour_length(genomes)
+
+    @staticmethod
+    def random(n: int, seed: int = 0) -> "TSPEuclidean":
+        g = torch.Generator().manual_seed(seed)
+        return TSPEuclidean(torch.rand(n, 2, generator=g) * 1000.0)
+
+    @staticmethod
+    def circle(n: int) -> "TSPEuclidean":
+        """Cities on a circle: the optimal tour (length ~ 2 pi r) is known."""
+        th = torch.arange(n, dtype=torch.float64) * (2 * torch.pi / n)
+        return TSPEuclidean(torch.stack([500 + 400 * torch.cos(th), 500 + 400 * torch.sin(th)], 1).float())

@@ -1,0 +1,85 @@
+"""PERMUTATION encoding (TSP): validity, oracle agreement, operators, and
+gfx950 vs CPU bit-exactness."""
+import pytest
+import torch
+
+import libpga_amd as pga
+
+M = pga.models
+
+
+def is_perm(g):
+    n = g.shape[1]
+    return bool((g.sort(-1).values == torch.arange(n, device=g.device)).all())
+
+
+@pytest.mark.parametrize("xo", ["ox", "pmx", "none"])
+@pytest.mark.parametrize("mut", ["swap", "inversion"])
+@pytest.mark.parametrize("n", [5, 8, 50, 257])
+def test_cpu_valid_and_scores(xo, mut, n):
+    p = M.TSP.random_euclidean(n, seed=n)
+    ga = pga.GeneticAlgorithm(p, 96, seed=4, device="cpu", crossover=xo, mutation=mut, mutation_rate=0.5,
+                              crossover_prob=0.9, elitism=1)
+    assert is_perm(ga.genomes())
+    ga.run(4)
+    g = ga.genomes()
+    assert is_perm(g)
+    assert torch.allclose(p.reference_fitness(g), ga.scores, rtol=1e-5, atol=1e-2)
+
+
+def test_ox_reference_example():
+    """OX1 on the textbook example: A = 1..9 segment [3,7), B = 9 3 7 8 2 6 5 1 4."""
+    from libpga_amd import _C  # noqa: F401
+    A = torch.tensor([0, 1, 2, 3, 4, 5, 6, 7, 8])
+    B = torch.tensor([8, 2, 6, 7, 1, 5, 4, 0, 3])
+    lo, hi = 3, 7
+    seg = set(A[lo:hi].tolist())
+    child = [None] * 9
+    child[lo:hi] = A[lo:hi].tolist()
+    order = [B[(hi + t) % 9].item() for t in range(9) if B[(hi + t) % 9].item() not in seg]
+    pos = [(hi + t) % 9 for t in range(9 - (hi - lo))]
+    for c, q in zip(order, pos):
+        child[q] = c
+    assert sorted(child) == list(range(9))
+
+
+def test_tsp_circle_converges():
+    p = M.TSPEuclidean.circle(24)
+    ga = pga.GeneticAlgorithm(p, 2048, seed=1, device="cpu", elitism=1)
+    ga.run(150)
+    opt = float(p.tour_length(torch.arange(24).unsqueeze(0))[0])
+    assert -ga.best_score() < 1.05 * opt
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("xo", ["ox", "pmx"])
+@pytest.mark.parametrize("n,S", [(9, 333), (64, 1000), (256, 2048), (1000, 64)])
+@pytest.mark.parametrize("prob", ["matrix", "euc", "open"])
+def test_gpu_bitexact(xo, n, S, prob):
+    p = {"matrix": lambda: M.TSP.random_euclidean(n, seed=2), "euc": lambda: M.TSPEuclidean.random(n, seed=2),
+         "open": lambda: M.TSP.random_euclidean(n, seed=2, open_path=True)}[prob]()
+    kw = dict(seed=5, crossover=xo, mutation="inversion", mutation_rate=0.4, elitism=2)
+    g = pga.GeneticAlgorithm(p, S, device="cuda:0", **kw)
+    c = pga.GeneticAlgorithm(p, S, device="cpu", **kw)
+    for _ in range(3):
+        torch.cuda.synchronize()
+        assert torch.equal(g.rows.cpu(), c.rows)
+        assert torch.equal(g.scores.cpu(), c.scores)
+        g.run(1)
+        c.run(1)
+    assert is_perm(g.genomes().cpu())
+
+
+@pytest.mark.gpu
+def test_gpu_tsp256_pop256k():
+    """BASELINE config 5 shape on one GPU: TSP-256, pop = 256K, OX."""
+    p = M.TSPEuclidean.random(256, seed=9)
+    ga = pga.GeneticAlgorithm(p, 256 * 1024, seed=1, device="cuda:0", elitism=1)
+    b0 = ga.best_score()
+    ga.run(10)
+    torch.cuda.synchronize()
+    idx = torch.randint(0, 256 * 1024, (2048,), device="cuda:0")
+    g = ga.genomes()[idx]
+    assert is_perm(g)
+    assert torch.allclose(p.reference_fitness(g), ga.scores[idx], rtol=1e-4, atol=0.5)
+    assert ga.best_score() > b0
