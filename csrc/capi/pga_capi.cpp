@@ -1,0 +1,705 @@
+// pga_capi.cpp — the C API (include/pga.h, include/pga_ext.h) on top of the
+// native Island runtime.
+//
+// Reference: include/pga.h:17-156 and src/pga.cu:148-395.  Parity notes:
+//   * pga_create_population: NULL at MAX_POPULATIONS or genome_len < 4
+//     (src/pga.cu:180-186); genes U(0, 1].
+//   * pga_run evolves population 0 only (src/pga.cu:376-391); one fused
+//     generation kernel per generation instead of fill_rand + 3 stage
+//     kernels x ceil(S/512) launches + 3 device syncs.
+//   * pga_get_best prints the best score with "%f\n" (src/pga.cu:230) unless
+//     pga_set_quiet(p, 1), and returns a malloc'd copy the caller frees.
+//   * NULL mutate / crossover restore the built-in defaults (the header says
+//     so, include/pga.h:74-85; the original stored NULL).
+//   * The stubs of the original (pga_get_best_top*, pga_get_best_all,
+//     pga_migrate*, pga_run_islands, src/pga.cu:238-248, :368-374, :393-395)
+//     are implemented.
+//   * Errors: print + exit(1) by default, like the original's gpuAssert
+//     (src/pga.cu:25-33); pga_set_abort_on_error(p, 0) records them for
+//     pga_last_error() instead.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <ctime>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "pga.h"
+#include "pga/comm.hpp"
+#include "pga/island.hpp"
+#include "pga/ops.hpp"
+#include "pga_ext.h"
+
+struct pga_population {
+  std::unique_ptr<pga::Island> isl;
+  pga_t* owner = nullptr;
+  int builtin = -1;  // built-in objective id, -1: the pga-level obj_f callback
+};
+
+struct pga_solver {
+  int device = 0;
+  uint64_t seed = 0;
+  bool quiet = false;
+  bool abort_on_error = true;
+  std::vector<population_t*> pops;
+  obj_f objective = nullptr;
+  mutate_f mutate = nullptr;
+  crossover_f crossover = nullptr;
+  hipStream_t stream = nullptr;
+  uint32_t migration_epoch = 0;
+  pga::RcclComm* comm = nullptr;
+  void* mig_send = nullptr;
+  void* mig_recv = nullptr;
+  size_t mig_bytes = 0;
+};
+
+namespace {
+
+thread_local std::string g_last_error;
+
+void fail(pga_t* p, const char* what) {
+  g_last_error = what;
+  if (!p || p->abort_on_error) {
+    std::fprintf(stderr, "pga error: %s\n", what);
+    std::exit(1);
+  }
+}
+
+template <typename F>
+void guard(pga_t* p, F&& f) {
+  try {
+    f();
+  } catch (const std::exception& e) {
+    fail(p, e.what());
+  }
+}
+template <typename R, typename F>
+R guard_r(pga_t* p, R bad, F&& f) {
+  try {
+    return f();
+  } catch (const std::exception& e) {
+    fail(p, e.what());
+    return bad;
+  }
+}
+
+bool valid_pop(pga_t* p, population_t* pop) {
+  return p && pop && pop->owner == p && std::find(p->pops.begin(), p->pops.end(), pop) != p->pops.end();
+}
+
+// push the current callbacks / built-in objective into a population
+void sync_callbacks(pga_t* p, population_t* pop) {
+  pga::Island& isl = *pop->isl;
+  pga::Config c = isl.config();
+  if (pop->builtin < 0) {
+    c.objective = p->objective ? pga::OBJ_USER_FNPTR : pga::OBJ_NONE;
+    isl.set_user_fn((void*)p->objective);
+    if (c.encoding == pga::ENC_REAL) isl.set_user_operators((void*)p->crossover, (void*)p->mutate);
+  }
+  isl.set_operators(c);
+  isl.stream = p->stream;
+}
+
+float fraction(float pct) { return pct > 1.f ? pct / 100.f : pct; }
+
+uint32_t migrants(uint64_t from_S, uint64_t to_S, float pct) {
+  const double f = fraction(pct);
+  if (f <= 0) return 0;
+  uint64_t k = (uint64_t)std::llround(f * (double)from_S);
+  k = std::max<uint64_t>(k, 1);
+  k = std::min<uint64_t>(k, std::min(from_S, to_S) / 2 ? std::min(from_S, to_S) / 2 : 1);
+  return (uint32_t)k;
+}
+
+// row -> float genes (BINARY: one float per bit, PERMUTATION: city ids)
+gene* decode_row(const pga::Island& isl, const std::vector<uint32_t>& row) {
+  const uint32_t L = isl.config().L;
+  gene* g = (gene*)std::malloc(sizeof(gene) * L);
+  if (!g) throw std::bad_alloc();
+  switch (isl.config().encoding) {
+    case pga::ENC_REAL: std::memcpy(g, row.data(), sizeof(float) * L); break;
+    case pga::ENC_BINARY:
+      for (uint32_t i = 0; i < L; ++i) g[i] = (float)((row[i / 32] >> (i % 32)) & 1u);
+      break;
+    default: {
+      const uint16_t* h = (const uint16_t*)row.data();
+      for (uint32_t i = 0; i < L; ++i) g[i] = (float)h[i];
+    }
+  }
+  return g;
+}
+
+void* dev_alloc(pga::Island& isl, size_t bytes) {
+  void* ptr = nullptr;
+  if (isl.on_gpu()) PGA_HIP_CHECK(hipMalloc(&ptr, bytes));
+  else ptr = std::malloc(bytes);
+  if (!ptr) throw std::bad_alloc();
+  return ptr;
+}
+void dev_free(pga::Island& isl, void* ptr) {
+  if (!ptr) return;
+  if (isl.on_gpu()) (void)hipFree(ptr);
+  else std::free(ptr);
+}
+
+struct Emigrants {
+  uint32_t k = 0;
+  void* rows = nullptr;
+  float* scores = nullptr;
+};
+
+Emigrants take_best(pga::Island& isl, uint32_t k) {
+  Emigrants e;
+  e.k = k;
+  uint32_t* idx = (uint32_t*)dev_alloc(isl, 4ull * k);
+  e.rows = dev_alloc(isl, isl.row_bytes() * k);
+  e.scores = (float*)dev_alloc(isl, 4ull * k);
+  isl.topk(k, true, idx);
+  isl.gather(idx, k, e.rows, e.scores);
+  isl.synchronize();
+  dev_free(isl, idx);
+  return e;
+}
+
+void replace_worst(pga::Island& isl, Emigrants& e) {
+  uint32_t* idx = (uint32_t*)dev_alloc(isl, 4ull * e.k);
+  isl.topk(e.k, false, idx);
+  isl.scatter(idx, e.k, e.rows, e.scores);
+  isl.synchronize();
+  dev_free(isl, idx);
+}
+
+void free_emigrants(pga::Island& isl, Emigrants& e) {
+  dev_free(isl, e.rows);
+  dev_free(isl, e.scores);
+  e = Emigrants();
+}
+
+int default_device() {
+  const char* e = std::getenv("PGA_DEVICE");
+  if (e && *e) return std::atoi(e);
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return -1;
+  return 0;
+}
+
+uint64_t default_seed() {
+  const char* e = std::getenv("PGA_SEED");
+  if (e && *e) return std::strtoull(e, nullptr, 10);
+  return (uint64_t)std::time(nullptr);  // reference: time(NULL) (src/pga.cu:154)
+}
+
+population_t* create(pga_t* p, unsigned long size, unsigned genome_len, int encoding) {
+  if (!p) return nullptr;
+  if (p->pops.size() >= MAX_POPULATIONS) return nullptr;
+  if (genome_len < 4 || size == 0) return nullptr;
+  return guard_r<population_t*>(p, nullptr, [&]() -> population_t* {
+    pga::Config c;
+    c.encoding = encoding;
+    c.S = size;
+    c.L = genome_len;
+    c.seed = p->seed;
+    c.island = (uint32_t)p->pops.size();
+    c.objective = pga::OBJ_NONE;
+    c.selection = pga::SEL_TOURNAMENT;
+    c.tour_k = 2;
+    if (encoding == pga::ENC_REAL) {  // reference semantics
+      c.lo = 0.f;
+      c.hi = 1.f;
+      c.crossover = pga::XO_UNIFORM;
+      c.mutation = pga::MUT_RESET_ONE;
+      c.mut_rate = 0.01f;
+    } else if (encoding == pga::ENC_BINARY) {
+      c.crossover = pga::XO_UNIFORM;
+      c.mutation = pga::MUT_BIT_FLIP;
+    } else {
+      c.crossover = pga::XO_OX;
+      c.mutation = pga::MUT_INVERSION;
+      c.mut_rate = 0.3f;
+      c.tour_k = 4;
+    }
+    auto pop = std::make_unique<pga_population>();
+    pop->owner = p;
+    pop->isl = std::make_unique<pga::Island>(c, p->device);
+    pop->isl->stream = p->stream;
+    pop->isl->initialize();
+    population_t* raw = pop.release();
+    p->pops.push_back(raw);
+    return raw;
+  });
+}
+
+}  // namespace
+
+extern "C" {
+
+// ------------------------------------------------------------------ lifetime
+pga_t* pga_init_device(int device) {
+  pga_t* p = new (std::nothrow) pga_solver;
+  if (!p) return nullptr;
+  p->device = device;
+  p->seed = default_seed();
+  if (device >= 0) {
+    if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&p->stream, hipStreamNonBlocking) != hipSuccess) {
+      g_last_error = "cannot initialise the GPU";
+      delete p;
+      return nullptr;
+    }
+  }
+  return p;
+}
+
+pga_t* pga_init(void) { return pga_init_device(default_device()); }
+
+void pga_deinit(pga_t* p) {
+  if (!p) return;
+  for (population_t* pop : p->pops) {
+    if (p->mig_send) {
+      dev_free(*pop->isl, p->mig_send);
+      dev_free(*pop->isl, p->mig_recv);
+      p->mig_send = p->mig_recv = nullptr;
+    }
+    delete pop;
+  }
+  p->pops.clear();
+  if (p->comm) pga::rccl_destroy(p->comm);
+  if (p->stream) (void)hipStreamDestroy(p->stream);
+  delete p;
+}
+
+void pga_set_seed(pga_t* p, uint64_t seed) {
+  if (p) p->seed = seed;
+}
+void pga_set_quiet(pga_t* p, int quiet) {
+  if (p) p->quiet = quiet != 0;
+}
+void pga_set_abort_on_error(pga_t* p, int a) {
+  if (p) p->abort_on_error = a != 0;
+}
+const char* pga_last_error(void) { return g_last_error.c_str(); }
+
+// --------------------------------------------------------------- populations
+population_t* pga_create_population(pga_t* p, unsigned long size, unsigned genome_len, enum population_type type) {
+  if (type != RANDOM_POPULATION) return nullptr;
+  return create(p, size, genome_len, pga::ENC_REAL);
+}
+
+population_t* pga_create_population_ext(pga_t* p, unsigned long size, unsigned genome_len, enum pga_encoding e) {
+  if (e != PGA_BINARY && e != PGA_REAL && e != PGA_PERMUTATION) return nullptr;
+  if (genome_len == 0 || size == 0 || !p || p->pops.size() >= MAX_POPULATIONS) return nullptr;
+  return create(p, size, genome_len < 4 && e == PGA_REAL ? 4 : genome_len, (int)e);
+}
+
+void pga_set_objective_function(pga_t* p, obj_f f) {
+  if (p) p->objective = f;
+}
+void pga_set_mutate_function(pga_t* p, mutate_f f) {
+  if (p) p->mutate = f;
+}
+void pga_set_crossover_function(pga_t* p, crossover_f f) {
+  if (p) p->crossover = f;
+}
+
+int pga_set_objective_builtin(pga_t* p, population_t* pop, enum pga_objective obj, const float* data, size_t n,
+                              const float* data2, size_t n2, int iparam, float f0, float f1) {
+  if (!valid_pop(p, pop)) return -1;
+  return guard_r<int>(p, -1, [&]() {
+    pga::Island& isl = *pop->isl;
+    isl.stream = p->stream;
+    if (data) isl.set_objective_data(data, n, 0);
+    if (data2) isl.set_objective_data(data2, n2, 1);
+    pga::Config c = isl.config();
+    c.objective = (int32_t)obj;
+    c.obj_i = iparam;
+    c.obj_f0 = f0;
+    c.obj_f1 = f1;
+    isl.set_operators(c);
+    pop->builtin = (int)obj;
+    return 0;
+  });
+}
+
+int pga_set_operators(pga_t* p, population_t* pop, enum pga_selection sel, unsigned k, enum pga_crossover xo,
+                      float xo_prob, enum pga_mutation mut, float rate, float sigma, unsigned elitism) {
+  if (!valid_pop(p, pop)) return -1;
+  return guard_r<int>(p, -1, [&]() {
+    pga::Config c = pop->isl->config();
+    c.selection = (int32_t)sel;
+    c.tour_k = k ? k : 2;
+    c.crossover = (int32_t)xo;
+    c.xo_prob = xo_prob;
+    c.mutation = (int32_t)mut;
+    c.mut_rate = rate;
+    c.sigma = sigma;
+    c.n_elite = elitism;
+    pop->isl->stream = p->stream;
+    pop->isl->set_operators(c);
+    return 0;
+  });
+}
+
+int pga_set_bounds(pga_t* p, population_t* pop, float lo, float hi) {
+  if (!valid_pop(p, pop) || !(lo < hi)) return -1;
+  return guard_r<int>(p, -1, [&]() {
+    pga::Config c = pop->isl->config();
+    c.lo = lo;
+    c.hi = hi;
+    pop->isl->set_operators(c);
+    return 0;
+  });
+}
+
+int pga_set_blend_alpha(pga_t* p, population_t* pop, float alpha) {
+  if (!valid_pop(p, pop)) return -1;
+  return guard_r<int>(p, -1, [&]() {
+    pga::Config c = pop->isl->config();
+    c.blend_alpha = alpha;
+    pop->isl->set_operators(c);
+    return 0;
+  });
+}
+
+// -------------------------------------------------------------------- stages
+void pga_evaluate(pga_t* p, population_t* pop) {
+  if (!valid_pop(p, pop)) return;
+  guard(p, [&]() {
+    sync_callbacks(p, pop);
+    pop->isl->evaluate();
+  });
+}
+
+void pga_evaluate_all(pga_t* p) {
+  if (!p) return;
+  for (population_t* pop : p->pops) pga_evaluate(p, pop);
+}
+
+void pga_crossover(pga_t* p, population_t* pop, enum crossover_selection_type type) {
+  (void)type;  // TOURNAMENT is the only selection of the original enum; see pga_set_operators
+  if (!valid_pop(p, pop)) return;
+  guard(p, [&]() {
+    sync_callbacks(p, pop);
+    pop->isl->crossover_stage();
+  });
+}
+
+void pga_crossover_all(pga_t* p, enum crossover_selection_type type) {
+  if (!p) return;
+  for (population_t* pop : p->pops) pga_crossover(p, pop, type);
+}
+
+void pga_mutate(pga_t* p, population_t* pop) {
+  if (!valid_pop(p, pop)) return;
+  guard(p, [&]() {
+    sync_callbacks(p, pop);
+    pop->isl->mutate_stage();
+  });
+}
+
+void pga_mutate_all(pga_t* p) {
+  if (!p) return;
+  for (population_t* pop : p->pops) pga_mutate(p, pop);
+}
+
+void pga_swap_generations(pga_t* p, population_t* pop) {
+  if (!valid_pop(p, pop)) return;
+  pop->isl->swap();
+}
+
+void pga_fill_random_values(pga_t* p, population_t* pop) {
+  // Randomness is counter-based; this only re-keys the population's streams
+  // so repeated stage calls within one generation draw fresh numbers.
+  if (!valid_pop(p, pop)) return;
+  pop->isl->bump_epoch();
+}
+
+// ------------------------------------------------------------------- results
+gene* pga_get_best(pga_t* p, population_t* pop) {
+  if (!valid_pop(p, pop)) return nullptr;
+  return guard_r<gene*>(p, nullptr, [&]() {
+    pga::Island& isl = *pop->isl;
+    isl.stream = p->stream;
+    const unsigned long long b = isl.best_packed();
+    if (!p->quiet) std::printf("%f\n", (double)pga::best_score(b));
+    return decode_row(isl, isl.row_host(pga::best_index(b)));
+  });
+}
+
+gene** pga_get_best_top(pga_t* p, population_t* pop, unsigned length) {
+  if (!valid_pop(p, pop) || length == 0) return nullptr;
+  return guard_r<gene**>(p, nullptr, [&]() -> gene** {
+    pga::Island& isl = *pop->isl;
+    isl.stream = p->stream;
+    const uint32_t k = (uint32_t)std::min<uint64_t>(length, isl.config().S);
+    std::vector<uint32_t> idx = isl.topk_host(k, true);
+    gene** out = (gene**)std::calloc(length, sizeof(gene*));
+    if (!out) throw std::bad_alloc();
+    for (uint32_t i = 0; i < k; ++i) out[i] = decode_row(isl, isl.row_host(idx[i]));
+    return out;
+  });
+}
+
+gene* pga_get_best_all(pga_t* p) {
+  if (!p || p->pops.empty()) return nullptr;
+  return guard_r<gene*>(p, nullptr, [&]() -> gene* {
+    population_t* bp = nullptr;
+    unsigned long long best = 0;
+    for (population_t* pop : p->pops) {
+      pop->isl->stream = p->stream;
+      const unsigned long long b = pop->isl->best_packed();
+      if (!bp || pga::best_score(b) > pga::best_score(best)) {
+        bp = pop;
+        best = b;
+      }
+    }
+    if (!p->quiet) std::printf("%f\n", (double)pga::best_score(best));
+    return decode_row(*bp->isl, bp->isl->row_host(pga::best_index(best)));
+  });
+}
+
+gene** pga_get_best_top_all(pga_t* p, unsigned length) {
+  if (!p || p->pops.empty() || length == 0) return nullptr;
+  return guard_r<gene**>(p, nullptr, [&]() -> gene** {
+    struct Cand {
+      float score;
+      size_t pop;
+      uint32_t idx;
+    };
+    std::vector<Cand> all;
+    for (size_t i = 0; i < p->pops.size(); ++i) {
+      pga::Island& isl = *p->pops[i]->isl;
+      isl.stream = p->stream;
+      const uint32_t k = (uint32_t)std::min<uint64_t>(length, isl.config().S);
+      std::vector<uint32_t> idx = isl.topk_host(k, true);
+      std::vector<float> sc(isl.config().S);
+      isl.copy_to_host(sc.data(), isl.scores(0), 4ull * sc.size());
+      for (uint32_t j : idx) all.push_back({sc[j], i, j});
+    }
+    std::stable_sort(all.begin(), all.end(), [](const Cand& a, const Cand& b) { return a.score > b.score; });
+    gene** out = (gene**)std::calloc(length, sizeof(gene*));
+    if (!out) throw std::bad_alloc();
+    for (size_t i = 0; i < std::min<size_t>(length, all.size()); ++i) {
+      pga::Island& isl = *p->pops[all[i].pop]->isl;
+      out[i] = decode_row(isl, isl.row_host(all[i].idx));
+    }
+    return out;
+  });
+}
+
+// -------------------------------------------------------------------- islands
+void pga_migrate_between(pga_t* p, population_t* from, population_t* to, float pct) {
+  if (!valid_pop(p, from) || !valid_pop(p, to) || from == to) return;
+  guard(p, [&]() {
+    pga::Island &a = *from->isl, &b = *to->isl;
+    if (a.config().encoding != b.config().encoding || a.config().L != b.config().L)
+      throw std::invalid_argument("migration needs populations of the same encoding and genome length");
+    a.stream = b.stream = p->stream;
+    const uint32_t k = migrants(a.config().S, b.config().S, pct);
+    if (!k) return;
+    Emigrants e = take_best(a, k);
+    replace_worst(b, e);
+    free_emigrants(a, e);
+  });
+}
+
+void pga_migrate(pga_t* p, float pct) {
+  if (!p || p->pops.size() < 2) return;
+  guard(p, [&]() {
+    // random island ring, drawn from the seed so runs are reproducible;
+    // every population's emigrants are taken before any is replaced
+    const size_t n = p->pops.size();
+    std::vector<uint32_t> perm(n);
+    for (uint32_t i = 0; i < n; ++i) perm[i] = i;
+    pga::RngKey key{(uint32_t)p->seed, (uint32_t)(p->seed >> 32), p->migration_epoch++, 0};
+    for (uint32_t i = (uint32_t)n - 1; i >= 1; --i) {
+      const uint32_t j = pga::word_to_index(pga::draw(key, pga::ST_MIGRATE, 0, i).x, i + 1);
+      std::swap(perm[i], perm[j]);
+    }
+    std::vector<Emigrants> out(n);
+    for (size_t i = 0; i < n; ++i) {
+      population_t* src = p->pops[perm[i]];
+      population_t* dst = p->pops[perm[(i + 1) % n]];
+      src->isl->stream = p->stream;
+      const uint32_t k = migrants(src->isl->config().S, dst->isl->config().S, pct);
+      if (k) out[i] = take_best(*src->isl, k);
+    }
+    for (size_t i = 0; i < n; ++i) {
+      population_t* dst = p->pops[perm[(i + 1) % n]];
+      if (out[i].k) {
+        dst->isl->stream = p->stream;
+        replace_worst(*dst->isl, out[i]);
+      }
+      free_emigrants(*p->pops[perm[i]]->isl, out[i]);
+    }
+  });
+}
+
+namespace {
+void migrate_ranks(pga_t* p, float pct) {
+  if (!p->comm || pga::rccl_size(p->comm) == 1 || p->pops.empty()) return;
+  pga::Island& isl = *p->pops[0]->isl;
+  isl.stream = p->stream;
+  const uint32_t k = migrants(isl.config().S, isl.config().S, pct);
+  if (!k) return;
+  const size_t rows = isl.row_bytes() * k, bytes = rows + 4ull * k;
+  if (p->mig_bytes < bytes) {
+    dev_free(isl, p->mig_send);
+    dev_free(isl, p->mig_recv);
+    p->mig_send = dev_alloc(isl, bytes);
+    p->mig_recv = dev_alloc(isl, bytes);
+    p->mig_bytes = bytes;
+  }
+  uint32_t* idx = (uint32_t*)isl.scratch(4ull * k);
+  isl.topk(k, true, idx);
+  isl.gather(idx, k, p->mig_send, (float*)((char*)p->mig_send + rows));
+  pga::rccl_ring_exchange(p->comm, p->mig_send, p->mig_recv, bytes, p->stream);
+  isl.topk(k, false, idx);
+  isl.scatter(idx, k, p->mig_recv, (const float*)((const char*)p->mig_recv + rows));
+}
+}  // namespace
+
+void pga_run(pga_t* p, unsigned n) {
+  if (!p || p->pops.empty()) return;
+  guard(p, [&]() {
+    population_t* pop = p->pops[0];
+    sync_callbacks(p, pop);
+    pop->isl->evaluate();  // reference: evaluate precedes every crossover (src/pga.cu:383)
+    pop->isl->run(n);      // each fused generation leaves its children evaluated
+  });
+}
+
+void pga_run_islands(pga_t* p, unsigned n, unsigned m, float pct) {
+  if (!p || p->pops.empty()) return;
+  guard(p, [&]() {
+    for (population_t* pop : p->pops) {
+      sync_callbacks(p, pop);
+      pop->isl->evaluate();
+    }
+    for (unsigned g = 1; g <= n; ++g) {
+      for (population_t* pop : p->pops) pop->isl->run(1);
+      if (m > 0 && g % m == 0 && g < n) {
+        pga_migrate(p, pct);
+        migrate_ranks(p, pct);
+      }
+    }
+  });
+}
+
+// -------------------------------------------------------------------- queries
+unsigned long pga_population_size(const population_t* pop) { return pop ? (unsigned long)pop->isl->config().S : 0; }
+unsigned pga_genome_length(const population_t* pop) { return pop ? pop->isl->config().L : 0; }
+unsigned pga_generation(const population_t* pop) { return pop ? pop->isl->generation() : 0; }
+size_t pga_row_bytes(const population_t* pop) { return pop ? pop->isl->row_bytes() : 0; }
+
+float pga_best_score(pga_t* p, population_t* pop) {
+  if (!valid_pop(p, pop)) return NAN;
+  return guard_r<float>(p, NAN, [&]() {
+    pop->isl->stream = p->stream;
+    return pop->isl->best_score();
+  });
+}
+
+unsigned long pga_best_index(pga_t* p, population_t* pop) {
+  if (!valid_pop(p, pop)) return 0;
+  return guard_r<unsigned long>(p, 0, [&]() {
+    pop->isl->stream = p->stream;
+    return (unsigned long)pop->isl->best_index();
+  });
+}
+
+int pga_get_scores(pga_t* p, population_t* pop, float* out) {
+  if (!valid_pop(p, pop) || !out) return -1;
+  return guard_r<int>(p, -1, [&]() {
+    pop->isl->stream = p->stream;
+    pop->isl->copy_to_host(out, pop->isl->scores(0), 4ull * pop->isl->config().S);
+    return 0;
+  });
+}
+
+int pga_get_genome(pga_t* p, population_t* pop, unsigned long i, void* out) {
+  if (!valid_pop(p, pop) || !out) return -1;
+  return guard_r<int>(p, -1, [&]() {
+    pop->isl->stream = p->stream;
+    std::vector<uint32_t> r = pop->isl->row_host(i);
+    std::memcpy(out, r.data(), 4 * r.size());
+    return 0;
+  });
+}
+
+int pga_stats(pga_t* p, population_t* pop, float out[4]) {
+  if (!valid_pop(p, pop) || !out) return -1;
+  return guard_r<int>(p, -1, [&]() {
+    pop->isl->stream = p->stream;
+    pop->isl->stats(out);
+    return 0;
+  });
+}
+
+int pga_synchronize(pga_t* p) {
+  if (!p) return -1;
+  if (p->stream) return hipStreamSynchronize(p->stream) == hipSuccess ? 0 : -1;
+  return 0;
+}
+
+int pga_save(pga_t* p, population_t* pop, const char* path) {
+  if (!valid_pop(p, pop) || !path) return -1;
+  return guard_r<int>(p, -1, [&]() {
+    pop->isl->stream = p->stream;
+    pop->isl->save(path);
+    return 0;
+  });
+}
+
+int pga_load(pga_t* p, population_t* pop, const char* path) {
+  if (!valid_pop(p, pop) || !path) return -1;
+  return guard_r<int>(p, -1, [&]() {
+    pop->isl->stream = p->stream;
+    pop->isl->load(path);
+    return 0;
+  });
+}
+
+// ---------------------------------------------------------------------- comm
+int pga_comm_unique_id(char id[128]) {
+  try {
+    return pga::rccl_unique_id(id);
+  } catch (const std::exception& e) {
+    g_last_error = e.what();
+    return -1;
+  }
+}
+
+int pga_comm_init(pga_t* p, int nranks, int rank, const char id[128]) {
+  if (!p || p->device < 0) return -1;
+  return guard_r<int>(p, -1, [&]() {
+    p->comm = pga::rccl_init(nranks, rank, id, p->device);
+    return 0;
+  });
+}
+
+int pga_comm_rank(const pga_t* p) { return p ? pga::rccl_rank(p->comm) : 0; }
+int pga_comm_size(const pga_t* p) { return p ? pga::rccl_size(p->comm) : 1; }
+
+int pga_comm_best(pga_t* p, float* score, int* rank) {
+  if (!p || p->pops.empty()) return -1;
+  return guard_r<int>(p, -1, [&]() {
+    pga::Island& isl = *p->pops[0]->isl;
+    isl.stream = p->stream;
+    const float mine = isl.best_score();
+    const int n = pga::rccl_size(p->comm);
+    std::vector<float> all(n);
+    pga::rccl_allgather_f32(p->comm, mine, all.data(), p->stream);
+    int br = 0;
+    for (int i = 1; i < n; ++i)
+      if (all[i] > all[br]) br = i;
+    if (score) *score = all[br];
+    if (rank) *rank = br;
+    return 0;
+  });
+}
+
+}  // extern "C"

@@ -64,7 +64,7 @@ Island::Island(const Config& cfg, int device) : cfg_(cfg), device_(device) {
 Island::~Island() {
   Buffer* all[] = {&rows_[0],   &rows_[1],     &scores_[0],   &scores_[1],  &best_[0],  &best_[1],   &mut_thr_,
                    &obj_data_[0], &obj_data_[1], &keys_[0], &keys_[1], &elite_idx_, &cumfit_, &cum_ws_, &topk_ws_, &stats_,
-                   &out_best_,  &scratch_};
+                   &out_best_,  &scratch_, &compat_rand_};
   for (Buffer* b : all) {
     try {
       release(*b);
@@ -157,6 +157,15 @@ void Island::set_operators(const Config& c) {
   }
 }
 
+void Island::set_user_operators(void* xo, void* mut) {
+  if ((xo || mut) && !on_gpu()) throw std::invalid_argument("device function pointers need the GPU backend");
+  if ((xo || mut) && cfg_.encoding != ENC_REAL)
+    throw std::invalid_argument("user crossover/mutate callbacks need the REAL (float gene) encoding");
+  user_xo_fn_ = xo;
+  user_mut_fn_ = mut;
+  if ((xo || mut) && !compat_rand_.ptr) compat_rand_ = alloc(4ull * cfg_.S * cfg_.L);
+}
+
 void Island::set_objective_data(const float* host, size_t n, int which) {
   if (which < 0 || which > 1) throw std::invalid_argument("objective data slot must be 0 or 1");
   if (on_gpu()) synchronize();
@@ -212,6 +221,9 @@ GenArgs Island::make_args(int mode) {
   a.obj_data = (const float*)obj_data_[0].ptr;
   a.obj_data2 = (const float*)obj_data_[1].ptr;
   a.user_fn = user_fn_;
+  a.user_xo_fn = user_xo_fn_;
+  a.user_mut_fn = user_mut_fn_;
+  a.compat_rand = (float*)compat_rand_.ptr;
   a.n_elite = cfg_.n_elite;
   a.elite_idx = cfg_.n_elite > 1 ? (const uint32_t*)elite_idx_.ptr : nullptr;
   a.best_cur = (const unsigned long long*)best_[cur_].ptr;

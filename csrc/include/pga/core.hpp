@@ -252,6 +252,9 @@ struct GenArgs {
   const float* obj_data; // problem data (weights, distance matrix, rotation, shift)
   const float* obj_data2;
   void* user_fn;         // reference-ABI device function pointer (OBJ_USER_FNPTR)
+  void* user_xo_fn;      // reference-ABI crossover_f (compat kernel), nullptr = built-in
+  void* user_mut_fn;     // reference-ABI mutate_f (compat kernel), nullptr = built-in
+  float* compat_rand;    // S*L scratch for the rand slices handed to user callbacks
 
   // elitism: children [0, n_elite) copy elite_idx[i] (E==1 may use best_cur)
   uint32_t n_elite;

@@ -75,6 +75,8 @@ class Island {
   void set_operators(const Config& c);  // selection/crossover/mutation/objective scalars
   void set_objective_data(const float* host, size_t n, int which);  // which = 0 or 1
   void set_user_fn(void* f) { user_fn_ = f; }
+  // reference-ABI crossover_f / mutate_f device pointers (nullptr = built-in)
+  void set_user_operators(void* xo, void* mut);
 
   // ---- stages ----
   void initialize();          // random population + evaluation (generation 0)
@@ -137,6 +139,9 @@ class Island {
   float mut_inv_ = 0.f;
   float mut_rate_eff_ = 0.f;
   void* user_fn_ = nullptr;
+  void* user_xo_fn_ = nullptr;
+  void* user_mut_fn_ = nullptr;
+  Buffer compat_rand_;
   u32x4 last_mask_{0, 0, 0, 0};
 };
 

@@ -42,10 +42,16 @@ uint32_t binary_launch(int mode, const GenArgs& a, unsigned long long* best_part
 uint32_t real_launch(int mode, const GenArgs& a, unsigned long long* best_parts, hipStream_t s);
 uint32_t perm_launch(int mode, const GenArgs& a, unsigned long long* best_parts, hipStream_t s);
 
+// reference-ABI path: thread-per-individual kernel calling user device
+// function pointers (crossover_f / mutate_f / obj_f), REAL encoding only
+uint32_t compat_launch(int mode, const GenArgs& a, unsigned long long* best_parts, hipStream_t s);
+
 inline uint32_t encoding_launch(int mode, const GenArgs& a, unsigned long long* best_parts, hipStream_t s) {
   switch (a.encoding) {
     case ENC_BINARY: return binary_launch(mode, a, best_parts, s);
-    case ENC_REAL: return real_launch(mode, a, best_parts, s);
+    case ENC_REAL:
+      if (a.user_xo_fn || a.user_mut_fn) return compat_launch(mode, a, best_parts, s);
+      return real_launch(mode, a, best_parts, s);
     default: return perm_launch(mode, a, best_parts, s);
   }
 }

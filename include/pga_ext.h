@@ -1,0 +1,87 @@
+/*
+ * pga_ext.h — extensions of the pga.h C API (not in the original library).
+ *
+ * Enum values mirror csrc/include/pga/core.hpp exactly.
+ */
+#ifndef PGA_EXT_H
+#define PGA_EXT_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include "pga.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum pga_encoding { PGA_BINARY = 0, PGA_REAL = 1, PGA_PERMUTATION = 2 };
+enum pga_selection { PGA_SEL_TOURNAMENT = 0, PGA_SEL_ROULETTE = 1, PGA_SEL_RANDOM = 2 };
+enum pga_crossover {
+  PGA_XO_UNIFORM = 0, PGA_XO_ONE_POINT = 1, PGA_XO_TWO_POINT = 2, PGA_XO_BLEND = 3,
+  PGA_XO_ARITHMETIC = 4, PGA_XO_PMX = 5, PGA_XO_OX = 6, PGA_XO_NONE = 7
+};
+enum pga_mutation {
+  PGA_MUT_BIT_FLIP = 0, PGA_MUT_GAUSSIAN = 1, PGA_MUT_UNIFORM = 2, PGA_MUT_RESET_ONE = 3,
+  PGA_MUT_SWAP = 4, PGA_MUT_INVERSION = 5, PGA_MUT_NONE = 6
+};
+enum pga_objective {
+  PGA_OBJ_NONE = 0, PGA_OBJ_ONEMAX = 1, PGA_OBJ_KNAPSACK = 2, PGA_OBJ_TRAP = 3, PGA_OBJ_LEADING_ONES = 4,
+  PGA_OBJ_SPHERE = 16, PGA_OBJ_RASTRIGIN = 17, PGA_OBJ_ROSENBROCK = 18, PGA_OBJ_ACKLEY = 19,
+  PGA_OBJ_GRIEWANK = 20, PGA_OBJ_SCHWEFEL = 21, PGA_OBJ_LINEAR = 22, PGA_OBJ_KNAPSACK_REAL = 23,
+  PGA_OBJ_TSP_RANDOM_KEY = 24, PGA_OBJ_TSP = 32, PGA_OBJ_TSP_OPEN = 33, PGA_OBJ_TSP_EUC = 34,
+  PGA_OBJ_USER_FNPTR = 64
+};
+
+/* ---- solver options (call before creating populations) ---- */
+pga_t *pga_init_device(int device);            /* device < 0: CPU reference backend */
+void pga_set_seed(pga_t *p, uint64_t seed);      /* default: PGA_SEED env or time(NULL) */
+void pga_set_quiet(pga_t *p, int quiet);         /* 1: pga_get_best does not print */
+/* 1 (default, reference behaviour): print the error and exit; 0: record it and return */
+void pga_set_abort_on_error(pga_t *p, int abort_on_error);
+const char *pga_last_error(void);                /* thread-local, "" when none */
+
+/* ---- populations of any encoding ---- */
+population_t *pga_create_population_ext(pga_t *p, unsigned long size, unsigned genome_len,
+                                        enum pga_encoding encoding);
+/* built-in fused objective; data / data2 are host arrays copied to the device */
+int pga_set_objective_builtin(pga_t *p, population_t *pop, enum pga_objective objective, const float *data,
+                              size_t n, const float *data2, size_t n2, int iparam, float fparam0, float fparam1);
+int pga_set_operators(pga_t *p, population_t *pop, enum pga_selection selection, unsigned tournament_k,
+                      enum pga_crossover crossover, float crossover_prob, enum pga_mutation mutation,
+                      float mutation_rate /* < 0: default */, float sigma, unsigned elitism);
+int pga_set_bounds(pga_t *p, population_t *pop, float lo, float hi);
+int pga_set_blend_alpha(pga_t *p, population_t *pop, float alpha);
+
+/* ---- queries ---- */
+unsigned long pga_population_size(const population_t *pop);
+unsigned pga_genome_length(const population_t *pop);
+unsigned pga_generation(const population_t *pop);
+float pga_best_score(pga_t *p, population_t *pop);
+unsigned long pga_best_index(pga_t *p, population_t *pop);
+int pga_get_scores(pga_t *p, population_t *pop, float *out);             /* S floats */
+int pga_get_genome(pga_t *p, population_t *pop, unsigned long i, void *out); /* raw row (row bytes) */
+size_t pga_row_bytes(const population_t *pop);
+int pga_stats(pga_t *p, population_t *pop, float out[4]);                /* min, max, sum, count */
+int pga_synchronize(pga_t *p);
+
+/* ---- checkpoint / resume (exact: the generation counter is the RNG state) ---- */
+int pga_save(pga_t *p, population_t *pop, const char *path);
+int pga_load(pga_t *p, population_t *pop, const char *path);
+
+/* ---- multi-GPU island model over RCCL (one process per GPU) ----
+ * Rank 0 creates an id (128 bytes) and shares it (file, env, MPI, ...);
+ * every rank calls pga_comm_init.  pga_run_islands then also migrates
+ * population 0 of each rank around a ring of ranks. */
+int pga_comm_unique_id(char id[128]);
+int pga_comm_init(pga_t *p, int nranks, int rank, const char id[128]);
+int pga_comm_rank(const pga_t *p);
+int pga_comm_size(const pga_t *p);
+/* global best over ranks (score, owning rank) */
+int pga_comm_best(pga_t *p, float *score, int *rank);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* PGA_EXT_H */

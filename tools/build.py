@@ -28,10 +28,10 @@ BUILD = os.path.join(ROOT, "build")
 ARCH = os.environ.get("PGA_ARCH", "gfx950")
 
 KERNELS = ["csrc/kernels/binary.hip", "csrc/kernels/real.hip", "csrc/kernels/perm.hip",
-           "csrc/kernels/util.hip"]
+           "csrc/kernels/util.hip", "csrc/kernels/compat.hip"]
 HOST = ["csrc/engine/island.cpp", "csrc/cpu/cpu_ops.cpp", "csrc/cpu/cpu_real.cpp", "csrc/cpu/cpu_perm.cpp"]
-CAPI = ["csrc/capi/pga_capi.cpp"]
-COMPAT = ["csrc/capi/compat.hip"]
+CAPI = ["csrc/capi/pga_capi.cpp", "csrc/capi/comm_rccl.cpp"]
+COMPAT = []
 BINDINGS = ["csrc/python/bindings.cpp"]
 
 
@@ -89,6 +89,12 @@ def write_ninja(opt: str, with_torch: bool) -> str:
         "rule ar",
         "  command = rm -f $out && /opt/rocm/lib/llvm/bin/llvm-ar rcs $out $in",
         "  description = AR $out",
+        "rule cc",
+        "  command = gcc -O2 -o $out $in",
+        "  description = CC $out",
+        "rule cexe",
+        "  command = gcc -O2 -Iinclude -o $out $in -Lbuild -lpga -Wl,-rpath,'$$ORIGIN/..'",
+        "  description = CC $out",
         "rule link_exe",
         f"  command = $hipcc --offload-arch={ARCH} $extra -o $out $in $ldflags",
         "  description = LINK $out",
@@ -115,7 +121,7 @@ def write_ninja(opt: str, with_torch: bool) -> str:
         lines.append(f"build {o}: hip {s}")
         compat_objs.append(o)
     lines.append(f"build build/libpga.so: link_so {' '.join(core_objs + capi_objs + compat_objs)}")
-    lines.append("  ldflags = -Wl,-soname,libpga.so")
+    lines.append("  ldflags = -Wl,-soname,libpga.so -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib")
 
     # static rdc library for user device function pointers
     rdc_objs = []
@@ -136,11 +142,16 @@ def write_ninja(opt: str, with_torch: bool) -> str:
         exe = f"build/examples/{name}"
         lines.append(f"build {exe}: link_exe {o} build/libpga.a")
         lines.append(f"  extra = -fgpu-rdc --hip-link")
-        lines.append("  ldflags = -lpthread")
+        lines.append("  ldflags = -lpthread -L/opt/rocm/lib -lrccl")
+        ex.append(exe)
+    for name in ("onemax_bits",):
+        src = f"examples/{name}.c"
+        if not os.path.exists(os.path.join(ROOT, src)):
+            continue
+        exe = f"build/examples/{name}"
+        lines.append(f"build {exe}: cexe {src} | build/libpga.so")
         ex.append(exe)
     if os.path.exists(os.path.join(ROOT, "examples/gen_tsp.c")):
-        lines.append("rule cc")
-        lines.append("  command = gcc -O2 -o $out $in")
         lines.append("build build/examples/gen_tsp: cc examples/gen_tsp.c")
         ex.append("build/examples/gen_tsp")
 
