@@ -198,6 +198,14 @@ class IslandModel:
     def flush(self) -> None:
         self.finish_migration()
 
+    def connect(self) -> None:
+        """Run one migration now: RCCL establishes its point-to-point
+        connections lazily on the first exchange, so benchmarks call this
+        before timing."""
+        if self.world > 1 and self.k > 0:
+            self.start_migration()
+            self.finish_migration()
+
     # -------------------------------------------------------------- queries --
     def global_best(self) -> Tuple[float, int, torch.Tensor]:
         """(score, owning rank, decoded genome) of the best individual of all islands."""
