@@ -96,7 +96,7 @@ uint32_t perm_run(int mode, const GenArgs& a, unsigned long long* best_parts) {
       float lane[64] = {0};
       const uint32_t last = a.objective == OBJ_TSP_OPEN ? L - 1 : L;
       for (uint32_t p = 0; p < last; ++p) {
-        const uint32_t u = C[p], w = C[(p + 1) % L];
+        const uint32_t u = std::min<uint32_t>(C[p], L - 1), w = std::min<uint32_t>(C[(p + 1) % L], L - 1);
         float d;
         if (a.objective == OBJ_TSP_EUC) {
           const float dx = a.obj_data[2 * u] - a.obj_data[2 * w], dy = a.obj_data[2 * u + 1] - a.obj_data[2 * w + 1];

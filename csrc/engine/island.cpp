@@ -9,6 +9,7 @@
 
 #include "pga/cpu.hpp"
 #include "pga/ops.hpp"
+#include "pga/trace.hpp"
 
 namespace pga {
 
@@ -64,7 +65,7 @@ Island::Island(const Config& cfg, int device) : cfg_(cfg), device_(device) {
 Island::~Island() {
   Buffer* all[] = {&rows_[0],   &rows_[1],     &scores_[0],   &scores_[1],  &best_[0],  &best_[1],   &mut_thr_,
                    &obj_data_[0], &obj_data_[1], &keys_[0], &keys_[1], &elite_idx_, &cumfit_, &cum_ws_, &topk_ws_, &stats_,
-                   &out_best_,  &scratch_, &compat_rand_};
+                   &out_best_,  &scratch_, &compat_rand_, &ev_parts_};
   for (Buffer* b : all) {
     try {
       release(*b);
@@ -243,12 +244,14 @@ uint32_t Island::launch(int mode, const GenArgs& a, unsigned long long* parts) {
 }
 
 void Island::initialize() {
+  TraceRange tr("pga.initialize");
   GenArgs a = make_args(MODE_INIT);
   n_best_[cur_] = launch(MODE_INIT, a, (unsigned long long*)best_[cur_].ptr);
   if (cfg_.objective == OBJ_NONE) rebest();
 }
 
 void Island::evaluate() {
+  TraceRange tr("pga.evaluate");
   GenArgs a = make_args(MODE_EVAL);
   n_best_[cur_] = launch(MODE_EVAL, a, (unsigned long long*)best_[cur_].ptr);
 }
@@ -274,7 +277,9 @@ void Island::prepare_generation() {
 }
 
 void Island::run(uint32_t n) {
+  TraceRange tr("pga.run");
   for (uint32_t i = 0; i < n; ++i) {
+    TraceRange tg("pga.generation", 2);
     prepare_generation();
     GenArgs a = make_args(MODE_GEN);
     n_best_[cur_ ^ 1] = launch(MODE_GEN, a, (unsigned long long*)best_[cur_ ^ 1].ptr);
@@ -283,12 +288,14 @@ void Island::run(uint32_t n) {
 }
 
 void Island::crossover_stage() {
+  TraceRange tr("pga.crossover");
   prepare_generation();
   GenArgs a = make_args(MODE_CROSS);
   launch(MODE_CROSS, a, nullptr);
 }
 
 void Island::mutate_stage() {
+  TraceRange tr("pga.mutate");
   GenArgs a = make_args(MODE_MUTATE);
   launch(MODE_MUTATE, a, nullptr);
 }
@@ -321,6 +328,7 @@ void Island::stats(float out[4]) {
 }
 
 void Island::topk(uint32_t k, bool largest, uint32_t* idx_out) {
+  TraceRange tr(largest ? "pga.topk" : "pga.bottomk");
   if (k > cfg_.S) throw std::invalid_argument("k exceeds population size");
   const float* sc = (const float*)scores_[cur_].ptr;
   if (on_gpu()) {
@@ -357,6 +365,7 @@ std::vector<uint32_t> Island::row_host(uint64_t i) {
 }
 
 void Island::gather(const uint32_t* idx, uint32_t n, void* out_rows, float* out_scores) {
+  TraceRange tr("pga.migrate.gather");
   if (on_gpu())
     gather_rows_launch(rows_[cur_].ptr, (const float*)scores_[cur_].ptr, row_words_, idx, n, out_rows, out_scores,
                        stream);
@@ -365,11 +374,31 @@ void Island::gather(const uint32_t* idx, uint32_t n, void* out_rows, float* out_
 }
 
 void Island::scatter(const uint32_t* idx, uint32_t n, const void* in_rows, const float* in_scores) {
+  TraceRange tr("pga.migrate.scatter");
   if (on_gpu())
     scatter_rows_launch(rows_[cur_].ptr, (float*)scores_[cur_].ptr, row_words_, idx, n, in_rows, in_scores, stream);
   else
     cpu::scatter_rows(rows_[cur_].ptr, (float*)scores_[cur_].ptr, row_words_, idx, n, in_rows, in_scores);
   rebest();  // best partials and tournament keys follow the new scores
+}
+
+bool Island::evaluate_rows(void* rows, float* scores, uint32_t n) {
+  if (cfg_.objective == OBJ_NONE) return false;
+  if (n == 0) return true;
+  TraceRange tr("pga.migrate.evaluate");
+  if (!ev_parts_.ptr) ev_parts_ = alloc(8ull * kMaxGrid);
+  GenArgs a = make_args(MODE_EVAL);
+  a.cur = rows;
+  a.next = rows;
+  a.score_cur = scores;
+  a.score_next = scores;
+  a.S = n;
+  a.key_cur = nullptr;
+  a.key_next = nullptr;
+  a.n_elite = 0;
+  a.elite_idx = nullptr;
+  launch(MODE_EVAL, a, (unsigned long long*)ev_parts_.ptr);
+  return true;
 }
 
 // ------------------------------------------------------------ checkpoint ---
@@ -384,6 +413,7 @@ struct CkptHeader {
 }  // namespace
 
 void Island::save(const std::string& path) {
+  TraceRange tr("pga.checkpoint.save");
   CkptHeader h;
   std::memset(&h, 0, sizeof(h));
   std::memcpy(h.magic, "PGACKPT1", 8);
@@ -409,6 +439,7 @@ void Island::save(const std::string& path) {
 }
 
 void Island::load(const std::string& path) {
+  TraceRange tr("pga.checkpoint.load");
   FILE* f = std::fopen(path.c_str(), "rb");
   if (!f) throw std::runtime_error("cannot open checkpoint: " + path);
   CkptHeader h;

@@ -99,6 +99,9 @@ class Island {
   void topk(uint32_t k, bool largest, uint32_t* idx_out);  // idx_out: device (or host for CPU) memory
   void gather(const uint32_t* idx, uint32_t n, void* out_rows, float* out_scores);
   void scatter(const uint32_t* idx, uint32_t n, const void* in_rows, const float* in_scores);
+  // score n external rows (e.g. received migrants) with this island's
+  // objective, in place; false when the objective is not native (OBJ_NONE)
+  bool evaluate_rows(void* rows, float* scores, uint32_t n);
 
   // raw buffers (cur = current generation)
   void* rows(int which) { return rows_[which ^ cur_].ptr; }
@@ -141,7 +144,7 @@ class Island {
   void* user_fn_ = nullptr;
   void* user_xo_fn_ = nullptr;
   void* user_mut_fn_ = nullptr;
-  Buffer compat_rand_;
+  Buffer compat_rand_, ev_parts_;
   u32x4 last_mask_{0, 0, 0, 0};
 };
 

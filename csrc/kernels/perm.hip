@@ -240,7 +240,9 @@ __global__ __launch_bounds__(kBlock) void perm_kernel(GenArgs a, unsigned long l
           for (uint32_t e = 0; e < 8; ++e) {
             const uint32_t p = 8 * c + e;
             if (p >= last) break;
-            const uint32_t u = e8[e], w = (e < 7 && p + 1 < L) ? e8[e + 1] : Cc[(p + 1 == L) ? 0 : p + 1];
+            // min(): a forged row (e.g. a corrupted migrant) can never index out of bounds
+            const uint32_t u = min(e8[e], L - 1),
+                           w = min((e < 7 && p + 1 < L) ? e8[e + 1] : (uint32_t)Cc[(p + 1 == L) ? 0 : p + 1], L - 1);
             if (OBJ == OBJ_TSP_EUC) {
               const float dx = coords[2 * u] - coords[2 * w], dy = coords[2 * u + 1] - coords[2 * w + 1];
               len += sqrtf(dx * dx + dy * dy);

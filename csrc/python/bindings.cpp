@@ -11,6 +11,7 @@
 #include <memory>
 
 #include "pga/island.hpp"
+#include "pga/trace.hpp"
 #include "pga/ops.hpp"
 
 namespace py = pybind11;
@@ -85,6 +86,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     return py::make_tuple(rw, ch);
   });
   m.def("group_size", &pga::group_size);
+  m.def("trace_level", &pga::trace_level);
+  m.def("trace_push", [](const std::string& n) { pga::trace_push(n.c_str()); });
+  m.def("trace_pop", &pga::trace_pop);
+  m.def("trace_mark", [](const std::string& n) { pga::trace_mark(n.c_str()); });
   m.def("philox", [](uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t k0, uint32_t k1) {
     pga::u32x4 r = pga::philox4x32_10(pga::u32x4{c0, c1, c2, c3}, k0, k1);
     return py::make_tuple(r.x, r.y, r.z, r.w);
@@ -179,6 +184,15 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
              TORCH_CHECK(in_rows.numel() >= n * i->row_words() && in_scores.numel() >= n, "input too small");
              i->scatter((const uint32_t*)idx.data_ptr<int32_t>(), (uint32_t)n, in_rows.data_ptr(),
                         in_scores.data_ptr<float>());
+           })
+      .def("evaluate_rows",
+           [](const IslandPtr& i, torch::Tensor rows, torch::Tensor scores) {
+             bind_stream(*i);
+             check_tensor(rows, *i, torch::kInt32, "rows");
+             check_tensor(scores, *i, torch::kFloat32, "scores");
+             const int64_t n = scores.numel();
+             TORCH_CHECK(rows.numel() >= n * i->row_words(), "rows too small");
+             return i->evaluate_rows(rows.data_ptr(), scores.data_ptr<float>(), (uint32_t)n);
            })
       .def("row", [](Island& i, uint64_t k) {
         bind_stream(i);

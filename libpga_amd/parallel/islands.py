@@ -20,15 +20,26 @@ the same volume over all 7 links (``all_to_all_single``) for larger
 migrations; ``"random"`` draws a fresh island permutation per epoch from the
 shared seed (all ranks agree without communicating).
 
+Failure handling (the reference aborts on any error):
+  * received migrants are re-scored with the LOCAL objective before they
+    enter the population (``validate=True``), so a corrupted or forged batch
+    can never inject a fake fitness;
+  * a migration that fails or exceeds ``timeout_s`` puts the model in
+    DEGRADED mode: islands are loosely coupled, so each keeps evolving alone
+    and ``degraded`` / ``failures`` report it;
+  * ``fault_hook(recv, epoch) -> bool`` is a test-only injection point that
+    may corrupt the received buffer in place or drop it (return False).
+
 Reference: ``pga_migrate`` / ``pga_migrate_between`` / ``pga_run_islands``
 are declared but empty in the reference (include/pga.h:108-115, :145-150;
 src/pga.cu:368-374, :393-395); the README claims "GPUs+MPI" (README.md:4).
 """
 from __future__ import annotations
 
+import datetime
 import math
 import os
-from typing import Optional, Tuple
+from typing import Callable, Optional, Tuple
 
 import torch
 import torch.distributed as dist
@@ -74,6 +85,9 @@ class IslandModel:
         group=None,
         overlap: bool = True,
         seed: int = 0,
+        validate: bool = True,
+        timeout_s: Optional[float] = None,
+        fault_hook: Optional[Callable[[torch.Tensor, int], bool]] = None,
     ):
         if topology not in TOPOLOGIES:
             raise ValueError(f"topology must be one of {TOPOLOGIES}")
@@ -83,6 +97,12 @@ class IslandModel:
         self.group = group
         self.overlap = overlap
         self.seed = seed
+        self.validate = validate
+        self.timeout = datetime.timedelta(seconds=timeout_s) if timeout_s else None
+        self.fault_hook = fault_hook
+        self.degraded = False
+        self.failures = 0
+        self.dropped = 0
         self.distributed = dist.is_available() and dist.is_initialized()
         self.rank = dist.get_rank(group) if self.distributed else 0
         self.world = dist.get_world_size(group) if self.distributed else 1
@@ -122,7 +142,7 @@ class IslandModel:
     # ----------------------------------------------------------- migration --
     def start_migration(self) -> None:
         """Pack the top-k emigrants and post the exchange (asynchronous)."""
-        if self.world == 1 or self.k == 0:
+        if self.world == 1 or self.k == 0 or self.degraded:
             return
         isl = self.ga.island
         idx = isl.topk(self.k, True)
@@ -134,7 +154,11 @@ class IslandModel:
             dst, src = self._peers()
             ops = [dist.P2POp(dist.isend, self.send, dst, group=self.group),
                    dist.P2POp(dist.irecv, self.recv, src, group=self.group)]
-            self._pending = dist.batch_isend_irecv(ops)
+            try:
+                self._pending = dist.batch_isend_irecv(ops)
+            except Exception as e:  # noqa: BLE001 — any comm failure degrades
+                self._fail(e)
+                return
         self._epoch += 1
         self.bytes_sent += self.send.numel() * 4
 
@@ -162,10 +186,22 @@ class IslandModel:
         """Wait for the exchange and replace the worst individuals."""
         if self._pending is None:
             return
-        for wk in self._pending:
-            wk.wait()
+        try:
+            for wk in self._pending:
+                ok = wk.wait(self.timeout) if self.timeout is not None else wk.wait()
+                if ok is False:
+                    raise TimeoutError(f"migration epoch {self._epoch} timed out")
+        except Exception as e:  # noqa: BLE001
+            self._pending = None
+            self._fail(e)
+            return
         self._pending = None
         isl = self.ga.island
+        if self.fault_hook is not None:
+            buf = self._a2a_recv if self.topology == "all_to_all" else self.recv
+            if self.fault_hook(buf, self._epoch) is False:
+                self.dropped += 1
+                return
         if self.topology == "all_to_all":
             w, per = self.world, self.k // (self.world - 1)
             pv = self._a2a_recv.view(w, per * (self.rw + 1))
@@ -173,9 +209,31 @@ class IslandModel:
             scores = torch.cat([pv[p, per * self.rw:] for p in range(w) if p != self.rank]).view(torch.float32)
         else:
             rows, scores = self._views(self.recv)
+        rows, scores = rows.contiguous(), scores.contiguous()
+        if self.validate:
+            isl.evaluate_rows(rows, scores)  # trust nothing from the wire
+            if self.ga.problem.encoding == "permutation":
+                self._sanitize_perm(rows, scores)
         victims = isl.topk(self.k, False)
-        isl.scatter(victims, rows.contiguous(), scores.contiguous())  # also refreshes best + keys
+        isl.scatter(victims, rows, scores)  # also refreshes best + keys
         self.migrations += 1
+
+    def _sanitize_perm(self, rows: torch.Tensor, scores: torch.Tensor) -> None:
+        """Replace received rows that are not permutations by the identity
+        with score -inf (device-side, no host sync)."""
+        L = self.ga.problem.length
+        genes = rows.view(self.k, self.rw).view(torch.int16)[:, :L].to(torch.int32) & 0xFFFF
+        ok = (genes.sort(dim=1).values == torch.arange(L, device=genes.device)).all(dim=1)
+        ident = torch.zeros(self.rw * 2, dtype=torch.int16, device=genes.device)
+        ident[:L] = torch.arange(L, device=genes.device, dtype=torch.int32).to(torch.int16)
+        r16 = rows.view(self.k, self.rw).view(torch.int16)
+        r16.copy_(torch.where(ok[:, None], r16, ident[None, :]))
+        scores.copy_(torch.where(ok, scores, torch.full_like(scores, float("-inf"))))
+
+    def _fail(self, e: BaseException) -> None:
+        self.failures += 1
+        self.degraded = True
+        log.error("migration failed (%s: %s); island %d continues without migration", type(e).__name__, e, self.rank)
 
     # ----------------------------------------------------------------- run --
     def run(self, generations: int) -> None:

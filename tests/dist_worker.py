@@ -42,5 +42,51 @@ def run(rank: int, world: int, port: int, topology: str, out_dir: str) -> None:
     dist.destroy_process_group()
 
 
+def run_faults(rank: int, world: int, port: int, out_dir: str) -> None:
+    """Forged migrants are re-scored, dropped batches are skipped, and an
+    island-model checkpoint resumes bit-exactly."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    import libpga_amd as pga
+    from libpga_amd.parallel import IslandModel, init_distributed
+    from libpga_amd.utils import load_model, save_model
+
+    init_distributed("gloo")
+    L = 64
+
+    def hook(buf, epoch):
+        if epoch == 1:  # forge: claim every migrant is perfect and zero its genes
+            k = model.k
+            buf[: k * model.rw] = 0
+            buf[k * model.rw:] = torch.tensor([1e9], dtype=torch.float32).view(torch.int32)
+            return True
+        return epoch != 2  # drop the second batch
+
+    ga = pga.GeneticAlgorithm(pga.models.OneMax(L), 128, seed=5, island=rank, device="cpu", elitism=1)
+    model = IslandModel(ga, migrate_every=4, migrate_pct=0.1, topology="ring", fault_hook=hook)
+    model.run(5)  # one migration (forged)
+    forged_ok = ga.best_score() <= L and bool((ga.scores == ga.genomes().sum(1).float()).all())
+    model.run(4)  # second migration (dropped)
+    dropped = model.dropped
+    model.fault_hook = None
+    model.run(3)
+    prefix = os.path.join(out_dir, "ckpt")
+    save_model(model, prefix)
+    model.run(10)
+    final = ga.rows.clone()
+    ga2 = pga.GeneticAlgorithm(pga.models.OneMax(L), 128, seed=5, island=rank, device="cpu", elitism=1)
+    model2 = IslandModel(ga2, migrate_every=4, migrate_pct=0.1, topology="ring")
+    meta = load_model(model2, prefix)
+    model2.run(10)
+    torch.save({"forged_ok": forged_ok, "dropped": dropped, "resume_equal": bool(torch.equal(final, ga2.rows)),
+                "gen": meta["generation"], "migrations": model.migrations, "migrations2": model2.migrations},
+               os.path.join(out_dir, f"fault_{rank}.pt"))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
 if __name__ == "__main__":
-    run(int(sys.argv[1]), int(sys.argv[2]), int(sys.argv[3]), sys.argv[4], sys.argv[5])
+    if sys.argv[4] == "faults":
+        run_faults(int(sys.argv[1]), int(sys.argv[2]), int(sys.argv[3]), sys.argv[5])
+    else:
+        run(int(sys.argv[1]), int(sys.argv[2]), int(sys.argv[3]), sys.argv[4], sys.argv[5])

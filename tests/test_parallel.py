@@ -19,6 +19,25 @@ def free_port() -> int:
     return p
 
 
+def spawn(world, mode, tmp_path):
+    port = free_port()
+    procs = [subprocess.Popen([sys.executable, os.path.join(HERE, "dist_worker.py"), str(r), str(world), str(port),
+                               mode, str(tmp_path)]) for r in range(world)]
+    for p in procs:
+        assert p.wait(timeout=300) == 0
+
+
+def test_migration_faults_and_resume(tmp_path):
+    spawn(2, "faults", tmp_path)
+    for r in range(2):
+        x = torch.load(tmp_path / f"fault_{r}.pt", weights_only=True)
+        assert x["forged_ok"], "forged migrant scores leaked into the population"
+        assert x["dropped"] == 1
+        assert x["gen"] == 12
+        assert x["resume_equal"], "island-model checkpoint did not resume bit-exactly"
+        assert x["migrations"] >= 3  # forged (accepted after re-scoring) + later epochs; the dropped one not counted
+
+
 def launch(world, topology, tmp_path):
     port = free_port()
     procs = [subprocess.Popen([sys.executable, os.path.join(HERE, "dist_worker.py"), str(r), str(world), str(port),
