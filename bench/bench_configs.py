@@ -1,0 +1,100 @@
+#!/usr/bin/env python3
+"""Every BASELINE.json config on one device, one JSON line each.
+
+    python bench/bench_configs.py [--only NAME ...] [--out FILE]
+
+Configs (BASELINE.md "Targets" table):
+  onemax64_cpu      OneMax 64-bit, pop=1024, CPU reference backend
+  onemax1024        OneMax 1024-bit, pop=1M, one GPU (the headline island)
+  rastrigin30       Rastrigin-30D float, pop=1M (blend + gaussian)
+  rastrigin30_rot   Rastrigin-30D rotated, pop=1M (fitness through MFMA tiles)
+  tsp256_ox / _pmx  TSP-256 permutation, pop=256K, OX / PMX crossover
+  e1_sum100_refops  reference example E1 (S=40000, L=100) with the reference's
+                    operators — the head-to-head against build/bench/refsem
+The 8-GPU island configs are bench.py under torchrun (the driver runs those).
+Each line: gens/s, evals/s, ms/gen, best fitness, effective HBM GB/s (the
+bytes one generation must move at minimum: read 2 parent rows + write 1
+child row + scores, divided by the time).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import libpga_amd as pga  # noqa: E402
+
+
+def make(name: str):
+    M = pga.models
+    if name == "onemax64_cpu":
+        return M.OneMax(64), 1024, "cpu", {}, 2000
+    if name == "onemax1024":
+        return M.OneMax(1024), 1 << 20, None, dict(elitism=1), 300
+    if name == "rastrigin30":
+        return M.Rastrigin(30), 1 << 20, None, dict(elitism=1), 200
+    if name == "rastrigin30_rot":
+        return M.Rastrigin(30, rotate=True, seed=1), 1 << 20, None, dict(elitism=1), 200
+    if name == "e1_sum100_refops":
+        # reference example E1 with the reference's own operators (binary tournament,
+        # uniform crossover, 1% single-gene reset): same algorithm as build/bench/refsem
+        return M.SumGenes(100), 40000, None, {}, 500
+    if name in ("tsp256_ox", "tsp256_pmx"):
+        g = torch.Generator().manual_seed(7)
+        xy = torch.rand(256, 2, generator=g)
+        d = torch.cdist(xy, xy)
+        xo = "ox" if name.endswith("ox") else "pmx"
+        return M.TSP(d), 1 << 18, None, dict(elitism=1, crossover=xo), 50
+    raise KeyError(name)
+
+
+NAMES = ["onemax64_cpu", "onemax1024", "rastrigin30", "rastrigin30_rot", "tsp256_ox", "tsp256_pmx", "e1_sum100_refops"]
+
+
+def run_one(name: str, steps_scale: float) -> dict:
+    problem, S, dev, kw, steps = make(name)
+    steps = max(5, int(steps * steps_scale))
+    if dev is None:
+        dev = "cuda" if torch.cuda.is_available() else "cpu"
+        if dev == "cpu":
+            S, steps = min(S, 4096), min(steps, 20)
+    ga = pga.GeneticAlgorithm(problem, S, seed=1, device=dev, **kw)
+    ga.run(max(2, steps // 10))
+    ga.synchronize()
+    t0 = time.perf_counter()
+    ga.run(steps)
+    ga.synchronize()
+    dt = time.perf_counter() - t0
+    row_bytes = int(ga.island.row_words) * 4
+    gens = steps / dt
+    min_bytes = S * (3 * row_bytes + 8)
+    return {"config": name, "device": dev if dev == "cpu" else torch.cuda.get_device_name(), "pop": S,
+            "length": problem.length, "encoding": problem.encoding, "gens_per_sec": gens, "evals_per_sec": gens * S,
+            "ms_per_gen": dt / steps * 1e3, "best": ga.best_score(), "steps": steps,
+            "effective_GBps": min_bytes * gens / 1e9}
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--only", nargs="*", default=None)
+    ap.add_argument("--scale", type=float, default=1.0, help="multiply the step counts")
+    ap.add_argument("--out", default=None)
+    a = ap.parse_args()
+    res = []
+    for n in (a.only or NAMES):
+        r = run_one(n, a.scale)
+        print(json.dumps(r), flush=True)
+        res.append(r)
+    if a.out:
+        with open(a.out, "w") as f:
+            json.dump(res, f, indent=1)
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

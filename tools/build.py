@@ -155,6 +155,14 @@ def write_ninja(opt: str, with_torch: bool) -> str:
         lines.append("build build/examples/gen_tsp: cc examples/gen_tsp.c")
         ex.append("build/examples/gen_tsp")
 
+    # reference-semantics baseline (bench/refsem.hip)
+    if os.path.exists(os.path.join(ROOT, "bench/refsem.hip")):
+        o = obj_path("bench/refsem.hip", "k")
+        lines.append(f"build {o}: hip bench/refsem.hip")
+        lines.append(f"build build/bench/refsem: link_exe {o}")
+        lines.append("  ldflags = ")
+        ex.append("build/bench/refsem")
+
     defaults = ["build/libpga.so", "build/libpga.a"] + ex
     if with_torch:
         inc, lib, abi = torch_paths()
