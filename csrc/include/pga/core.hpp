@@ -150,10 +150,19 @@ PGA_HD u32x4 draw(const RngKey& key, uint32_t stream, uint64_t ind, uint32_t blo
   return philox4x32_10(c, key.k0, key.k1);
 }
 
-PGA_HD uint32_t sel4(const u32x4& v, uint32_t i) {
-  return i == 0 ? v.x : (i == 1 ? v.y : (i == 2 ? v.z : v.w));
+// by value + value selects: a select over field REFERENCES becomes a select of
+// addresses, which forces the struct into scratch memory on the device
+PGA_HD uint32_t sel4(u32x4 v, uint32_t i) {
+  uint32_t r = v.w;
+  r = i == 2 ? v.z : r;
+  r = i == 1 ? v.y : r;
+  return i == 0 ? v.x : r;
 }
-PGA_HD uint32_t sel3(const u32x4& v, uint32_t i) { return i == 0 ? v.x : (i == 1 ? v.y : v.z); }
+PGA_HD uint32_t sel3(u32x4 v, uint32_t i) {
+  uint32_t r = v.z;
+  r = i == 1 ? v.y : r;
+  return i == 0 ? v.x : r;
+}
 
 // child word t (reference definition; kernels fetch it from the owner lane)
 PGA_HD uint32_t child_word(const RngKey& key, uint64_t child, uint32_t t) {

@@ -16,6 +16,20 @@ namespace pga {
 
 constexpr float kPi = 3.14159265358979323846f;
 
+// bitwise select: both operands are loaded unconditionally, so the device
+// compiler cannot turn "c ? A[j] : B[j]" into a load through a selected
+// address (which demotes the arrays to scratch memory)
+PGA_HD float fsel(bool c, float x, float y) {
+  uint32_t a, b;
+  __builtin_memcpy(&a, &x, 4);
+  __builtin_memcpy(&b, &y, 4);
+  const uint32_t m = 0u - (uint32_t)c;
+  const uint32_t r = (a & m) | (b & ~m);
+  float f;
+  __builtin_memcpy(&f, &r, 4);
+  return f;
+}
+
 PGA_HD float clampf(float x, float lo, float hi) { return x < lo ? lo : (x > hi ? hi : x); }
 // explicit fmaf everywhere a gene VALUE is produced: device (-ffp-contract=fast)
 // and host compilers then agree bit for bit on the rows
@@ -41,7 +55,7 @@ PGA_HD void real_cross_chunk(const GenArgs& a, uint64_t child, uint32_t c, const
   switch (a.crossover) {
     case XO_UNIFORM: {
       const uint32_t m = draw(a.key, ST_XO, child, c).x;  // low 4 bits: 1 = parent A
-      for (int j = 0; j < 4; ++j) v[j] = ((m >> j) & 1u) ? A[j] : B[j];
+      for (int j = 0; j < 4; ++j) v[j] = fsel((m >> j) & 1u, A[j], B[j]);
       break;
     }
     case XO_BLEND: {  // BLX-alpha: u in [-alpha, 1 + alpha] per gene
@@ -59,7 +73,7 @@ PGA_HD void real_cross_chunk(const GenArgs& a, uint64_t child, uint32_t c, const
     default:  // ONE_POINT / TWO_POINT over gene indices
       for (int j = 0; j < 4; ++j) {
         const uint32_t g = 4 * c + j;
-        v[j] = (g >= blo && g < bhi) ? B[j] : A[j];
+        v[j] = fsel(g >= blo && g < bhi, B[j], A[j]);
       }
       break;
   }
@@ -79,16 +93,16 @@ PGA_HD void real_mutate_chunk(const GenArgs& a, uint64_t child, uint32_t c, uint
     if (a.mutation == MUT_GAUSSIAN) {
       const float u1 = word_to_unit(r.x), u2 = word_to_unit(r.y);
       const float z = sqrtf(-2.f * logf(u1)) * cosf(2.f * kPi * u2);
-      const float old = pos == 0 ? v[0] : (pos == 1 ? v[1] : (pos == 2 ? v[2] : v[3]));
+      const float old = fsel(pos == 0, v[0], fsel(pos == 1, v[1], fsel(pos == 2, v[2], v[3])));
       x = clampf(fmaf(a.sigma, z, old), a.lo, a.hi);
     } else {
       x = unit_range(r.z, a.lo, a.hi);
     }
     // assign through a branch-free select (no runtime-indexed register array)
-    v[0] = pos == 0 ? x : v[0];
-    v[1] = pos == 1 ? x : v[1];
-    v[2] = pos == 2 ? x : v[2];
-    v[3] = pos == 3 ? x : v[3];
+    v[0] = fsel(pos == 0, x, v[0]);
+    v[1] = fsel(pos == 1, x, v[1]);
+    v[2] = fsel(pos == 2, x, v[2]);
+    v[3] = fsel(pos == 3, x, v[3]);
     ++n;
     pos += 1u + geom_skip(chunk_mut_extra(a.key, child, c, ne++), thr, kMutCap, a.mut_inv_log2_1mp);
   }

@@ -65,7 +65,10 @@ __host__ __device__ inline size_t real_lds_floats(uint32_t GS, uint32_t chunks, 
   return n;
 }
 
-template <int GS, int MODE, bool ROT>
+// UFN: the user-objective instantiation is the only one that contains the
+// indirect call (an indirect call forces a scratch stack and a conservative
+// register allocation on every instantiation that can reach it)
+template <int GS, int MODE, bool ROT, bool UFN>
 __global__ __launch_bounds__(kBlock) void real_kernel(GenArgs a, unsigned long long* best_parts) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   uint32_t* lds_thr = (uint32_t*)smem;
@@ -177,7 +180,7 @@ __global__ __launch_bounds__(kBlock) void real_kernel(GenArgs a, unsigned long l
         }
       }
       // padding genes of the last chunk stay zero
-      for (uint32_t j = clen; j < 4; ++j) v[j] = 0.f;
+      for (uint32_t j = 0; j < 4; ++j) v[j] = j < clen ? v[j] : 0.f;  // static indices: no scratch
       if (MODE != MODE_EVAL && have) nxt[child * rs + q] = make_float4(v[0], v[1], v[2], v[3]);
     }
 
@@ -219,7 +222,7 @@ __global__ __launch_bounds__(kBlock) void real_kernel(GenArgs a, unsigned long l
         __syncthreads();
       }
       if (valid && !elite) {
-        if (a.objective == OBJ_USER_FNPTR) {
+        if (UFN) {
           // reference ABI: obj_f(gene*, unsigned) on the child's genome (LDS row)
           float s = 0.f;
           if (q == 0) s = ((obj_fn_t)a.user_fn)(X + g * G.tw, L);
@@ -268,17 +271,14 @@ __global__ __launch_bounds__(kBlock) void real_kernel(GenArgs a, unsigned long l
   }
 }
 
-template <int GS, int MODE, bool ROT>
-uint32_t go(const GenArgs& a, unsigned long long* parts, hipStream_t s) {
-  const size_t lds = real_lds_floats(GS, a.chunks, ROT) * sizeof(float);
-  auto k = real_kernel<GS, MODE, ROT>;
-  static bool configured = false;  // one per instantiation
+template <typename K>
+uint32_t launch_occ(K k, uint32_t children_per_block, size_t lds, const GenArgs& a, unsigned long long* parts,
+                    hipStream_t s, bool& configured) {
   if (!configured) {
     PGA_HIP_CHECK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     configured = true;
   }
-  const uint32_t gpb = kBlock / GS;
-  uint64_t need = (a.S + gpb - 1) / gpb;
+  uint64_t need = (a.S + children_per_block - 1) / children_per_block;
   int per_cu = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)k, kBlock, lds) != hipSuccess || per_cu <= 0)
     per_cu = 1;
@@ -289,10 +289,294 @@ uint32_t go(const GenArgs& a, unsigned long long* parts, hipStream_t s) {
   return grid;
 }
 
+template <int GS, int MODE, bool ROT>
+uint32_t go(const GenArgs& a, unsigned long long* parts, hipStream_t s) {
+  const size_t lds = real_lds_floats(GS, a.chunks, ROT) * sizeof(float);
+  if (a.objective == OBJ_USER_FNPTR) {
+    static bool c1 = false;
+    return launch_occ(real_kernel<GS, MODE, false, true>, kBlock / GS, lds, a, parts, s, c1);
+  }
+  static bool c0 = false;  // one per instantiation
+  return launch_occ(real_kernel<GS, MODE, ROT, false>, kBlock / GS, lds, a, parts, s, c0);
+}
+
+
+// ---------------------------------------------------------------------------
+// Fast GEN path.  The generic kernel above walks one child per group per block
+// iteration through a strictly serial chain (pool draw -> 4 score loads ->
+// 2 parent-row loads -> crossover/mutation -> store -> objective), so with a
+// few waves per SIMD it is latency bound (rocprof: ~5.7 us per iteration,
+// 1.1 TB/s effective on Rastrigin-30D @ 1M).  Here every group carries U
+// children through each phase together: U x 4 tournament loads are in flight
+// at once, then U x 2 parent rows, then the U children are finished back to
+// back — U-fold memory-level parallelism per wave with no extra waves.
+// Semantics (RNG words, operators, elitism, MFMA order) are exactly the
+// generic kernel's, so rows stay bit-identical to the CPU reference.
+// Eligible: MODE_GEN, tournament-2 or random selection, built-in objectives
+// that need no neighbour dimension (not Rosenbrock without rotation, not
+// random-key TSP, not user fn-ptrs).
+template <int GS, int U, bool ROT>
+__global__ __launch_bounds__(kBlock) void real_gen_fast(GenArgs a, unsigned long long* best_parts) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  uint32_t* lds_thr = (uint32_t*)smem;
+  unsigned long long* lds_red = (unsigned long long*)(smem + 128);
+  uint32_t* lds_elite = (uint32_t*)(smem + 136);
+  constexpr uint32_t GPB = kBlock / GS;
+  constexpr uint32_t ROWS = GPB * U;
+  constexpr uint32_t XR = ROWS > 16 ? ROWS : 16;
+  constexpr uint32_t TW = (4 * GS > 16 ? 4 * GS : 16) + 1;
+  const uint32_t dp = ((4 * a.chunks + 15) / 16) * 16;
+  float* X = smem + kHdr;  // [XR][TW] shifted x (ROT)
+  float* Z = X + XR * TW;  // [XR][TW] rotated z (ROT)
+  float* MS = Z + XR * TW; // [dp][dp+1]
+
+  const uint32_t lane = lane_id();
+  const uint32_t q = lane & (GS - 1);
+  const uint32_t gbase = lane & ~(uint32_t)(GS - 1);
+  const uint32_t g = threadIdx.x / GS;
+  const uint64_t rs = a.row_words >> 2;
+  const float4* cur = (const float4*)a.cur;
+  float4* nxt = (float4*)a.next;
+  const uint32_t L = a.L;
+  const uint32_t S32 = (uint32_t)a.S;
+  const bool have = q < a.chunks;
+  const uint32_t qc = have ? q : a.chunks - 1;  // unconditional loads, clamped chunk
+  const uint32_t clen = have ? (L - 4 * q >= 4 ? 4u : L - 4 * q) : 0u;
+  const bool evals = a.objective != OBJ_NONE;
+  const bool tour2 = a.selection == SEL_TOURNAMENT;
+  const bool per_gene_mut = (a.mutation == MUT_GAUSSIAN || a.mutation == MUT_UNIFORM) && a.mut_rate > 0.f;
+  const bool reset_one = a.mutation == MUT_RESET_ONE;
+  const bool shift = (a.obj_i & 1) && a.obj_data2 && real_obj_rotatable(a.objective);
+
+  if (a.n_elite > 0 && a.elite_idx == nullptr && blockIdx.x == 0) {
+    unsigned long long b = block_reduce_parts(a.best_cur, a.n_best_cur, lds_red);
+    if (threadIdx.x == 0) *lds_elite = (uint32_t)best_index(b);
+  }
+  if (per_gene_mut)
+    for (uint32_t i = threadIdx.x; i < kMutCap; i += kBlock) lds_thr[i] = a.mut_thr[i];
+  if (ROT) {
+    for (uint32_t i = threadIdx.x; i < 2 * XR * TW; i += kBlock) X[i] = 0.f;
+    for (uint32_t i = threadIdx.x; i < dp * (dp + 1); i += kBlock) {
+      const uint32_t n = i / (dp + 1), k = i % (dp + 1);
+      MS[i] = (n < L && k < L) ? a.obj_data[n * L + k] : 0.f;
+    }
+  }
+  __syncthreads();
+
+  unsigned long long my_best = 0;
+  for (uint64_t base = (uint64_t)blockIdx.x * ROWS; base < a.S; base += (uint64_t)gridDim.x * ROWS) {
+    uint64_t ch[U];
+    u32x4 pw[U];
+    uint32_t pa[U], pb[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      ch[u] = base + u * GPB + g;
+      pw[u] = draw(a.key, ST_CHILD, ch[u], q);
+    }
+    // ---- phase 1: selection (all U x 4 score loads in flight together) ----
+    if (tour2) {
+      uint32_t i0[U], i1[U], i2[U], i3[U];
+      float s0[U], s1[U], s2[U], s3[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const Pool<GS> pool{pw[u], gbase};
+        i0[u] = word_to_index(pool.get(W_SEL + 0, a.key, ch[u]), S32);
+        i1[u] = word_to_index(pool.get(W_SEL + 1, a.key, ch[u]), S32);
+        i2[u] = word_to_index(pool.get(W_SEL + 2, a.key, ch[u]), S32);
+        i3[u] = word_to_index(pool.get(W_SEL + 3, a.key, ch[u]), S32);
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        s0[u] = a.score_cur[i0[u]];
+        s1[u] = a.score_cur[i1[u]];
+        s2[u] = a.score_cur[i2[u]];
+        s3[u] = a.score_cur[i3[u]];
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        pa[u] = (s0[u] < s1[u]) ? i1[u] : i0[u];
+        pb[u] = (s2[u] < s3[u]) ? i3[u] : i2[u];
+      }
+    } else {
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const Pool<GS> pool{pw[u], gbase};
+        pa[u] = word_to_index(pool.get(W_SEL + 0, a.key, ch[u]), S32);
+        pb[u] = word_to_index(pool.get(W_SEL + 1, a.key, ch[u]), S32);
+      }
+    }
+    bool el[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      el[u] = ch[u] < a.n_elite;
+      if (el[u]) {
+        pa[u] = a.elite_idx ? a.elite_idx[ch[u]] : *lds_elite;
+        pb[u] = pa[u];
+      }
+    }
+    // ---- phase 2: parent rows (U x 2 dwordx4 loads in flight) ----
+    float4 A4[U], B4[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      A4[u] = cur[(uint64_t)pa[u] * rs + qc];
+      B4[u] = cur[(uint64_t)pb[u] * rs + qc];
+    }
+    // ---- phase 3: variation + store ----
+    float v[U][4];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const float A[4] = {A4[u].x, A4[u].y, A4[u].z, A4[u].w}, B[4] = {B4[u].x, B4[u].y, B4[u].z, B4[u].w};
+      if (el[u]) {
+        for (int j = 0; j < 4; ++j) v[u][j] = A[j];
+      } else {
+        const Pool<GS> pool{pw[u], gbase};
+        const bool xo = a.crossover != XO_NONE && do_crossover(a, pool.get(W_XOPROB, a.key, ch[u]));
+        uint32_t blo = 0, bhi = 0;
+        float ua = 0.f;
+        if (a.crossover == XO_ONE_POINT) {
+          blo = word_to_index(pool.get(W_CUT1, a.key, ch[u]), L);
+          bhi = L;
+        } else if (a.crossover == XO_TWO_POINT) {
+          const uint32_t c1 = word_to_index(pool.get(W_CUT1, a.key, ch[u]), L);
+          const uint32_t c2 = word_to_index(pool.get(W_CUT2, a.key, ch[u]), L);
+          blo = c1 < c2 ? c1 : c2;
+          bhi = c1 < c2 ? c2 : c1;
+        } else if (a.crossover == XO_ARITHMETIC) {
+          ua = word_to_unit(pool.get(W_CUT1, a.key, ch[u]));
+        }
+        real_cross_chunk(a, ch[u], q, A, B, xo, blo, bhi, ua, v[u]);
+        if (per_gene_mut) {
+          if (have) real_mutate_chunk(a, ch[u], q, clen, pw[u].w, lds_thr, v[u]);
+        } else if (reset_one && pool.get(W_MUTIND, a.key, ch[u]) < a.mut_ind_thresh) {
+          const uint32_t pos = word_to_index(pool.get(W_MUTPOS, a.key, ch[u]), L);
+          const float x = real_reset_value(a, pool.get(W_SEL + sel_words(a), a.key, ch[u]));
+          if ((pos >> 2) == q) {
+            const uint32_t j = pos & 3u;
+            v[u][0] = j == 0 ? x : v[u][0];
+            v[u][1] = j == 1 ? x : v[u][1];
+            v[u][2] = j == 2 ? x : v[u][2];
+            v[u][3] = j == 3 ? x : v[u][3];
+          }
+        }
+      }
+      for (uint32_t j = 0; j < 4; ++j) v[u][j] = j < clen ? v[u][j] : 0.f;
+      if (ch[u] < a.S && have) nxt[ch[u] * rs + q] = make_float4(v[u][0], v[u][1], v[u][2], v[u][3]);
+    }
+    if (!evals) continue;
+    // ---- phase 4: objective (rotated: one MFMA pass over the U*GPB-row tile) ----
+    float z[U][4];
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      for (int j = 0; j < 4; ++j) {
+        const uint32_t d = 4 * q + j;
+        z[u][j] = d < L ? ((shift) ? v[u][j] - a.obj_data2[d] : v[u][j]) : 0.f;
+      }
+    if (ROT) {
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        float* row = X + (u * GPB + g) * TW + 4 * q;
+        row[0] = z[u][0]; row[1] = z[u][1]; row[2] = z[u][2]; row[3] = z[u][3];
+      }
+      __syncthreads();
+      const uint32_t w = threadIdx.x >> 6;
+      const uint32_t nct = dp / 16;
+      for (uint32_t t = w; t < (XR / 16) * nct; t += kBlock / 64) {
+        const uint32_t rt = t / nct, ct = t % nct;
+        floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+        const float* xa = X + (rt * 16 + (lane & 15)) * TW + (lane >> 4);
+        const float* mb = MS + (ct * 16 + (lane & 15)) * (dp + 1) + (lane >> 4);
+        for (uint32_t k0 = 0; k0 < dp; k0 += 4) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(xa[k0], mb[k0], acc, 0, 0, 0);
+        float* zo = Z + (rt * 16 + (lane >> 4) * 4) * TW + ct * 16 + (lane & 15);
+        zo[0] = acc[0];
+        zo[TW] = acc[1];
+        zo[2 * TW] = acc[2];
+        zo[3 * TW] = acc[3];
+      }
+      __syncthreads();
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      float score;
+      if (el[u]) {
+        score = a.score_cur[pa[u]];
+      } else {
+        RealAcc acc{0.f, 0.f, 1.f};
+        const float* zrow = Z + (u * GPB + g) * TW + 4 * q;
+        for (uint32_t j = 0; j < 4; ++j) {
+          const uint32_t d = 4 * q + j;
+          if (d < L) {
+            const float zj = ROT ? zrow[j] : z[u][j];
+            const float zn = ROT ? zrow[j + 1] : 0.f;  // Rosenbrock only reaches here rotated
+            real_obj_term(a, d, zj, zn, v[u][j], acc);
+          }
+        }
+        acc.s0 = group_sum<GS>(acc.s0);
+        acc.s1 = group_sum<GS>(acc.s1);
+        acc.s2 = group_prod<GS>(acc.s2);
+        score = real_obj_finish(a, acc);
+      }
+      if (ch[u] < a.S && q == 0) {
+        a.score_next[ch[u]] = score;
+        const unsigned long long pb2 = pack_best(score, ch[u]);
+        my_best = pb2 > my_best ? pb2 : my_best;
+      }
+    }
+    if (ROT) __syncthreads();  // X/Z are rewritten next iteration
+  }
+  if (evals && best_parts) {
+    unsigned long long b = block_max_u64(my_best, lds_red);
+    if (threadIdx.x == 0) best_parts[blockIdx.x] = b;
+  }
+}
+
+template <int GS, int U, bool ROT>
+uint32_t go_fast(const GenArgs& a, unsigned long long* parts, hipStream_t s) {
+  constexpr uint32_t ROWS = (kBlock / GS) * U;
+  constexpr uint32_t XR = ROWS > 16 ? ROWS : 16;
+  constexpr uint32_t TW = (4 * GS > 16 ? 4 * GS : 16) + 1;
+  const uint32_t dp = ((4 * a.chunks + 15) / 16) * 16;
+  const size_t lds = (kHdr + (ROT ? 2 * XR * TW + (size_t)dp * (dp + 1) : 0)) * sizeof(float);
+  static bool c = false;
+  return launch_occ(real_gen_fast<GS, U, ROT>, ROWS, lds, a, parts, s, c);
+}
+
+// PGA_REAL_FAST=0 forces the generic kernel; PGA_REAL_U = 1|2|4 children per group
+int real_fast_u() {
+  static int v = -2;
+  if (v == -2) {
+    const char* e = getenv("PGA_REAL_FAST");
+    const char* u = getenv("PGA_REAL_U");
+    v = (e && e[0] == '0') ? 0 : (u ? atoi(u) : 1);
+    if (v != 0 && v != 1 && v != 2 && v != 4) v = 1;
+  }
+  return v;
+}
+
+bool real_fast_eligible(int mode, const GenArgs& a, bool rot) {
+  if (mode != MODE_GEN || real_fast_u() == 0) return false;
+  if (a.objective == OBJ_USER_FNPTR || a.objective == OBJ_TSP_RANDOM_KEY) return false;
+  if (a.objective == OBJ_ROSENBROCK && !rot) return false;
+  if (!(a.selection == SEL_RANDOM || (a.selection == SEL_TOURNAMENT && a.tour_k == 2))) return false;
+  if (a.n_elite > 1 && a.elite_idx == nullptr) return false;
+  return true;
+}
+
+template <int GS, bool ROT>
+uint32_t launch_fast(const GenArgs& a, unsigned long long* parts, hipStream_t s) {
+  switch (real_fast_u()) {
+    case 1: return go_fast<GS, 1, ROT>(a, parts, s);
+    case 4: return go_fast<GS, 4, ROT>(a, parts, s);
+    case 2: return go_fast<GS, 2, ROT>(a, parts, s);
+    default: return go_fast<GS, 1, ROT>(a, parts, s);
+  }
+}
+
 template <int GS, bool ROT>
 uint32_t launch_mode(int mode, const GenArgs& a, unsigned long long* parts, hipStream_t s) {
   switch (mode) {
-    case MODE_GEN: return go<GS, MODE_GEN, ROT>(a, parts, s);
+    case MODE_GEN:
+      if (real_fast_eligible(mode, a, ROT)) return launch_fast<GS, ROT>(a, parts, s);
+      return go<GS, MODE_GEN, ROT>(a, parts, s);
     case MODE_INIT: return go<GS, MODE_INIT, ROT>(a, parts, s);
     case MODE_EVAL: return go<GS, MODE_EVAL, ROT>(a, parts, s);
     case MODE_CROSS: return go<GS, MODE_CROSS, false>(a, parts, s);
