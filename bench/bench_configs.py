@@ -11,6 +11,8 @@ Configs (BASELINE.md "Targets" table):
   tsp256_ox / _pmx  TSP-256 permutation, pop=256K, OX / PMX crossover
   e1_sum100_refops  reference example E1 (S=40000, L=100) with the reference's
                     operators — the head-to-head against build/bench/refsem
+  e2_knap_refops    reference example E2 (S=100, L=6), launch-bound (hipGraph)
+  onemax64_gpu      OneMax 64-bit, pop=1024 on the GPU (launch-bound)
 The 8-GPU island configs are bench.py under torchrun (the driver runs those).
 Each line: gens/s, evals/s, ms/gen, best fitness, effective HBM GB/s (the
 bytes one generation must move at minimum: read 2 parent rows + write 1
@@ -44,6 +46,11 @@ def make(name: str):
         # reference example E1 with the reference's own operators (binary tournament,
         # uniform crossover, 1% single-gene reset): same algorithm as build/bench/refsem
         return M.SumGenes(100), 40000, None, {}, 500
+    if name == "e2_knap_refops":
+        # reference example E2 (S=100, L=6): launch-bound, the hipGraph replay case
+        return M.ReferenceKnapsack(), 100, None, {}, 5000
+    if name == "onemax64_gpu":
+        return M.OneMax(64), 1024, None, {}, 5000
     if name in ("tsp256_ox", "tsp256_pmx"):
         g = torch.Generator().manual_seed(7)
         xy = torch.rand(256, 2, generator=g)
@@ -53,7 +60,8 @@ def make(name: str):
     raise KeyError(name)
 
 
-NAMES = ["onemax64_cpu", "onemax1024", "rastrigin30", "rastrigin30_rot", "tsp256_ox", "tsp256_pmx", "e1_sum100_refops"]
+NAMES = ["onemax64_cpu", "onemax1024", "rastrigin30", "rastrigin30_rot", "tsp256_ox", "tsp256_pmx", "e1_sum100_refops",
+         "e2_knap_refops", "onemax64_gpu"]
 
 
 def run_one(name: str, steps_scale: float) -> dict:

@@ -60,12 +60,15 @@ Island::Island(const Config& cfg, int device) : cfg_(cfg), device_(device) {
     last_mask_ = u32x4{~0u, ~0u, ~0u, ~0u};
   }
   set_operators(cfg_);
+  if (const char* e = std::getenv("PGA_GRAPH")) set_graph_generations((uint32_t)std::strtoul(e, nullptr, 10));
 }
 
 Island::~Island() {
   Buffer* all[] = {&rows_[0],   &rows_[1],     &scores_[0],   &scores_[1],  &best_[0],  &best_[1],   &mut_thr_,
                    &obj_data_[0], &obj_data_[1], &keys_[0], &keys_[1], &elite_idx_, &cumfit_, &cum_ws_, &topk_ws_, &stats_,
-                   &out_best_,  &scratch_, &compat_rand_, &ev_parts_};
+                   &out_best_,  &scratch_, &compat_rand_, &ev_parts_, &gen_dev_};
+  drop_graph();
+  if (cap_stream_) (void)hipStreamDestroy(cap_stream_);
   for (Buffer* b : all) {
     try {
       release(*b);
@@ -139,6 +142,7 @@ void Island::rebuild_mut_table() {
 }
 
 void Island::set_operators(const Config& c) {
+  invalidate();
   if (c.S != cfg_.S || c.L != cfg_.L || c.encoding != cfg_.encoding)
     throw std::invalid_argument("set_operators cannot change S, L or encoding");
   if (c.selection == SEL_TOURNAMENT && (c.tour_k < 1 || c.tour_k > 64))
@@ -159,6 +163,7 @@ void Island::set_operators(const Config& c) {
 }
 
 void Island::set_user_operators(void* xo, void* mut) {
+  invalidate();
   if ((xo || mut) && !on_gpu()) throw std::invalid_argument("device function pointers need the GPU backend");
   if ((xo || mut) && cfg_.encoding != ENC_REAL)
     throw std::invalid_argument("user crossover/mutate callbacks need the REAL (float gene) encoding");
@@ -168,6 +173,7 @@ void Island::set_user_operators(void* xo, void* mut) {
 }
 
 void Island::set_objective_data(const float* host, size_t n, int which) {
+  invalidate();
   if (which < 0 || which > 1) throw std::invalid_argument("objective data slot must be 0 or 1");
   if (on_gpu()) synchronize();
   release(obj_data_[which]);
@@ -230,6 +236,10 @@ GenArgs Island::make_args(int mode) {
   a.best_cur = (const unsigned long long*)best_[cur_].ptr;
   a.n_best_cur = n_best_[cur_];
   a.last_mask = last_mask_;
+  if (capturing_) {
+    a.gen_dev = (const uint32_t*)gen_dev_.ptr;
+    a.gen_off = gen_ - capture_base_;
+  }
   if (integer_objective(cfg_.objective, cfg_.L)) {
     a.key_cur = (const uint16_t*)keys_[cur_].ptr;
     a.key_next = (uint16_t*)keys_[nx].ptr;
@@ -278,6 +288,22 @@ void Island::prepare_generation() {
 
 void Island::run(uint32_t n) {
   TraceRange tr("pga.run");
+  if (on_gpu() && graph_g_ > 0 && !graph_broken_ && n >= graph_g_ + 2) {
+    const bool fresh = gexec_ && g_cur_ == cur_ && g_epoch_ == epoch_ && g_version_ == version_ &&
+                       g_nbest_ == n_best_[cur_] && g_len_ == graph_g_;
+    if (!fresh) {
+      // two plain generations first: the best-partials count of this parity
+      // then equals the GEN kernel's grid, which is what every replay leaves
+      run_plain(2);
+      n -= 2;
+    }
+    const uint32_t reps = n / graph_g_;
+    if (run_graph(reps, fresh)) n -= reps * graph_g_;
+  }
+  run_plain(n);
+}
+
+void Island::run_plain(uint32_t n) {
   for (uint32_t i = 0; i < n; ++i) {
     TraceRange tg("pga.generation", 2);
     prepare_generation();
@@ -398,6 +424,78 @@ bool Island::evaluate_rows(void* rows, float* scores, uint32_t n) {
   a.n_elite = 0;
   a.elite_idx = nullptr;
   launch(MODE_EVAL, a, (unsigned long long*)ev_parts_.ptr);
+  return true;
+}
+
+// ------------------------------------------------------------ hipGraph ---
+void Island::set_graph_generations(uint32_t g) {
+  if (g % 2) ++g;  // even: the graph must end on the parity it started from
+  graph_g_ = g;
+  drop_graph();
+}
+
+void Island::drop_graph() {
+  if (gexec_) (void)hipGraphExecDestroy(gexec_);
+  gexec_ = nullptr;
+  g_cur_ = -1;
+}
+
+bool Island::capture_graph() {
+  drop_graph();
+  if (!gen_dev_.ptr) gen_dev_ = alloc(64);
+  if (!cap_stream_) PGA_HIP_CHECK(hipStreamCreateWithFlags(&cap_stream_, hipStreamNonBlocking));
+  // workspaces that a stage would otherwise (re)allocate synchronously
+  if (cfg_.n_elite > 1) {
+    const size_t need = topk_workspace_bytes(cfg_.S, cfg_.n_elite);
+    if (topk_ws_.bytes < need) {
+      synchronize();
+      release(topk_ws_);
+      topk_ws_ = alloc(need);
+    }
+  }
+  const int cur0 = cur_;
+  const uint32_t gen0 = gen_, nb0 = n_best_[cur_];
+  hipStream_t user = stream;
+  stream = cap_stream_;
+  capturing_ = true;
+  capture_base_ = gen_;
+  hipGraph_t graph = nullptr;
+  bool ok = hipStreamBeginCapture(cap_stream_, hipStreamCaptureModeThreadLocal) == hipSuccess;
+  if (ok) {
+    try {
+      run_plain(graph_g_);
+      advance_counter_launch((uint32_t*)gen_dev_.ptr, graph_g_, cap_stream_);
+    } catch (...) {
+      ok = false;
+    }
+    ok = (hipStreamEndCapture(cap_stream_, &graph) == hipSuccess) && ok && graph;
+  }
+  capturing_ = false;
+  stream = user;
+  gen_ = gen0;  // the captured launches ran nothing: restore the host view
+  if (cur_ != cur0) cur_ = cur0;
+  if (ok) ok = hipGraphInstantiate(&gexec_, graph, nullptr, nullptr, 0) == hipSuccess;
+  if (graph) (void)hipGraphDestroy(graph);
+  if (!ok) {
+    (void)hipGetLastError();
+    gexec_ = nullptr;
+    graph_broken_ = true;  // fall back to plain launches for good
+    return false;
+  }
+  g_cur_ = cur0;
+  g_epoch_ = epoch_;
+  g_version_ = version_;
+  g_nbest_ = nb0;
+  g_len_ = graph_g_;
+  return true;
+}
+
+bool Island::run_graph(uint32_t reps, bool fresh) {
+  if (!fresh && !capture_graph()) return false;
+  PGA_HIP_CHECK(hipMemsetD32Async((hipDeviceptr_t)gen_dev_.ptr, (int)gen_, 1, stream));
+  for (uint32_t r = 0; r < reps; ++r) PGA_HIP_CHECK(hipGraphLaunch(gexec_, stream));
+  gen_ += reps * graph_g_;
+  graph_replays_ += reps;
   return true;
 }
 

@@ -281,6 +281,12 @@ struct GenArgs {
 
   // padding mask for the last chunk (BINARY)
   u32x4 last_mask;
+
+  // hipGraph replay: when set, the generation counter is read from device
+  // memory (key.gen = *gen_dev + gen_off) so one captured graph of G
+  // generations can be replayed without re-recording kernel arguments
+  const uint32_t* gen_dev;
+  uint32_t gen_off;
 };
 
 PGA_HD uint32_t sel_words(const GenArgs& a) {

@@ -94,6 +94,11 @@ __device__ __forceinline__ uint32_t roulette_pick(const float* cumfit, uint32_t 
   return lo;
 }
 
+// graph replay: take the generation from the device counter (see GenArgs)
+__device__ __forceinline__ void resolve_gen(GenArgs& a) {
+  if (a.gen_dev) a.key.gen = *a.gen_dev + a.gen_off;
+}
+
 // Pick two parents.  All selection words are group-uniform.
 template <int GS>
 __device__ __forceinline__ void select_parents(const GenArgs& a, const Pool<GS>& pool, uint64_t child,

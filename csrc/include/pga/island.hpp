@@ -74,7 +74,10 @@ class Island {
   // ---- configuration (may be changed between generations) ----
   void set_operators(const Config& c);  // selection/crossover/mutation/objective scalars
   void set_objective_data(const float* host, size_t n, int which);  // which = 0 or 1
-  void set_user_fn(void* f) { user_fn_ = f; }
+  void set_user_fn(void* f) {
+    user_fn_ = f;
+    invalidate();
+  }
   // reference-ABI crossover_f / mutate_f device pointers (nullptr = built-in)
   void set_user_operators(void* xo, void* mut);
 
@@ -114,6 +117,17 @@ class Island {
   // scratch buffers for callers (migration staging)
   void* scratch(size_t bytes);
 
+  // hipGraph replay: run() records G generations once per (parity, epoch,
+  // configuration) and replays the graph; 0 disables.  Default: PGA_GRAPH
+  // env (generations per graph), else 0.  Bit-identical to plain launches.
+  // Off by default because it measured no gain on MI355X: even the smallest
+  // populations (S=100) are bound by the kernel's own dependent memory chain
+  // (~4.8 us/gen with or without the graph), not by host launch cost
+  // (profiles/README.md).
+  void set_graph_generations(uint32_t g);
+  uint32_t graph_generations() const { return graph_g_; }
+  uint64_t graph_replays() const { return graph_replays_; }
+
   // checkpoint: header + current rows + scores
   void save(const std::string& path);
   void load(const std::string& path);
@@ -146,6 +160,22 @@ class Island {
   void* user_mut_fn_ = nullptr;
   Buffer compat_rand_, ev_parts_;
   u32x4 last_mask_{0, 0, 0, 0};
+
+  // graph replay state
+  void run_plain(uint32_t n);
+  bool run_graph(uint32_t reps, bool fresh);
+  bool capture_graph();
+  void drop_graph();
+  void invalidate() { ++version_; }
+  uint32_t graph_g_ = 0, version_ = 0;
+  bool graph_broken_ = false, capturing_ = false;
+  uint32_t capture_base_ = 0;
+  Buffer gen_dev_;
+  hipStream_t cap_stream_ = nullptr;
+  hipGraphExec_t gexec_ = nullptr;
+  int g_cur_ = -1;
+  uint32_t g_epoch_ = 0, g_version_ = 0, g_nbest_ = 0, g_len_ = 0;
+  uint64_t graph_replays_ = 0;
 };
 
 }  // namespace pga

@@ -63,6 +63,8 @@ void reduce_best_launch(const unsigned long long* parts, uint32_t n, unsigned lo
 uint32_t best_of_scores_launch(const float* scores, uint64_t S, unsigned long long* parts, hipStream_t s);
 // keys[i] = (uint16)scores[i] (integer objectives' tournament keys)
 void scores_to_keys_launch(const float* scores, uint64_t S, uint16_t* keys, hipStream_t s);
+// *counter += delta (graph replay: the device-resident generation counter)
+void advance_counter_launch(uint32_t* counter, uint32_t delta, hipStream_t s);
 // stats[0..3] = {min, max, sum, count} of scores (count as float)
 void score_stats_launch(const float* scores, uint64_t S, float* stats, hipStream_t s);
 // roulette: cumfit = inclusive prefix sum of max(score - min, 0); workspace >= 2*kMaxGrid floats

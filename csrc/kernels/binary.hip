@@ -133,6 +133,7 @@ __device__ __forceinline__ uint32_t chunk_len(uint32_t L, uint32_t c) {
 // ---------------------------------------------------------------------------
 template <int GS, int OBJ, int MODE>
 __global__ __launch_bounds__(kBlock) void binary_kernel(GenArgs a, unsigned long long* best_parts) {
+  resolve_gen(a);
   __shared__ unsigned long long lds_red[kBlock / 64];
   __shared__ uint32_t lds_elite;
   __shared__ uint32_t lds_thr[kMutCap];
@@ -285,6 +286,7 @@ __device__ __forceinline__ uint4 load_row(const uint4* p) {
 
 template <int GS, int OBJ, int XOK, bool KEY>
 __global__ __launch_bounds__(kBlock) void binary_gen_pipe(GenArgs a, unsigned long long* best_parts) {
+  resolve_gen(a);
   __shared__ unsigned long long lds_red[kBlock / 64];
   __shared__ uint32_t lds_elite;
   __shared__ uint32_t lds_thr[kMutCap];

@@ -57,6 +57,7 @@ __device__ __forceinline__ void fill_rand(const GenArgs& a, uint64_t child, uint
 
 template <int MODE>
 __global__ __launch_bounds__(kBlock) void compat_kernel(GenArgs a, unsigned long long* best_parts) {
+  resolve_gen(a);
   __shared__ unsigned long long lds_red[kBlock / 64];
   __shared__ uint32_t lds_elite;
   const uint32_t L = a.L;

@@ -56,6 +56,7 @@ __device__ __forceinline__ void ld8(const uint16_t* p, uint32_t e[8]) {
 
 template <int GS, int MODE, int OBJ>
 __global__ __launch_bounds__(kBlock) void perm_kernel(GenArgs a, unsigned long long* best_parts) {
+  resolve_gen(a);
   extern __shared__ __attribute__((aligned(16))) float smem[];
   unsigned long long* lds_red = (unsigned long long*)smem;
   uint32_t* lds_elite = (uint32_t*)(smem + 8);

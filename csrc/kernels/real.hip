@@ -70,6 +70,7 @@ __host__ __device__ inline size_t real_lds_floats(uint32_t GS, uint32_t chunks, 
 // register allocation on every instantiation that can reach it)
 template <int GS, int MODE, bool ROT, bool UFN>
 __global__ __launch_bounds__(kBlock) void real_kernel(GenArgs a, unsigned long long* best_parts) {
+  resolve_gen(a);
   extern __shared__ __attribute__((aligned(16))) float smem[];
   uint32_t* lds_thr = (uint32_t*)smem;
   unsigned long long* lds_red = (unsigned long long*)(smem + 128);
@@ -317,6 +318,7 @@ uint32_t go(const GenArgs& a, unsigned long long* parts, hipStream_t s) {
 // random-key TSP, not user fn-ptrs).
 template <int GS, int U, bool ROT>
 __global__ __launch_bounds__(kBlock) void real_gen_fast(GenArgs a, unsigned long long* best_parts) {
+  resolve_gen(a);
   extern __shared__ __attribute__((aligned(16))) float smem[];
   uint32_t* lds_thr = (uint32_t*)smem;
   unsigned long long* lds_red = (unsigned long long*)(smem + 128);

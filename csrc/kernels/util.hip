@@ -392,7 +392,16 @@ __global__ __launch_bounds__(kBlock) void scores_to_keys_kernel(const float* s, 
 
 inline size_t align_up(size_t x) { return (x + 255) & ~(size_t)255; }
 
+__global__ void advance_counter_kernel(uint32_t* c, uint32_t d) {
+  if (threadIdx.x == 0) *c += d;
+}
+
 }  // namespace
+
+void advance_counter_launch(uint32_t* counter, uint32_t delta, hipStream_t s) {
+  hipLaunchKernelGGL(advance_counter_kernel, 1, 64, 0, s, counter, delta);
+  PGA_HIP_CHECK(hipGetLastError());
+}
 
 void reduce_best_launch(const unsigned long long* parts, uint32_t n, unsigned long long* out, hipStream_t s) {
   hipLaunchKernelGGL(reduce_best_kernel, 1, kBlock, 0, s, parts, n, out);

@@ -113,6 +113,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def_property("generation", &Island::generation, &Island::set_generation)
       .def_property_readonly("epoch", &Island::epoch)
       .def("bump_epoch", &Island::bump_epoch)
+      .def_property("graph_generations", &Island::graph_generations, &Island::set_graph_generations)
+      .def_property_readonly("graph_replays", &Island::graph_replays)
       .def("config", [](Island& i) { return i.config(); })
       .def("set_operators", [](Island& i, const pga::Config& c) { bind_stream(i); i.set_operators(c); })
       .def("set_objective_data",
