@@ -38,6 +38,12 @@
 struct pga_population {
   std::unique_ptr<pga::Island> isl;
   pga_t* owner = nullptr;
+  hipStream_t stream = nullptr;  // own stream: islands of pga_run_islands evolve concurrently
+  hipEvent_t done = nullptr;
+  ~pga_population() {
+    if (done) (void)hipEventDestroy(done);
+    if (stream) (void)hipStreamDestroy(stream);
+  }
   int builtin = -1;  // built-in objective id, -1: the pga-level obj_f callback
 };
 
@@ -572,15 +578,56 @@ void pga_run(pga_t* p, unsigned n) {
   });
 }
 
+// Islands evolve concurrently, one HIP stream each, between migration points;
+// a migration joins them on the solver stream (events), exchanges, and forks
+// them again.  Small islands are launch/latency bound, so running them side by
+// side on the 256 CUs is what makes many-island runs cheap on one MI355X.
+namespace {
+void fork_islands(pga_t* p) {
+  hipEvent_t ev;
+  PGA_HIP_CHECK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+  PGA_HIP_CHECK(hipEventRecord(ev, p->stream));
+  for (population_t* pop : p->pops) {
+    if (!pop->stream) {
+      PGA_HIP_CHECK(hipStreamCreateWithFlags(&pop->stream, hipStreamNonBlocking));
+      PGA_HIP_CHECK(hipEventCreateWithFlags(&pop->done, hipEventDisableTiming));
+    }
+    PGA_HIP_CHECK(hipStreamWaitEvent(pop->stream, ev, 0));
+    pop->isl->stream = pop->stream;
+  }
+  PGA_HIP_CHECK(hipEventDestroy(ev));
+}
+
+void join_islands(pga_t* p) {
+  for (population_t* pop : p->pops) {
+    PGA_HIP_CHECK(hipEventRecord(pop->done, pop->stream));
+    PGA_HIP_CHECK(hipStreamWaitEvent(p->stream, pop->done, 0));
+    pop->isl->stream = p->stream;
+  }
+}
+}  // namespace
+
 void pga_run_islands(pga_t* p, unsigned n, unsigned m, float pct) {
   if (!p || p->pops.empty()) return;
   guard(p, [&]() {
+    const bool gpu = p->device >= 0;
     for (population_t* pop : p->pops) {
       sync_callbacks(p, pop);
+      pop->isl->stream = p->stream;
       pop->isl->evaluate();
     }
-    for (unsigned g = 1; g <= n; ++g) {
-      for (population_t* pop : p->pops) pop->isl->run(1);
+    unsigned g = 0;
+    while (g < n) {
+      // generations until the next migration point (or the end)
+      unsigned step = n - g;
+      if (m > 0) {
+        const unsigned next = (g / m + 1) * m;
+        if (next < n) step = next - g;
+      }
+      if (gpu) fork_islands(p);
+      for (population_t* pop : p->pops) pop->isl->run(step);
+      if (gpu) join_islands(p);
+      g += step;
       if (m > 0 && g % m == 0 && g < n) {
         pga_migrate(p, pct);
         migrate_ranks(p, pct);

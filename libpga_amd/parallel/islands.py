@@ -236,11 +236,17 @@ class IslandModel:
         log.error("migration failed (%s: %s); island %d continues without migration", type(e).__name__, e, self.rank)
 
     # ----------------------------------------------------------------- run --
-    def run(self, generations: int) -> None:
+    def run(self, generations: int, *, target: Optional[float] = None, check_every: int = 0) -> int:
         """Run ``generations`` generations with periodic migration.
 
         Generation counting is global (``ga.generation``), so a run split into
-        several calls migrates at the same generations as one long call."""
+        several calls migrates at the same generations as one long call.
+        With ``target``, every ``check_every`` generations (default: the
+        migration interval) the islands agree on the global best with one
+        all-reduce(max) and all stop together once it reaches ``target``.
+        Returns the generations executed."""
+        every = check_every or self.migrate_every or 1
+        done = 0
         for _ in range(int(generations)):
             g = self.ga.generation
             if self.migrate_every > 0 and g > 0 and g % self.migrate_every == 0 and self._pending is None:
@@ -252,6 +258,10 @@ class IslandModel:
                 self.ga._custom_eval()
             if self._pending is not None:
                 self.finish_migration()
+            done += 1
+            if target is not None and self.ga.generation % every == 0 and self.global_reduce_best() >= target:
+                break
+        return done
 
     def flush(self) -> None:
         self.finish_migration()

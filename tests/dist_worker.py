@@ -32,11 +32,15 @@ def run(rank: int, world: int, port: int, topology: str, out_dir: str) -> None:
                 "scores_after": ga.scores.clone(), "send_best": float(send_scores.max())},
                os.path.join(out_dir, f"mig_{rank}.pt"))
     model.run(40)
+    # early stop: every island stops at the same generation once the global best reaches the target
+    tgt = model.global_reduce_best()
+    ran = model.run(50, target=tgt, check_every=5)
+    assert ran == 5, ran
     score, owner, genome = model.global_best()
     gmax = model.global_reduce_best()
     torch.save({"rank": rank, "b0": b0, "best": ga.best_score(), "global": score, "owner": owner,
                 "gmax": gmax, "genome_sum": float(genome.sum()), "migrations": model.migrations,
-                "gen": ga.generation},
+                "gen": ga.generation - 5},
                os.path.join(out_dir, f"res_{rank}.pt"))
     dist.barrier()
     dist.destroy_process_group()
