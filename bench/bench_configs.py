@@ -13,6 +13,7 @@ Configs (BASELINE.md "Targets" table):
                     operators — the head-to-head against build/bench/refsem
   e2_knap_refops    reference example E2 (S=100, L=6), launch-bound (hipGraph)
   onemax64_gpu      OneMax 64-bit, pop=1024 on the GPU (launch-bound)
+  onemax1024_jit    the headline island with a hipRTC-compiled objective
 The 8-GPU island configs are bench.py under torchrun (the driver runs those).
 Each line: gens/s, evals/s, ms/gen, best fitness, effective HBM GB/s (the
 bytes one generation must move at minimum: read 2 parent rows + write 1
@@ -46,6 +47,11 @@ def make(name: str):
         # reference example E1 with the reference's own operators (binary tournament,
         # uniform crossover, 1% single-gene reset): same algorithm as build/bench/refsem
         return M.SumGenes(100), 40000, None, {}, 500
+    if name == "onemax1024_jit":
+        # the headline config with the objective written as HIP source (hipRTC)
+        src = """__device__ float ones(const unsigned int* w, unsigned int n, const float* d) {
+            float s = 0.f; for (unsigned i = 0; i < (n + 31) / 32; ++i) s += __popc(w[i]); return s; }"""
+        return M.JitObjective("binary", 1024, src, name="ones"), 1 << 20, None, dict(elitism=1), 300
     if name == "e2_knap_refops":
         # reference example E2 (S=100, L=6): launch-bound, the hipGraph replay case
         return M.ReferenceKnapsack(), 100, None, {}, 5000
@@ -61,7 +67,7 @@ def make(name: str):
 
 
 NAMES = ["onemax64_cpu", "onemax1024", "rastrigin30", "rastrigin30_rot", "tsp256_ox", "tsp256_pmx", "e1_sum100_refops",
-         "e2_knap_refops", "onemax64_gpu"]
+         "e2_knap_refops", "onemax64_gpu", "onemax1024_jit"]
 
 
 def run_one(name: str, steps_scale: float) -> dict:

@@ -44,7 +44,7 @@ struct pga_population {
     if (done) (void)hipEventDestroy(done);
     if (stream) (void)hipStreamDestroy(stream);
   }
-  int builtin = -1;  // built-in objective id, -1: the pga-level obj_f callback
+  int builtin = -1;  // built-in objective id, -1: the pga-level obj_f callback, -2: hipRTC source
 };
 
 struct pga_solver {
@@ -102,7 +102,7 @@ bool valid_pop(pga_t* p, population_t* pop) {
 void sync_callbacks(pga_t* p, population_t* pop) {
   pga::Island& isl = *pop->isl;
   pga::Config c = isl.config();
-  if (pop->builtin < 0) {
+  if (pop->builtin == -1) {
     c.objective = p->objective ? pga::OBJ_USER_FNPTR : pga::OBJ_NONE;
     isl.set_user_fn((void*)p->objective);
     if (c.encoding == pga::ENC_REAL) isl.set_user_operators((void*)p->crossover, (void*)p->mutate);
@@ -326,6 +326,23 @@ int pga_set_objective_builtin(pga_t* p, population_t* pop, enum pga_objective ob
     c.obj_f1 = f1;
     isl.set_operators(c);
     pop->builtin = (int)obj;
+    return 0;
+  });
+}
+
+int pga_set_objective_source(pga_t* p, population_t* pop, const char* source, const char* name, const float* data,
+                             size_t n) {
+  if (!valid_pop(p, pop) || !source || !name) return -1;
+  return guard_r<int>(p, -1, [&]() {
+    pga::Island& isl = *pop->isl;
+    isl.stream = p->stream;
+    auto k = pga::jit_compile(isl.config().encoding, source, name, {});
+    if (data) isl.set_objective_data(data, n, 0);
+    pga::Config c = isl.config();
+    c.objective = pga::OBJ_NONE;
+    isl.set_operators(c);
+    isl.set_jit_objective(k);
+    pop->builtin = -2;
     return 0;
   });
 }

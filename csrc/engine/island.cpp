@@ -257,11 +257,16 @@ void Island::initialize() {
   TraceRange tr("pga.initialize");
   GenArgs a = make_args(MODE_INIT);
   n_best_[cur_] = launch(MODE_INIT, a, (unsigned long long*)best_[cur_].ptr);
-  if (cfg_.objective == OBJ_NONE) rebest();
+  if (jit_) n_best_[cur_] = jit_eval(rows_[cur_].ptr, (float*)scores_[cur_].ptr, cfg_.S, (unsigned long long*)best_[cur_].ptr);
+  else if (cfg_.objective == OBJ_NONE) rebest();
 }
 
 void Island::evaluate() {
   TraceRange tr("pga.evaluate");
+  if (jit_) {
+    n_best_[cur_] = jit_eval(rows_[cur_].ptr, (float*)scores_[cur_].ptr, cfg_.S, (unsigned long long*)best_[cur_].ptr);
+    return;
+  }
   GenArgs a = make_args(MODE_EVAL);
   n_best_[cur_] = launch(MODE_EVAL, a, (unsigned long long*)best_[cur_].ptr);
 }
@@ -309,6 +314,9 @@ void Island::run_plain(uint32_t n) {
     prepare_generation();
     GenArgs a = make_args(MODE_GEN);
     n_best_[cur_ ^ 1] = launch(MODE_GEN, a, (unsigned long long*)best_[cur_ ^ 1].ptr);
+    if (jit_)
+      n_best_[cur_ ^ 1] = jit_eval(rows_[cur_ ^ 1].ptr, (float*)scores_[cur_ ^ 1].ptr, cfg_.S,
+                                   (unsigned long long*)best_[cur_ ^ 1].ptr);
     swap();
   }
 }
@@ -409,10 +417,14 @@ void Island::scatter(const uint32_t* idx, uint32_t n, const void* in_rows, const
 }
 
 bool Island::evaluate_rows(void* rows, float* scores, uint32_t n) {
-  if (cfg_.objective == OBJ_NONE) return false;
+  if (cfg_.objective == OBJ_NONE && !jit_) return false;
   if (n == 0) return true;
   TraceRange tr("pga.migrate.evaluate");
   if (!ev_parts_.ptr) ev_parts_ = alloc(8ull * kMaxGrid);
+  if (jit_) {
+    jit_eval(rows, scores, n, (unsigned long long*)ev_parts_.ptr);
+    return true;
+  }
   GenArgs a = make_args(MODE_EVAL);
   a.cur = rows;
   a.next = rows;
@@ -425,6 +437,25 @@ bool Island::evaluate_rows(void* rows, float* scores, uint32_t n) {
   a.elite_idx = nullptr;
   launch(MODE_EVAL, a, (unsigned long long*)ev_parts_.ptr);
   return true;
+}
+
+// ----------------------------------------------------------------- JIT ---
+void Island::set_jit_objective(std::shared_ptr<JitKernel> k) {
+  if (k) {
+    if (!on_gpu()) throw std::invalid_argument("JIT objectives need the GPU backend");
+    if (cfg_.objective != OBJ_NONE) throw std::invalid_argument("a JIT objective needs objective OBJ_NONE");
+    if (k->encoding != cfg_.encoding) throw std::invalid_argument("JIT objective compiled for another encoding");
+    k->function(device_);  // load the module now: errors surface here, not mid-run
+  }
+  jit_ = std::move(k);
+  invalidate();
+}
+
+uint32_t Island::jit_eval(const void* rows, float* scores, uint64_t n, unsigned long long* parts) {
+  TraceRange tr("pga.jit_eval", 2);
+  const uint32_t grid = launch_grid(n, 256);
+  jit_->eval(device_, rows, row_words_, n, cfg_.L, (const float*)obj_data_[0].ptr, scores, parts, grid, stream);
+  return grid;
 }
 
 // ------------------------------------------------------------ hipGraph ---

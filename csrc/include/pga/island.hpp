@@ -19,6 +19,7 @@
 #include <vector>
 
 #include "pga/core.hpp"
+#include "pga/jit.hpp"
 
 namespace pga {
 
@@ -80,6 +81,10 @@ class Island {
   }
   // reference-ABI crossover_f / mutate_f device pointers (nullptr = built-in)
   void set_user_operators(void* xo, void* mut);
+  // hipRTC-compiled objective (jit.hpp); needs objective OBJ_NONE and the GPU.
+  // Its data pointer is objective data slot 0.  nullptr detaches.
+  void set_jit_objective(std::shared_ptr<JitKernel> k);
+  bool has_jit() const { return (bool)jit_; }
 
   // ---- stages ----
   void initialize();          // random population + evaluation (generation 0)
@@ -159,6 +164,9 @@ class Island {
   void* user_xo_fn_ = nullptr;
   void* user_mut_fn_ = nullptr;
   Buffer compat_rand_, ev_parts_;
+  std::shared_ptr<JitKernel> jit_;
+  // JIT evaluation of `n` rows at `rows` -> scores, block bests -> parts; returns the grid
+  uint32_t jit_eval(const void* rows, float* scores, uint64_t n, unsigned long long* parts);
   u32x4 last_mask_{0, 0, 0, 0};
 
   // graph replay state

@@ -7,6 +7,7 @@
 // Every GPU call enqueues on torch's CURRENT stream of the island's device.
 #include <c10/hip/HIPStream.h>
 #include <torch/extension.h>
+#include <pybind11/stl.h>
 
 #include <memory>
 
@@ -86,6 +87,15 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     return py::make_tuple(rw, ch);
   });
   m.def("group_size", &pga::group_size);
+  py::class_<pga::JitKernel, std::shared_ptr<pga::JitKernel>>(m, "JitKernel")
+      .def_readonly("encoding", &pga::JitKernel::encoding)
+      .def_readonly("name", &pga::JitKernel::name)
+      .def_readonly("source", &pga::JitKernel::source)
+      .def_readonly("log", &pga::JitKernel::log)
+      .def_property_readonly("code_size", [](const pga::JitKernel& k) { return k.code.size(); });
+  m.def("jit_compile", &pga::jit_compile, py::arg("encoding"), py::arg("source"), py::arg("name"),
+        py::arg("options") = std::vector<std::string>{}, py::call_guard<py::gil_scoped_release>());
+  m.def("jit_kernel_source", &pga::jit_kernel_source);
   m.def("trace_level", &pga::trace_level);
   m.def("trace_push", [](const std::string& n) { pga::trace_push(n.c_str()); });
   m.def("trace_pop", &pga::trace_pop);
@@ -113,6 +123,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def_property("generation", &Island::generation, &Island::set_generation)
       .def_property_readonly("epoch", &Island::epoch)
       .def("bump_epoch", &Island::bump_epoch)
+      .def("set_jit_objective",
+           [](Island& i, std::shared_ptr<pga::JitKernel> k) {
+             bind_stream(i);
+             i.set_jit_objective(std::move(k));
+           })
+      .def_property_readonly("has_jit", &Island::has_jit)
       .def_property("graph_generations", &Island::graph_generations, &Island::set_graph_generations)
       .def_property_readonly("graph_replays", &Island::graph_replays)
       .def("config", [](Island& i) { return i.config(); })

@@ -47,6 +47,13 @@ population_t *pga_create_population_ext(pga_t *p, unsigned long size, unsigned g
 /* built-in fused objective; data / data2 are host arrays copied to the device */
 int pga_set_objective_builtin(pga_t *p, population_t *pop, enum pga_objective objective, const float *data,
                               size_t n, const float *data2, size_t n2, int iparam, float fparam0, float fparam1);
+/* objective from HIP source compiled at runtime for gfx950 (hipRTC): `name` is a
+ *   __device__ float name(const T *row, unsigned int n, const float *data)
+ * with T = unsigned int (BINARY words), float (REAL), unsigned short (PERMUTATION);
+ * data: n floats copied to the device (may be NULL).  GPU only.  On a compile
+ * error: -1 and the compiler log in pga_last_error() (when abort is off). */
+int pga_set_objective_source(pga_t *p, population_t *pop, const char *source, const char *name, const float *data,
+                             size_t n);
 int pga_set_operators(pga_t *p, population_t *pop, enum pga_selection selection, unsigned tournament_k,
                       enum pga_crossover crossover, float crossover_prob, enum pga_mutation mutation,
                       float mutation_rate /* < 0: default */, float sigma, unsigned elitism);

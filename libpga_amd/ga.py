@@ -87,6 +87,15 @@ class GeneticAlgorithm:
             self._island.set_objective_data(d1, 0)
         if d2 is not None:
             self._island.set_objective_data(d2, 1)
+        # the objective the Python layer evaluates (None: native, fused or JIT)
+        self.torch_objective = problem.torch_objective
+        if getattr(problem, "jit_source", None) is not None:
+            if self.device.type == "cuda":
+                self._island.set_jit_objective(problem.kernel())
+            elif getattr(problem, "fallback", None) is not None:
+                self.torch_objective = problem.fallback
+            else:
+                raise ValueError("a JIT objective needs a GPU (or a torch `fallback` for the CPU backend)")
         if initialize:
             self.initialize()
 
@@ -127,7 +136,7 @@ class GeneticAlgorithm:
 
     # ------------------------------------------------------------ stages ---
     def _custom_eval(self) -> None:
-        fn = self.problem.torch_objective
+        fn = self.torch_objective
         if fn is None:
             return
         genomes = self.problem.decode(self._island.rows(0))
@@ -139,7 +148,7 @@ class GeneticAlgorithm:
         self._custom_eval()
 
     def evaluate(self) -> None:
-        if self.problem.torch_objective is not None:
+        if self.torch_objective is not None:
             self._custom_eval()
         else:
             self._island.evaluate()
@@ -152,13 +161,13 @@ class GeneticAlgorithm:
         """Run ``generations`` fused generations.  With ``target`` (or a
         callback returning True) stop early; those checks synchronise every
         ``check_every`` generations.  Returns generations executed."""
-        if self.problem.torch_objective is None and callback is None and target is None:
+        if self.torch_objective is None and callback is None and target is None:
             self._island.run(int(generations))
             return int(generations)
         done = 0
         while done < generations:
             n = min(check_every, generations - done)
-            if self.problem.torch_objective is None:
+            if self.torch_objective is None:
                 self._island.run(n)
             else:
                 for _ in range(n):

@@ -5,4 +5,5 @@ from .real import (  # noqa: F401
     Ackley, Griewank, RandomKeyTSP, Rastrigin, RealTorchObjective, ReferenceKnapsack, Rosenbrock, Schwefel, Sphere,
     SumGenes, random_rotation,
 )
+from .jit import JitObjective  # noqa: F401
 from .permutation import TSP, TSPEuclidean  # noqa: F401

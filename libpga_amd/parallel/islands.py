@@ -254,7 +254,7 @@ class IslandModel:
                 if not self.overlap:
                     self.finish_migration()
             self.ga.island.run(1)
-            if self.ga.problem.torch_objective is not None:
+            if self.ga.torch_objective is not None:
                 self.ga._custom_eval()
             if self._pending is not None:
                 self.finish_migration()

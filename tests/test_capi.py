@@ -65,6 +65,7 @@ def lib():
     L.pga_generation.argtypes = [vp]
     L.pga_save.argtypes = [vp, vp, C.c_char_p]
     L.pga_load.argtypes = [vp, vp, C.c_char_p]
+    L.pga_set_objective_source.argtypes = [vp, vp, C.c_char_p, C.c_char_p, C.POINTER(C.c_float), C.c_size_t]
     L.free_ = C.CDLL(None).free
     L.free_.argtypes = [vp]
     return L
@@ -212,3 +213,36 @@ def test_example_e3_tsp_user_crossover():
 def test_example_onemax_bits_c():
     rc, out = run_ex([os.path.join(EX, "onemax_bits"), "65536", "100"])
     assert rc == 0, out
+
+
+def test_objective_source_cpu_is_refused(lib):
+    p = new(lib)
+    pop = lib.pga_create_population_ext(p, 64, 64, PGA_BINARY)
+    src = b"__device__ float f(const unsigned int* w, unsigned int n, const float* d) { return 0.f; }"
+    assert lib.pga_set_objective_source(p, pop, src, b"f", None, 0) == -1
+    assert b"GPU" in lib.pga_last_error()
+    lib.pga_deinit(p)
+
+
+@pytest.mark.gpu
+def test_objective_source_gpu(lib):
+    """pga_set_objective_source: hipRTC OneMax equals the built-in OneMax run for run."""
+    src = (b"__device__ float ones(const unsigned int* w, unsigned int n, const float* d) {"
+           b" float s = 0.f; for (unsigned i = 0; i < (n + 31) / 32; ++i) s += __popc(w[i]); return s; }")
+    best = []
+    for jit in (False, True):
+        p = lib.pga_init_device(0)
+        lib.pga_set_seed(p, 9)
+        lib.pga_set_quiet(p, 1)
+        lib.pga_set_abort_on_error(p, 0)
+        pop = lib.pga_create_population_ext(p, 4096, 512, PGA_BINARY)
+        if jit:
+            assert lib.pga_set_objective_source(p, pop, src, b"ones", None, 0) == 0, lib.pga_last_error()
+        else:
+            assert lib.pga_set_objective_builtin(p, pop, 1, None, 0, None, 0, 0, 0.0, 0.0) == 0
+        lib.pga_run(p, 25)
+        scores = (C.c_float * 4096)()
+        assert lib.pga_get_scores(p, pop, scores) == 0
+        best.append(list(scores))
+        lib.pga_deinit(p)
+    assert best[0] == best[1]
