@@ -453,9 +453,8 @@ void Island::set_jit_objective(std::shared_ptr<JitKernel> k) {
 
 uint32_t Island::jit_eval(const void* rows, float* scores, uint64_t n, unsigned long long* parts) {
   TraceRange tr("pga.jit_eval", 2);
-  const uint32_t grid = launch_grid(n, 256);
-  jit_->eval(device_, rows, row_words_, n, cfg_.L, (const float*)obj_data_[0].ptr, scores, parts, grid, stream);
-  return grid;
+  return jit_->eval(device_, rows, row_words_, n, cfg_.L, (const float*)obj_data_[0].ptr, scores, parts, kMaxGrid,
+                    stream);
 }
 
 // ------------------------------------------------------------ hipGraph ---

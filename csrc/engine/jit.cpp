@@ -73,18 +73,35 @@ __device__ __forceinline__ unsigned int score_key(float s) {
 __device__ __forceinline__ unsigned long long umax64(unsigned long long a, unsigned long long b) { return a > b ? a : b; }
 }  // namespace pga_jit_detail
 
+// Rows are staged through LDS a tile at a time: the tile is copied with
+// coalesced dword loads, then work-item t evaluates row t from LDS.  The LDS
+// row stride is row_words + 1 so that work-items walking their rows in step
+// hit different banks.
 extern "C" __global__ __launch_bounds__(256) void pga_jit_eval(const unsigned int* rows, unsigned int row_words,
-    unsigned long long S, unsigned int L, const float* data, float* scores, unsigned long long* parts) {
+    unsigned long long S, unsigned int L, const float* data, float* scores, unsigned long long* parts,
+    unsigned int tile) {
+  extern __shared__ unsigned int lds_rows[];
   __shared__ unsigned long long red[4];
+  const unsigned int stride = row_words + 1;
   unsigned long long best = 0;
-  for (unsigned long long i = (unsigned long long)blockIdx.x * 256u + threadIdx.x; i < S;
-       i += (unsigned long long)gridDim.x * 256u) {
-    const PGA_GENE* row = (const PGA_GENE*)(rows + i * row_words);
-    const float s = PGA_OBJECTIVE(row, L, data);
-    scores[i] = s;
-    const unsigned long long p = ((unsigned long long)pga_jit_detail::score_key(s) << 32) |
-                                 (0xFFFFFFFFull - (unsigned int)i);
-    best = pga_jit_detail::umax64(best, p);
+  for (unsigned long long base = (unsigned long long)blockIdx.x * tile; base < S;
+       base += (unsigned long long)gridDim.x * tile) {
+    const unsigned int n = (S - base < tile) ? (unsigned int)(S - base) : tile;
+    const unsigned int* src = rows + base * row_words;
+    for (unsigned int w = threadIdx.x; w < n * row_words; w += 256) {
+      const unsigned int r = w / row_words, c = w - r * row_words;
+      lds_rows[r * stride + c] = src[w];
+    }
+    __syncthreads();
+    for (unsigned int t = threadIdx.x; t < n; t += 256) {
+      const unsigned long long i = base + t;
+      const float s = PGA_OBJECTIVE((const PGA_GENE*)(lds_rows + t * stride), L, data);
+      scores[i] = s;
+      const unsigned long long p = ((unsigned long long)pga_jit_detail::score_key(s) << 32) |
+                                   (0xFFFFFFFFull - (unsigned int)i);
+      best = pga_jit_detail::umax64(best, p);
+    }
+    __syncthreads();
   }
   for (int o = 32; o > 0; o >>= 1) {
     const unsigned int lo = __shfl_xor((unsigned int)best, o, 64), hi = __shfl_xor((unsigned int)(best >> 32), o, 64);
@@ -169,14 +186,22 @@ hipFunction_t JitKernel::function(int device) {
   return fns_[device];
 }
 
-void JitKernel::eval(int device, const void* rows, uint32_t row_words, uint64_t S, uint32_t L, const float* data,
-                     float* scores, unsigned long long* parts, uint32_t grid, hipStream_t s) {
+uint32_t JitKernel::eval(int device, const void* rows, uint32_t row_words, uint64_t S, uint32_t L, const float* data,
+                         float* scores, unsigned long long* parts, uint32_t grid, hipStream_t s) {
   hipFunction_t f = function(device);
   const unsigned int* r = (const unsigned int*)rows;
   unsigned int rw = row_words, l = L;
   unsigned long long n = S;
-  void* args[] = {&r, &rw, &n, &l, &data, &scores, &parts};
-  PGA_HIP_CHECK(hipModuleLaunchKernel(f, grid, 1, 1, 256, 1, 1, 0, s, args, nullptr));
+  // rows per LDS tile: up to 256 (one per work-item), at most 64 KiB of LDS
+  unsigned int tile = (unsigned int)(65536 / (4ull * (row_words + 1)));
+  tile = tile > 256 ? 256 : (tile < 1 ? 1 : tile);
+  const size_t lds = 4ull * tile * (row_words + 1);
+  if (lds > 65536) throw std::invalid_argument("JIT objective: row too large for LDS staging (> 64 KiB)");
+  uint64_t blocks = (S + tile - 1) / tile;
+  if (blocks > grid) blocks = grid;
+  void* args[] = {&r, &rw, &n, &l, &data, &scores, &parts, &tile};
+  PGA_HIP_CHECK(hipModuleLaunchKernel(f, (unsigned)blocks, 1, 1, 256, 1, 1, (unsigned)lds, s, args, nullptr));
+  return (uint32_t)blocks;
 }
 
 }  // namespace pga

@@ -31,8 +31,9 @@ class JitKernel {
   std::vector<char> code;  // gfx950 code object
   // per-device loaded module / function (lazily, on first launch)
   hipFunction_t function(int device);
-  void eval(int device, const void* rows, uint32_t row_words, uint64_t S, uint32_t L, const float* data,
-            float* scores, unsigned long long* parts, uint32_t grid, hipStream_t s);
+  // returns the number of blocks launched (= best partials written), <= max_grid
+  uint32_t eval(int device, const void* rows, uint32_t row_words, uint64_t S, uint32_t L, const float* data,
+                float* scores, unsigned long long* parts, uint32_t max_grid, hipStream_t s);
 
  private:
   std::vector<hipModule_t> modules_;
