@@ -173,3 +173,51 @@ def test_philox_known_answer():
         0x408F276D, 0x41C83B0E, 0xA20BC7C6, 0x6D5451FD)
     assert _C.philox(0x243F6A88, 0x85A308D3, 0x13198A2E, 0x03707344, 0xA4093822, 0x299F31D0) == (
         0xD16CFE09, 0x94FDCCEB, 0x5001E420, 0x24126EA1)
+
+
+def _value_problem(L=24):
+    """Individual value = its bits as an integer (exact in f32 for L <= 24)."""
+    w = (2.0 ** torch.arange(L)).float()
+    return pga.models.BinaryTorchObjective(L, lambda g: g.float() @ w)
+
+
+def _set_population(ga, genomes):
+    ga.island.rows(0).copy_(ga.problem.encode(genomes, int(ga.island.row_words)))
+    ga._custom_eval()
+
+
+def test_tournament_selection_pressure():
+    """Tournament-k with distinct scores: a copied parent's rank u = r/S has
+    E[u] = k/(k+1) (P(u <= x) = x^k); binary tournament -> 2/3."""
+    S, L = 4096, 24
+    for k in (2, 4):
+        ga = make(_value_problem(L), S=S, tournament_k=k, crossover="none", mutation="none")
+        vals = torch.randperm(S)
+        bits = ((vals[:, None] >> torch.arange(L)) & 1).to(torch.uint8)
+        _set_population(ga, bits)
+        ga.run(1)
+        u = ga.scores.double() / (S - 1)
+        exp, sd = k / (k + 1), math.sqrt(k / ((k + 2) * (k + 1) ** 2))
+        assert abs(u.mean().item() - exp) < 5 * sd / math.sqrt(S), (k, u.mean().item())
+
+
+def test_uniform_crossover_bit_balance():
+    """Uniform crossover of an all-zeros and an all-ones parent gives each bit
+    from either parent with probability 1/2, independently."""
+    S, L = 4096, 256
+    ga = make(pga.models.OneMax(L), S=S, selection="random", crossover="uniform", mutation="none")
+    bits = torch.zeros(S, L, dtype=torch.uint8)
+    bits[S // 2:] = 1
+    ga.island.rows(0).copy_(ga.problem.encode(bits, int(ga.island.row_words)))
+    ga.evaluate()
+    ga.run(1)
+    ones = ga.scores
+    mixed = (ones > 0) & (ones < L)  # children of one zeros- and one ones-parent (whp)
+    frac = mixed.float().mean().item()
+    assert abs(frac - 0.5) < 0.05  # P(parents differ) = 1/2
+    m = ones[mixed].double()
+    assert abs(m.mean().item() - L / 2) < 5 * math.sqrt(L / 4 / m.numel())
+    assert abs(m.var().item() - L / 4) < 0.15 * L / 4
+    g = ga.genomes()[mixed].double()
+    per_bit = g.mean(0)  # every position balanced
+    assert (per_bit - 0.5).abs().max().item() < 6 * math.sqrt(0.25 / g.shape[0])
