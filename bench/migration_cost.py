@@ -1,0 +1,52 @@
+#!/usr/bin/env python3
+"""Per-epoch cost of the island-migration device work on one GPU (everything
+IslandModel does except the RCCL transfer itself): top-k emigrants, pack,
+bottom-k victims, scatter, best/key refresh.  Prints one JSON line."""
+import json
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import libpga_amd as pga  # noqa: E402
+
+
+def main():
+    S = int(sys.argv[1]) if len(sys.argv) > 1 else 1 << 20
+    pct = float(sys.argv[2]) if len(sys.argv) > 2 else 0.01
+    ga = pga.GeneticAlgorithm(pga.models.OneMax(1024), S, seed=1, device="cuda:0", elitism=1)
+    ga.run(20)
+    isl = ga.island
+    k = int(round(pct * S))
+    rw = int(isl.row_words)
+    rows = torch.empty(k * rw, dtype=torch.int32, device="cuda:0")
+    sc = torch.empty(k, dtype=torch.float32, device="cuda:0")
+
+    def epoch():  # exactly IslandModel's device work (selection-order top-k)
+        idx = isl.topk(k, True, False)
+        isl.gather(idx, rows, sc)
+        isl.evaluate_rows(rows, sc)
+        vic = isl.topk(k, False, False)
+        isl.scatter(vic, rows, sc)
+
+    for _ in range(5):
+        epoch()
+    torch.cuda.synchronize()
+    res = {}
+    for name, fn in (("topk_sorted", lambda: isl.topk(k, True)), ("topk", lambda: isl.topk(k, True, False)),
+                     ("epoch", epoch), ("generation", lambda: isl.run(1))):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        n = 50
+        a.record()
+        for _ in range(n):
+            fn()
+        b.record()
+        b.synchronize()
+        res[name + "_us"] = a.elapsed_time(b) / n * 1e3
+    res.update(pop=S, k=k)
+    print(json.dumps(res))
+
+
+if __name__ == "__main__":
+    main()

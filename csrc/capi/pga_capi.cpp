@@ -165,7 +165,7 @@ Emigrants take_best(pga::Island& isl, uint32_t k) {
   uint32_t* idx = (uint32_t*)dev_alloc(isl, 4ull * k);
   e.rows = dev_alloc(isl, isl.row_bytes() * k);
   e.scores = (float*)dev_alloc(isl, 4ull * k);
-  isl.topk(k, true, idx);
+  isl.topk(k, true, idx, false);
   isl.gather(idx, k, e.rows, e.scores);
   isl.synchronize();
   dev_free(isl, idx);
@@ -174,7 +174,7 @@ Emigrants take_best(pga::Island& isl, uint32_t k) {
 
 void replace_worst(pga::Island& isl, Emigrants& e) {
   uint32_t* idx = (uint32_t*)dev_alloc(isl, 4ull * e.k);
-  isl.topk(e.k, false, idx);
+  isl.topk(e.k, false, idx, false);
   isl.scatter(idx, e.k, e.rows, e.scores);
   isl.synchronize();
   dev_free(isl, idx);
@@ -577,10 +577,10 @@ void migrate_ranks(pga_t* p, float pct) {
     p->mig_bytes = bytes;
   }
   uint32_t* idx = (uint32_t*)isl.scratch(4ull * k);
-  isl.topk(k, true, idx);
+  isl.topk(k, true, idx, false);
   isl.gather(idx, k, p->mig_send, (float*)((char*)p->mig_send + rows));
   pga::rccl_ring_exchange(p->comm, p->mig_send, p->mig_recv, bytes, p->stream);
-  isl.topk(k, false, idx);
+  isl.topk(k, false, idx, false);
   isl.scatter(idx, k, p->mig_recv, (const float*)((const char*)p->mig_recv + rows));
 }
 }  // namespace

@@ -4,6 +4,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstring>
+#include <functional>
 #include <numeric>
 #include <stdexcept>
 #include <vector>
@@ -256,19 +257,40 @@ void roulette_prefix(const float* s, uint64_t S, float* cumfit) {
   }
 }
 
-void topk(const float* scores, uint64_t S, uint32_t k, bool largest, uint32_t* idx_out) {
+void topk(const float* scores, uint64_t S, uint32_t k, bool largest, uint32_t* idx_out, bool sorted) {
   if (k > S) throw std::runtime_error("topk: k > S");
-  std::vector<uint32_t> idx(S);
-  std::iota(idx.begin(), idx.end(), 0u);
+  if (k == 0) return;
   auto key = [&](uint32_t i) {
     uint32_t kk = score_key(scores[i]);
     return largest ? kk : ~kk;
   };
-  std::partial_sort(idx.begin(), idx.begin() + k, idx.end(), [&](uint32_t x, uint32_t y) {
-    uint32_t kx = key(x), ky = key(y);
-    return kx != ky ? kx > ky : x < y;
-  });
-  std::memcpy(idx_out, idx.data(), 4ull * k);
+  std::vector<uint32_t> idx(S);
+  std::iota(idx.begin(), idx.end(), 0u);
+  if (sorted) {
+    std::partial_sort(idx.begin(), idx.begin() + k, idx.end(), [&](uint32_t x, uint32_t y) {
+      uint32_t kx = key(x), ky = key(y);
+      return kx != ky ? kx > ky : x < y;
+    });
+    std::memcpy(idx_out, idx.data(), 4ull * k);
+    return;
+  }
+  // selection order (matches the GPU's unsorted mode): keys above the k-th
+  // largest key T by index, then the first (k - #above) keys equal to T by index
+  std::vector<uint32_t> keys(S);
+  for (uint64_t i = 0; i < S; ++i) keys[i] = key((uint32_t)i);
+  std::vector<uint32_t> tmp(keys);
+  std::nth_element(tmp.begin(), tmp.begin() + (k - 1), tmp.end(), std::greater<uint32_t>());
+  const uint32_t T = tmp[k - 1];
+  uint32_t n = 0, above = 0;
+  for (uint64_t i = 0; i < S; ++i) above += keys[i] > T;
+  uint32_t need_eq = k - above;
+  for (uint64_t i = 0; i < S; ++i)
+    if (keys[i] > T) idx_out[n++] = (uint32_t)i;
+  for (uint64_t i = 0; i < S && need_eq; ++i)
+    if (keys[i] == T) {
+      idx_out[n++] = (uint32_t)i;
+      --need_eq;
+    }
 }
 
 void gather_rows(const void* rows, const float* scores, uint32_t row_words, const uint32_t* idx, uint32_t n,

@@ -274,8 +274,8 @@ void Island::evaluate() {
 void Island::rebest() {
   const float* sc = (const float*)scores_[cur_].ptr;
   if (on_gpu()) {
-    n_best_[cur_] = best_of_scores_launch(sc, cfg_.S, (unsigned long long*)best_[cur_].ptr, stream);
-    if (integer_objective(cfg_.objective, cfg_.L)) scores_to_keys_launch(sc, cfg_.S, (uint16_t*)keys_[cur_].ptr, stream);
+    uint16_t* keys = integer_objective(cfg_.objective, cfg_.L) ? (uint16_t*)keys_[cur_].ptr : nullptr;
+    n_best_[cur_] = best_of_scores_launch(sc, cfg_.S, (unsigned long long*)best_[cur_].ptr, stream, keys);
   } else {
     ((unsigned long long*)best_[cur_].ptr)[0] = cpu::best_of_scores(sc, cfg_.S);
     n_best_[cur_] = 1;
@@ -288,7 +288,7 @@ void Island::prepare_generation() {
     if (on_gpu()) roulette_prefix_launch(sc, cfg_.S, (float*)cumfit_.ptr, (float*)cum_ws_.ptr, stream);
     else cpu::roulette_prefix(sc, cfg_.S, (float*)cumfit_.ptr);
   }
-  if (cfg_.n_elite > 1) topk(cfg_.n_elite, true, (uint32_t*)elite_idx_.ptr);
+  if (cfg_.n_elite > 1) topk(cfg_.n_elite, true, (uint32_t*)elite_idx_.ptr, /*sorted=*/false);
 }
 
 void Island::run(uint32_t n) {
@@ -361,7 +361,7 @@ void Island::stats(float out[4]) {
   }
 }
 
-void Island::topk(uint32_t k, bool largest, uint32_t* idx_out) {
+void Island::topk(uint32_t k, bool largest, uint32_t* idx_out, bool sorted) {
   TraceRange tr(largest ? "pga.topk" : "pga.bottomk");
   if (k > cfg_.S) throw std::invalid_argument("k exceeds population size");
   const float* sc = (const float*)scores_[cur_].ptr;
@@ -371,10 +371,12 @@ void Island::topk(uint32_t k, bool largest, uint32_t* idx_out) {
       synchronize();
       release(topk_ws_);
       topk_ws_ = alloc(need);
+      PGA_HIP_CHECK(hipMemset(topk_ws_.ptr, 0, need));  // the value histogram must start zeroed
     }
-    topk_launch(sc, cfg_.S, k, largest, idx_out, topk_ws_.ptr, stream);
+    const uint16_t* k16 = integer_objective(cfg_.objective, cfg_.L) ? (const uint16_t*)keys_[cur_].ptr : nullptr;
+    topk_launch(sc, k16, cfg_.L + 1, cfg_.S, k, largest, sorted, idx_out, topk_ws_.ptr, stream);
   } else {
-    cpu::topk(sc, cfg_.S, k, largest, idx_out);
+    cpu::topk(sc, cfg_.S, k, largest, idx_out, sorted);
   }
 }
 
@@ -481,6 +483,7 @@ bool Island::capture_graph() {
       synchronize();
       release(topk_ws_);
       topk_ws_ = alloc(need);
+      PGA_HIP_CHECK(hipMemset(topk_ws_.ptr, 0, need));
     }
   }
   const int cur0 = cur_;

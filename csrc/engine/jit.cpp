@@ -119,7 +119,7 @@ extern "C" __global__ __launch_bounds__(256) void pga_jit_eval(const unsigned in
 }  // namespace
 
 std::string jit_kernel_source(int encoding, const std::string& source, const std::string& name) {
-  std::string s = "#include <hip/hip_runtime.h>\n";
+  std::string s;  // hipRTC provides the HIP device built-ins itself
   s += "#define PGA_GENE " + std::string(gene_type(encoding)) + "\n";
   s += "#define PGA_OBJECTIVE " + name + "\n";
   s += "#line 1 \"user_objective\"\n";

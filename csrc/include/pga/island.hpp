@@ -104,7 +104,9 @@ class Island {
   std::vector<uint32_t> row_host(uint64_t i);
 
   // ---- device-side building blocks (no sync) ----
-  void topk(uint32_t k, bool largest, uint32_t* idx_out);  // idx_out: device (or host for CPU) memory
+  // idx_out: device (or host for CPU) memory.  sorted: best first (ties by
+  // index); unsorted: selection order, cheaper (migration, elitism)
+  void topk(uint32_t k, bool largest, uint32_t* idx_out, bool sorted = true);
   void gather(const uint32_t* idx, uint32_t n, void* out_rows, float* out_scores);
   void scatter(const uint32_t* idx, uint32_t n, const void* in_rows, const float* in_scores);
   // score n external rows (e.g. received migrants) with this island's

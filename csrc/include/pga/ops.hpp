@@ -60,7 +60,8 @@ inline uint32_t encoding_launch(int mode, const GenArgs& a, unsigned long long* 
 // out[0] = max over parts[0..n)
 void reduce_best_launch(const unsigned long long* parts, uint32_t n, unsigned long long* out, hipStream_t s);
 // per-block best over arbitrary scores (for externally evaluated populations)
-uint32_t best_of_scores_launch(const float* scores, uint64_t S, unsigned long long* parts, hipStream_t s);
+uint32_t best_of_scores_launch(const float* scores, uint64_t S, unsigned long long* parts, hipStream_t s,
+                               uint16_t* keys = nullptr);  // keys: also refresh u16 tournament keys
 // keys[i] = (uint16)scores[i] (integer objectives' tournament keys)
 void scores_to_keys_launch(const float* scores, uint64_t S, uint16_t* keys, hipStream_t s);
 // *counter += delta (graph replay: the device-resident generation counter)
@@ -71,8 +72,14 @@ void score_stats_launch(const float* scores, uint64_t S, float* stats, hipStream
 void roulette_prefix_launch(const float* scores, uint64_t S, float* cumfit, float* workspace, hipStream_t s);
 // top-k by score (descending, ties -> lower index); idx_out[k]; workspace: topk_workspace_bytes(S)
 size_t topk_workspace_bytes(uint64_t S, uint32_t k);
-void topk_launch(const float* scores, uint64_t S, uint32_t k, bool largest, uint32_t* idx_out, void* workspace,
-                 hipStream_t s);
+// sorted = false: the k indices in selection order (keys above the threshold by
+// index, then threshold ties by index) — cheaper, used by migration / elitism.
+// keys16 (optional): the u16 tournament keys of an integer objective (2 passes)
+// key_range: keys16 take values in [0, key_range) (L + 1 for the integer
+// objectives); <= kTopkMaxRange enables the one-pass value histogram
+constexpr uint32_t kTopkMaxRange = 8192;
+void topk_launch(const float* scores, const uint16_t* keys16, uint32_t key_range, uint64_t S, uint32_t k, bool largest,
+                 bool sorted, uint32_t* idx_out, void* workspace, hipStream_t s);
 // rows: out[i] = rows[idx[i]] (row_words 32-bit words per row), optional scores
 void gather_rows_launch(const void* rows, const float* scores, uint32_t row_words, const uint32_t* idx, uint32_t n,
                         void* out_rows, float* out_scores, hipStream_t s);

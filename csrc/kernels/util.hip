@@ -83,13 +83,17 @@ __global__ __launch_bounds__(kBlock) void reduce_best_kernel(const unsigned long
   if (threadIdx.x == 0) out[0] = b;
 }
 
+// per-block best partials of a score array; with `keys` also refreshes the
+// u16 tournament keys in the same pass (integer objectives)
 __global__ __launch_bounds__(kBlock) void best_of_scores_kernel(const float* scores, uint64_t S,
-                                                                unsigned long long* parts) {
+                                                                unsigned long long* parts, uint16_t* keys) {
   __shared__ unsigned long long lds[kBlock / 64];
   unsigned long long b = 0;
   for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < S; i += (uint64_t)gridDim.x * kBlock) {
-    unsigned long long p = pack_best(scores[i], i);
+    const float v = scores[i];
+    unsigned long long p = pack_best(v, i);
     b = p > b ? p : b;
+    if (keys) keys[i] = (uint16_t)(v <= 0.f ? 0.f : (v >= 65535.f ? 65535.f : v));
   }
   b = block_max_u64(b, lds);
   if (threadIdx.x == 0) parts[blockIdx.x] = b;
@@ -230,6 +234,22 @@ __device__ __forceinline__ uint32_t topk_key(float s, bool largest) {
   return largest ? k : ~k;
 }
 
+// Keys of the selection: 32-bit orderable f32 keys, or (integer objectives)
+// the population's u16 tournament keys — two radix passes instead of four.
+template <int BITS>
+struct TopkKeys {
+  const float* s;
+  const uint16_t* k16;
+  bool largest;
+  __device__ __forceinline__ uint32_t operator()(uint64_t i) const {
+    if (BITS == 16) {
+      const uint32_t v = k16[i];
+      return largest ? v : 0xFFFFu - v;
+    }
+    return topk_key(s[i], largest);
+  }
+};
+
 __global__ __launch_bounds__(kBlock) void topk_init_kernel(TopkState* st, uint32_t k) {
   if (threadIdx.x == 0) {
     st->prefix = 0;
@@ -239,47 +259,142 @@ __global__ __launch_bounds__(kBlock) void topk_init_kernel(TopkState* st, uint32
   st->hist[threadIdx.x] = 0;
 }
 
-__global__ __launch_bounds__(kBlock) void topk_hist_kernel(const float* s, uint64_t S, bool largest, uint32_t shift,
+// 8-bit digit histogram of the keys that match the prefix found so far.
+// Scores cluster (a converging population shares its high bytes), so lanes
+// of a wave are aggregated per distinct bin before the LDS atomic: one atomic
+// per (wave, bin) instead of one per lane on the same address.
+template <int BITS>
+__global__ __launch_bounds__(kBlock) void topk_hist_kernel(TopkKeys<BITS> keys, uint64_t S, uint32_t shift,
                                                            TopkState* st) {
   __shared__ uint32_t h[256];
   h[threadIdx.x] = 0;
   __syncthreads();
   const uint32_t prefix = st->prefix, mask = st->mask;
-  for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < S; i += (uint64_t)gridDim.x * kBlock) {
-    uint32_t key = topk_key(s[i], largest);
-    if ((key & mask) == prefix) atomicAdd(&h[(key >> shift) & 255u], 1u);
+  const uint32_t lane = lane_id();
+  const uint64_t stride = (uint64_t)gridDim.x * kBlock;
+  for (uint64_t base = (uint64_t)blockIdx.x * kBlock; base < S; base += stride) {  // wave-uniform trip count
+    const uint64_t i = base + threadIdx.x;
+    uint32_t bin = 0;
+    bool act = false;
+    if (i < S) {
+      const uint32_t key = keys(i);
+      act = (key & mask) == prefix;
+      bin = (key >> shift) & 255u;
+    }
+    // a converging population shares its high digits: when the whole wave
+    // agrees on one bin, one atomic; otherwise plain per-lane LDS atomics
+    const unsigned long long active = __ballot(act);
+    if (active) {
+      const int leader = __ffsll((long long)active) - 1;
+      const uint32_t b = (uint32_t)__shfl((int)bin, leader, 64);
+      const unsigned long long same = __ballot(act && bin == b);
+      if (same == active) {
+        if ((int)lane == leader) atomicAdd(&h[b], (uint32_t)__popcll(same));
+      } else if (act) {
+        atomicAdd(&h[bin], 1u);
+      }
+    }
   }
   __syncthreads();
   if (h[threadIdx.x]) atomicAdd(&st->hist[threadIdx.x], h[threadIdx.x]);
 }
 
+// pick the digit: the largest d whose suffix count reaches `remaining`
+// (block-parallel suffix sums over the 256 bins; one thread per bin)
 __global__ __launch_bounds__(kBlock) void topk_digit_kernel(TopkState* st, uint32_t shift) {
-  if (threadIdx.x == 0) {
-    uint32_t rem = st->remaining;
-    uint32_t d = 255;
-    for (;; --d) {
-      uint32_t c = st->hist[d];
-      if (c >= rem || d == 0) break;
-      rem -= c;
-    }
-    st->remaining = rem;
+  __shared__ uint32_t suf[kBlock];
+  const uint32_t t = threadIdx.x;
+  const uint32_t c = st->hist[255 - t];  // reversed: suf[t] = sum of bins >= 255 - t
+  const uint32_t rem = st->remaining;
+  suf[t] = c;
+  __syncthreads();
+  for (uint32_t o = 1; o < kBlock; o <<= 1) {
+    const uint32_t v = t >= o ? suf[t - o] : 0u;
+    __syncthreads();
+    suf[t] += v;
+    __syncthreads();
+  }
+  // first t (largest digit 255 - t) whose inclusive suffix reaches rem
+  const bool hit = suf[t] >= rem && (t == 0 || suf[t - 1] < rem);
+  const bool last = t == kBlock - 1 && suf[t] < rem;  // cannot happen for k <= S; keep digit 0
+  if (hit || last) {
+    const uint32_t d = 255 - t;
+    st->remaining = rem - (t ? suf[t - 1] : 0u);
     st->prefix |= d << shift;
     st->mask |= 255u << shift;
   }
   __syncthreads();
-  st->hist[threadIdx.x] = 0;
+  st->hist[t] = 0;
 }
 
-// ordered compaction: contiguous range per block
-__global__ __launch_bounds__(kBlock) void topk_count_kernel(const float* s, uint64_t S, uint64_t per_block,
-                                                            bool largest, const TopkState* st, uint32_t* cnt) {
+// ---- integer objectives: the u16 keys take at most R = L + 1 values, so one
+// LDS histogram of R bins replaces the radix passes ----
+__global__ __launch_bounds__(kBlock) void topk16_hist_kernel(const uint16_t* k16, uint64_t S, uint32_t R, bool largest,
+                                                             uint32_t* G) {
+  extern __shared__ uint32_t hr[];
+  for (uint32_t i = threadIdx.x; i < R; i += kBlock) hr[i] = 0;
+  __syncthreads();
+  for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < S; i += (uint64_t)gridDim.x * kBlock) {
+    const uint32_t v = min((uint32_t)k16[i], R - 1);
+    atomicAdd(&hr[largest ? v : R - 1 - v], 1u);
+  }
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < R; i += kBlock)
+    if (hr[i]) atomicAdd(&G[i], hr[i]);
+}
+
+// every block derives the threshold from the global histogram, block 0
+// publishes it, then each block counts its range (as topk_count_kernel)
+__global__ __launch_bounds__(kBlock) void topk16_count_kernel(const uint16_t* k16, uint64_t S, uint64_t per_block,
+                                                              uint32_t R, bool largest, uint32_t k, const uint32_t* G,
+                                                              TopkState* st, uint32_t* cnt) {
+  __shared__ uint32_t part[kBlock];
+  __shared__ uint32_t sh_T, sh_need;
   __shared__ uint32_t lds[kBlock / 64];
-  const uint32_t T = st->prefix;
+  // bins from the top: thread t owns bins [R-1 - (t+1)*per + 1, R-1 - t*per]
+  const uint32_t per = (R + kBlock - 1) / kBlock;
+  uint32_t mine = 0;
+  for (uint32_t j = 0; j < per; ++j) {
+    const int64_t b = (int64_t)R - 1 - (int64_t)threadIdx.x * per - j;
+    if (b >= 0) mine += G[b];
+  }
+  part[threadIdx.x] = mine;
+  __syncthreads();
+  for (uint32_t o = 1; o < kBlock; o <<= 1) {
+    const uint32_t v = threadIdx.x >= o ? part[threadIdx.x - o] : 0u;
+    __syncthreads();
+    part[threadIdx.x] += v;
+    __syncthreads();
+  }
+  const uint32_t before = threadIdx.x ? part[threadIdx.x - 1] : 0u;
+  if (before < k && part[threadIdx.x] >= k) {
+    uint32_t acc = before;
+    for (uint32_t j = 0; j < per; ++j) {
+      const int64_t b = (int64_t)R - 1 - (int64_t)threadIdx.x * per - j;
+      if (b < 0) break;
+      const uint32_t c = G[b];
+      if (acc + c >= k) {
+        sh_T = (uint32_t)b;
+        sh_need = k - acc;
+        break;
+      }
+      acc += c;
+    }
+  }
+  __syncthreads();
+  // bin -> key in TopkKeys<16> space (largest: v; smallest: 0xFFFF - v)
+  const uint32_t Tb = sh_T;
+  const uint32_t T = largest ? Tb : Tb + 0x10000u - R;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    st->prefix = T;
+    st->remaining = sh_need;
+  }
+  const TopkKeys<16> keys{nullptr, k16, largest};
   const uint64_t b0 = (uint64_t)blockIdx.x * per_block;
   const uint64_t b1 = b0 + per_block < S ? b0 + per_block : S;
   uint32_t gt = 0, eq = 0;
   for (uint64_t i = b0 + threadIdx.x; i < b1; i += kBlock) {
-    uint32_t key = topk_key(s[i], largest);
+    const uint32_t key = keys(i);
     gt += key > T;
     eq += key == T;
   }
@@ -292,17 +407,26 @@ __global__ __launch_bounds__(kBlock) void topk_count_kernel(const float* s, uint
   }
 }
 
-__global__ __launch_bounds__(kBlock) void topk_offsets_kernel(uint32_t* cnt, uint32_t n) {
+// ordered compaction: contiguous range per block
+template <int BITS>
+__global__ __launch_bounds__(kBlock) void topk_count_kernel(TopkKeys<BITS> keys, uint64_t S, uint64_t per_block,
+                                                            const TopkState* st, uint32_t* cnt) {
+  __shared__ uint32_t lds[kBlock / 64];
+  const uint32_t T = st->prefix;
+  const uint64_t b0 = (uint64_t)blockIdx.x * per_block;
+  const uint64_t b1 = b0 + per_block < S ? b0 + per_block : S;
+  uint32_t gt = 0, eq = 0;
+  for (uint64_t i = b0 + threadIdx.x; i < b1; i += kBlock) {
+    uint32_t key = keys(i);
+    gt += key > T;
+    eq += key == T;
+  }
+  auto add = [](uint32_t a, uint32_t b) { return a + b; };
+  gt = block_reduce(gt, lds, add);
+  eq = block_reduce(eq, lds, add);
   if (threadIdx.x == 0) {
-    uint32_t g = 0, e = 0;
-    for (uint32_t i = 0; i < n; ++i) {
-      uint32_t cg = cnt[2 * i], ce = cnt[2 * i + 1];
-      cnt[2 * i] = g;
-      cnt[2 * i + 1] = e;
-      g += cg;
-      e += ce;
-    }
-    cnt[2 * n] = g;  // total strictly greater
+    cnt[2 * blockIdx.x] = gt;
+    cnt[2 * blockIdx.x + 1] = eq;
   }
 }
 
@@ -326,9 +450,43 @@ __device__ __forceinline__ uint32_t block_excl_scan_u(uint32_t v, uint32_t* lds,
   return off + inc - v;
 }
 
-__global__ __launch_bounds__(kBlock) void topk_write_kernel(const float* s, uint64_t S, uint64_t per_block,
-                                                            bool largest, const TopkState* st, const uint32_t* cnt,
-                                                            uint32_t nblocks, uint32_t* keys_out, uint32_t* idx_out) {
+// exclusive scan of the per-block (gt, eq) counts, n <= 4 * kBlock, one block
+__global__ __launch_bounds__(kBlock) void topk_offsets_kernel(uint32_t* cnt, uint32_t n, uint32_t* G, uint32_t R) {
+  for (uint32_t i = threadIdx.x; i < R; i += kBlock) G[i] = 0;  // ready for the next selection
+  __shared__ uint32_t lds[kBlock / 64];
+  uint32_t g[4] = {0, 0, 0, 0}, e[4] = {0, 0, 0, 0};
+  uint32_t sg = 0, se = 0;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const uint32_t i = 4 * threadIdx.x + j;
+    if (i < n) {
+      g[j] = cnt[2 * i];
+      e[j] = cnt[2 * i + 1];
+    }
+    sg += g[j];
+    se += e[j];
+  }
+  uint32_t tg, te;
+  uint32_t og = block_excl_scan_u(sg, lds, tg);
+  __syncthreads();
+  uint32_t oe = block_excl_scan_u(se, lds, te);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const uint32_t i = 4 * threadIdx.x + j;
+    if (i < n) {
+      cnt[2 * i] = og;
+      cnt[2 * i + 1] = oe;
+    }
+    og += g[j];
+    oe += e[j];
+  }
+  if (threadIdx.x == 0) cnt[2 * n] = tg;  // total strictly greater
+}
+
+template <int BITS>
+__global__ __launch_bounds__(kBlock) void topk_write_kernel(TopkKeys<BITS> keys, uint64_t S, uint64_t per_block,
+                                                            const TopkState* st, const uint32_t* cnt, uint32_t nblocks,
+                                                            uint32_t* keys_out, uint32_t* idx_out) {
   __shared__ uint32_t lds[kBlock / 64];
   const uint32_t T = st->prefix;
   const uint32_t need_eq = st->remaining;
@@ -338,7 +496,7 @@ __global__ __launch_bounds__(kBlock) void topk_write_kernel(const float* s, uint
   const uint64_t b1 = b0 + per_block < S ? b0 + per_block : S;
   for (uint64_t t0 = b0; t0 < b1; t0 += kBlock) {
     uint64_t i = t0 + threadIdx.x;
-    uint32_t key = i < b1 ? topk_key(s[i], largest) : 0u;
+    uint32_t key = i < b1 ? keys(i) : 0u;
     uint32_t isg = (i < b1 && key > T) ? 1u : 0u;
     uint32_t ise = (i < b1 && key == T) ? 1u : 0u;
     uint32_t tg, te;
@@ -346,11 +504,11 @@ __global__ __launch_bounds__(kBlock) void topk_write_kernel(const float* s, uint
     __syncthreads();
     uint32_t re = block_excl_scan_u(ise, lds, te);
     if (isg) {
-      keys_out[gpos + rg] = key;
+      if (keys_out) keys_out[gpos + rg] = key;
       idx_out[gpos + rg] = (uint32_t)i;
     }
     if (ise && epos + re < need_eq) {
-      keys_out[gt_total + epos + re] = key;
+      if (keys_out) keys_out[gt_total + epos + re] = key;
       idx_out[gt_total + epos + re] = (uint32_t)i;
     }
     gpos += tg;
@@ -408,9 +566,10 @@ void reduce_best_launch(const unsigned long long* parts, uint32_t n, unsigned lo
   PGA_HIP_CHECK(hipGetLastError());
 }
 
-uint32_t best_of_scores_launch(const float* scores, uint64_t S, unsigned long long* parts, hipStream_t s) {
+uint32_t best_of_scores_launch(const float* scores, uint64_t S, unsigned long long* parts, hipStream_t s,
+                               uint16_t* keys) {
   uint32_t grid = launch_grid(S, kBlock * 4);
-  hipLaunchKernelGGL(best_of_scores_kernel, grid, kBlock, 0, s, scores, S, parts);
+  hipLaunchKernelGGL(best_of_scores_kernel, grid, kBlock, 0, s, scores, S, parts, keys);
   PGA_HIP_CHECK(hipGetLastError());
   return grid;
 }
@@ -449,46 +608,90 @@ size_t topk_workspace_bytes(uint64_t S, uint32_t k) {
                                                              (uint32_t*)nullptr, (uint32_t*)nullptr,
                                                              (uint32_t*)nullptr, (int)k));
   (void)S;
+  // layout: state | counts | 3 k-arrays | cub temp | value histogram (kept zeroed)
   return align_up(sizeof(TopkState)) + align_up(sizeof(uint32_t) * (2 * 1024 + 1)) + 3 * align_up(4ull * k) +
-         align_up(cub_bytes);
+         align_up(cub_bytes) + align_up(4ull * kTopkMaxRange);
 }
 
-void topk_launch(const float* scores, uint64_t S, uint32_t k, bool largest, uint32_t* idx_out, void* ws,
-                 hipStream_t s) {
-  if (k == 0) return;
-  if (k > S) throw std::runtime_error("topk: k > S");
+namespace {
+template <int BITS>
+void topk_run(TopkKeys<BITS> keys, uint64_t S, uint32_t k, bool sorted, uint32_t* idx_out, void* ws, hipStream_t s) {
   char* p = (char*)ws;
   TopkState* st = (TopkState*)p;
   p += align_up(sizeof(TopkState));
   uint32_t* cnt = (uint32_t*)p;
   p += align_up(sizeof(uint32_t) * (2 * 1024 + 1));
-  uint32_t* keys = (uint32_t*)p;
+  uint32_t* keys_buf = (uint32_t*)p;
   p += align_up(4ull * k);
   uint32_t* keys_sorted = (uint32_t*)p;
   p += align_up(4ull * k);
   uint32_t* idx = (uint32_t*)p;
   p += align_up(4ull * k);
-  size_t cub_bytes = 0;
-  PGA_HIP_CHECK(hipcub::DeviceRadixSort::SortPairsDescending(nullptr, cub_bytes, keys, keys_sorted, idx, idx_out,
-                                                             (int)k));
 
-  uint32_t grid = launch_grid(S, kBlock * 4);
+  const uint32_t grid = launch_grid(S, kBlock * 4);
   hipLaunchKernelGGL(topk_init_kernel, 1, kBlock, 0, s, st, k);
-  for (int d = 0; d < 4; ++d) {
-    const uint32_t shift = 24 - 8 * d;
-    hipLaunchKernelGGL(topk_hist_kernel, grid, kBlock, 0, s, scores, S, largest, shift, st);
+  for (int d = 0; d < BITS / 8; ++d) {
+    const uint32_t shift = BITS - 8 - 8 * d;
+    hipLaunchKernelGGL(topk_hist_kernel<BITS>, grid, kBlock, 0, s, keys, S, shift, st);
     hipLaunchKernelGGL(topk_digit_kernel, 1, kBlock, 0, s, st, shift);
   }
-  uint32_t cgrid = grid > 1024 ? 1024 : grid;
+  const uint32_t cgrid = grid > 1024 ? 1024 : grid;
   const uint64_t per_block = (S + cgrid - 1) / cgrid;
-  hipLaunchKernelGGL(topk_count_kernel, cgrid, kBlock, 0, s, scores, S, per_block, largest, st, cnt);
-  hipLaunchKernelGGL(topk_offsets_kernel, 1, 64, 0, s, cnt, cgrid);
-  hipLaunchKernelGGL(topk_write_kernel, cgrid, kBlock, 0, s, scores, S, per_block, largest, st, cnt, cgrid, keys,
-                     idx);
+  hipLaunchKernelGGL(topk_count_kernel<BITS>, cgrid, kBlock, 0, s, keys, S, per_block, st, cnt);
+  hipLaunchKernelGGL(topk_offsets_kernel, 1, kBlock, 0, s, cnt, cgrid, (uint32_t*)nullptr, 0u);
+  if (!sorted) {
+    // selection order: every key above the threshold by index, then the
+    // threshold ties by index — what the CPU backend's unsorted mode returns
+    hipLaunchKernelGGL(topk_write_kernel<BITS>, cgrid, kBlock, 0, s, keys, S, per_block, st, cnt, cgrid,
+                       (uint32_t*)nullptr, idx_out);
+    PGA_HIP_CHECK(hipGetLastError());
+    return;
+  }
+  hipLaunchKernelGGL(topk_write_kernel<BITS>, cgrid, kBlock, 0, s, keys, S, per_block, st, cnt, cgrid, keys_buf, idx);
   PGA_HIP_CHECK(hipGetLastError());
+  size_t cub_bytes = 0;
+  PGA_HIP_CHECK(hipcub::DeviceRadixSort::SortPairsDescending(nullptr, cub_bytes, keys_buf, keys_sorted, idx, idx_out,
+                                                             (int)k));
   // stable descending sort keeps equal keys in ascending index order
-  PGA_HIP_CHECK(hipcub::DeviceRadixSort::SortPairsDescending(p, cub_bytes, keys, keys_sorted, idx, idx_out, (int)k,
-                                                             0, 32, s));
+  PGA_HIP_CHECK(hipcub::DeviceRadixSort::SortPairsDescending(p, cub_bytes, keys_buf, keys_sorted, idx, idx_out,
+                                                             (int)k, 0, BITS, s));
+}
+}  // namespace
+
+void topk_launch(const float* scores, const uint16_t* keys16, uint32_t key_range, uint64_t S, uint32_t k,
+                 bool largest, bool sorted, uint32_t* idx_out, void* ws, hipStream_t s) {
+  if (k == 0) return;
+  if (k > S) throw std::runtime_error("topk: k > S");
+  if (keys16 && !sorted && key_range >= 2 && key_range <= kTopkMaxRange) {
+    // integer objective, selection order: histogram over the R key values
+    char* p = (char*)ws;
+    TopkState* st = (TopkState*)p;
+    p += align_up(sizeof(TopkState));
+    uint32_t* cnt = (uint32_t*)p;
+    p += align_up(sizeof(uint32_t) * (2 * 1024 + 1));
+    p += 3 * align_up(4ull * k);
+    size_t cub_bytes = 0;
+    PGA_HIP_CHECK(hipcub::DeviceRadixSort::SortPairsDescending(nullptr, cub_bytes, (uint32_t*)nullptr,
+                                                               (uint32_t*)nullptr, (uint32_t*)nullptr,
+                                                               (uint32_t*)nullptr, (int)k));
+    p += align_up(cub_bytes);
+    uint32_t* G = (uint32_t*)p;  // zero on allocation and after every use
+    const uint32_t R = key_range;
+    uint32_t grid = launch_grid(S, kBlock * 16);
+    hipLaunchKernelGGL(topk16_hist_kernel, grid, kBlock, 4 * R, s, keys16, S, R, largest, G);
+    const uint32_t cgrid = grid > 1024 ? 1024 : grid;
+    const uint64_t per_block = (S + cgrid - 1) / cgrid;
+    hipLaunchKernelGGL(topk16_count_kernel, cgrid, kBlock, 0, s, keys16, S, per_block, R, largest, k, G, st, cnt);
+    hipLaunchKernelGGL(topk_offsets_kernel, 1, kBlock, 0, s, cnt, cgrid, G, R);
+    hipLaunchKernelGGL(topk_write_kernel<16>, cgrid, kBlock, 0, s, TopkKeys<16>{scores, keys16, largest}, S,
+                       per_block, st, cnt, cgrid, (uint32_t*)nullptr, idx_out);
+    PGA_HIP_CHECK(hipGetLastError());
+    return;
+  }
+  if (keys16)
+    topk_run<16>(TopkKeys<16>{scores, keys16, largest}, S, k, sorted, idx_out, ws, s);
+  else
+    topk_run<32>(TopkKeys<32>{scores, keys16, largest}, S, k, sorted, idx_out, ws, s);
 }
 
 void gather_rows_launch(const void* rows, const float* scores, uint32_t row_words, const uint32_t* idx, uint32_t n,

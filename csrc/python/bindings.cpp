@@ -161,13 +161,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
              return py::make_tuple(s[0], s[1], s[2], s[3]);
            })
       .def("topk",
-           [](const IslandPtr& i, uint32_t k, bool largest) {
+           [](const IslandPtr& i, uint32_t k, bool largest, bool sorted) {
              bind_stream(*i);
              auto out = torch::empty({(int64_t)k}, torch::TensorOptions().dtype(torch::kInt32).device(dev_of(*i)));
-             i->topk(k, largest, (uint32_t*)out.data_ptr<int32_t>());
+             i->topk(k, largest, (uint32_t*)out.data_ptr<int32_t>(), sorted);
              return out;
            },
-           py::arg("k"), py::arg("largest") = true)
+           py::arg("k"), py::arg("largest") = true, py::arg("sorted") = true)
       .def("rows",
            [](const IslandPtr& i, int which) {
              return view(i, i->rows(which), {(int64_t)i->config().S, (int64_t)i->row_words()}, torch::kInt32);

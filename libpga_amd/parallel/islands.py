@@ -145,7 +145,7 @@ class IslandModel:
         if self.world == 1 or self.k == 0 or self.degraded:
             return
         isl = self.ga.island
-        idx = isl.topk(self.k, True)
+        idx = isl.topk(self.k, True, False)
         srows, sscores = self._views(self.send)
         isl.gather(idx, srows, sscores)
         if self.topology == "all_to_all":
@@ -214,7 +214,7 @@ class IslandModel:
             isl.evaluate_rows(rows, scores)  # trust nothing from the wire
             if self.ga.problem.encoding == "permutation":
                 self._sanitize_perm(rows, scores)
-        victims = isl.topk(self.k, False)
+        victims = isl.topk(self.k, False, False)
         isl.scatter(victims, rows, scores)  # also refreshes best + keys
         self.migrations += 1
 

@@ -79,7 +79,7 @@ class LocalIslands:
         out = []
         for i in order:  # take every island's emigrants before any is replaced
             isl = self.islands[i].island
-            idx = isl.topk(self.k, True)
+            idx = isl.topk(self.k, True, False)
             rows = torch.empty(self.k * int(isl.row_words), dtype=torch.int32, device=self.device)
             sc = torch.empty(self.k, dtype=torch.float32, device=self.device)
             isl.gather(idx, rows, sc)
@@ -88,7 +88,7 @@ class LocalIslands:
         for j, i in enumerate(order):
             dst = self.islands[order[(j + 1) % n]].island
             rows, sc = out[j]
-            dst.scatter(dst.topk(self.k, False), rows, sc)
+            dst.scatter(dst.topk(self.k, False, False), rows, sc)
         self._epoch += 1
         self.migrations += 1
 

@@ -135,3 +135,27 @@ def test_headline_config_converges():
     ref = ga.problem.reference_fitness(ga.genomes())
     assert torch.equal(ref, ga.scores)
     assert ga.best_score() > b0 + 20
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("problem", ["onemax", "knapsack_like"])
+@pytest.mark.parametrize("sorted_", [True, False])
+def test_gpu_topk_matches_cpu(problem, sorted_):
+    """Device top-k (u16-key path for integer objectives, f32 path otherwise),
+    sorted and selection order, equals the CPU backend's."""
+    S = 200_000
+    p = pga.models.OneMax(300) if problem == "onemax" else pga.models.Rastrigin(12)
+    g = pga.GeneticAlgorithm(p, S, seed=5, device="cuda:0", elitism=1)
+    c = pga.GeneticAlgorithm(p, S, seed=5, device="cpu", elitism=1)
+    g.run(3)
+    c.run(3)
+    torch.cuda.synchronize()
+    if problem == "onemax":
+        assert torch.equal(g.scores.cpu(), c.scores)
+    else:  # REAL rows can differ by ulps: use the GPU scores on both sides
+        c.island.scores(0).copy_(g.scores.cpu())
+    for k in (1, 7, 2000, 10486):
+        for largest in (True, False):
+            a = g.island.topk(k, largest, sorted_).cpu()
+            b = c.island.topk(k, largest, sorted_)
+            assert torch.equal(a, b), (k, largest, sorted_)
