@@ -3,6 +3,7 @@
 IslandModel does except the RCCL transfer itself): top-k emigrants, pack,
 bottom-k victims, scatter, best/key refresh.  Prints one JSON line."""
 import json
+import types
 import os
 import sys
 
@@ -48,5 +49,44 @@ def main():
     print(json.dumps(res))
 
 
-if __name__ == "__main__":
+if __name__ == "__main__" and not os.environ.get("PGA_LOOPBACK"):
     main()
+
+
+def loopback_overhead(S=1 << 20, every=10, gens=200):
+    """Generations/s of a 2-island ring whose transfer is a device copy
+    (one GPU): the island-model overhead the driver's N>1 runs pay, minus xGMI."""
+    import torch.distributed as dist
+    from libpga_amd.parallel import IslandModel
+
+    class Done:
+        def wait(self, *a):
+            return True
+
+    def fake_batch(ops):
+        ops[1].tensor.copy_(ops[0].tensor)
+        return [Done()]
+
+    dist.batch_isend_irecv = fake_batch
+    dist.P2POp = lambda op, t, peer, group=None: types.SimpleNamespace(op=op, tensor=t)
+    out = {}
+    for side in (False, True):
+        ga = pga.GeneticAlgorithm(pga.models.OneMax(1024), S, seed=1, device="cuda:0", elitism=1)
+        m = IslandModel(ga, migrate_every=every, migrate_pct=0.01)
+        m.world, m.rank = 2, 0
+        if not side:
+            m._side = None
+        m.run(20)
+        torch.cuda.synchronize()
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        m.run(gens)
+        m.flush()
+        b.record()
+        b.synchronize()
+        out["us_per_gen_" + ("overlap" if side else "serial")] = a.elapsed_time(b) / gens * 1e3
+    print(json.dumps(out))
+
+
+if __name__ == "__main__" and os.environ.get("PGA_LOOPBACK"):
+    loopback_overhead()

@@ -119,6 +119,10 @@ class IslandModel:
         self.send = torch.empty(n, dtype=torch.int32, device=dev)
         self.recv = torch.empty(n, dtype=torch.int32, device=dev)
         self._pending = None
+        # emigrant selection + packing run on a side stream, concurrently with
+        # the next generation kernel (they only read the current generation)
+        # (not with elitism > 1: the elite top-k shares the island's selection workspace)
+        self._side = torch.cuda.Stream(dev) if dev.type == "cuda" and ga.operators.elitism <= 1 else None
         self._epoch = 0
         self.migrations = 0
         self.bytes_sent = 0
@@ -144,23 +148,33 @@ class IslandModel:
         """Pack the top-k emigrants and post the exchange (asynchronous)."""
         if self.world == 1 or self.k == 0 or self.degraded:
             return
+        if self._side is not None:
+            self._side.wait_stream(torch.cuda.current_stream(self._side.device))
+            with torch.cuda.stream(self._side):
+                ok = self._post()
+        else:
+            ok = self._post()
+        if ok:
+            self._epoch += 1
+        self.bytes_sent += self.send.numel() * 4
+
+    def _post(self) -> bool:
         isl = self.ga.island
         idx = isl.topk(self.k, True, False)
         srows, sscores = self._views(self.send)
         isl.gather(idx, srows, sscores)
         if self.topology == "all_to_all":
             self._pending = self._a2a()
-        else:
-            dst, src = self._peers()
-            ops = [dist.P2POp(dist.isend, self.send, dst, group=self.group),
-                   dist.P2POp(dist.irecv, self.recv, src, group=self.group)]
-            try:
-                self._pending = dist.batch_isend_irecv(ops)
-            except Exception as e:  # noqa: BLE001 — any comm failure degrades
-                self._fail(e)
-                return
-        self._epoch += 1
-        self.bytes_sent += self.send.numel() * 4
+            return True
+        dst, src = self._peers()
+        ops = [dist.P2POp(dist.isend, self.send, dst, group=self.group),
+               dist.P2POp(dist.irecv, self.recv, src, group=self.group)]
+        try:
+            self._pending = dist.batch_isend_irecv(ops)
+        except Exception as e:  # noqa: BLE001 — any comm failure degrades
+            self._fail(e)
+            return False
+        return True
 
     def _a2a(self):
         # every peer gets an equal slice of the emigrants; self slice is empty
@@ -186,6 +200,9 @@ class IslandModel:
         """Wait for the exchange and replace the worst individuals."""
         if self._pending is None:
             return
+        if self._side is not None:
+            # the next generation must not overwrite rows the side stream still packs
+            torch.cuda.current_stream(self._side.device).wait_stream(self._side)
         try:
             for wk in self._pending:
                 ok = wk.wait(self.timeout) if self.timeout is not None else wk.wait()

@@ -1,6 +1,7 @@
 """Island model across processes (torch.distributed, gloo on CPU; the same
 code path uses RCCL on GPUs)."""
 import os
+import types
 import socket
 import subprocess
 import sys
@@ -66,3 +67,44 @@ def test_island_model_multiprocess(world, topology, tmp_path):
         assert x["global"] == gmax and x["gmax"] == gmax
         assert x["genome_sum"] == gmax  # OneMax: broadcast genome matches the global best score
         assert x["best"] > x["b0"]
+
+
+class _Done:
+    def wait(self, *a):
+        return True
+
+
+def _loopback_model(side: bool):
+    """A 2-island ring whose 'network' is a device copy send -> recv on the
+    posting stream: exercises the stream ordering of the overlapped migration
+    on one GPU (RCCL allows one rank per device)."""
+    import libpga_amd as pga
+    from libpga_amd.parallel import IslandModel
+
+    ga = pga.GeneticAlgorithm(pga.models.OneMax(512), 50_000, seed=3, device="cuda:0", elitism=1)
+    m = IslandModel(ga, migrate_every=3, migrate_pct=0.02)
+    m.world, m.rank = 2, 0
+    if not side:
+        m._side = None
+    return m
+
+
+@pytest.mark.gpu
+def test_overlapped_migration_stream_order_gpu(monkeypatch):
+    import torch.distributed as dist
+
+    def fake_batch(ops):
+        send = next(o.tensor for o in ops if o.op is dist.isend)
+        recv = next(o.tensor for o in ops if o.op is dist.irecv)
+        recv.copy_(send)  # on the current (side) stream, like the NCCL stream would after waiting on it
+        return [_Done()]
+
+    monkeypatch.setattr(dist, "batch_isend_irecv", fake_batch)
+    monkeypatch.setattr(dist, "P2POp", lambda op, t, peer, group=None: types.SimpleNamespace(op=op, tensor=t))
+    a, b = _loopback_model(True), _loopback_model(False)
+    assert a._side is not None
+    a.run(31)
+    b.run(31)
+    torch.cuda.synchronize()
+    assert a.migrations == b.migrations == 10
+    assert torch.equal(a.ga.rows, b.ga.rows) and torch.equal(a.ga.scores, b.ga.scores)
