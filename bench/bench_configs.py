@@ -8,7 +8,8 @@ Configs (BASELINE.md "Targets" table):
   onemax1024        OneMax 1024-bit, pop=1M, one GPU (the headline island)
   rastrigin30       Rastrigin-30D float, pop=1M (blend + gaussian)
   rastrigin30_rot   Rastrigin-30D rotated, pop=1M (fitness through MFMA tiles)
-  tsp256_ox / _pmx  TSP-256 permutation, pop=256K, OX / PMX crossover
+  tsp256_ox / _pmx  TSP-256 permutation, pop=256K, OX / PMX crossover (distance matrix)
+  tsp256_euc_*      the same instance as city coordinates (TSPEuclidean)
   e1_sum100_refops  reference example E1 (S=40000, L=100) with the reference's
                     operators — the head-to-head against build/bench/refsem
   e2_knap_refops    reference example E2 (S=100, L=6), launch-bound (hipGraph)
@@ -57,6 +58,13 @@ def make(name: str):
         return M.ReferenceKnapsack(), 100, None, {}, 5000
     if name == "onemax64_gpu":
         return M.OneMax(64), 1024, None, {}, 5000
+    if name in ("tsp256_euc_ox", "tsp256_euc_pmx"):
+        # the same 256-city instance as tsp256_*, given as coordinates: the
+        # fused kernel stages them in LDS instead of gathering matrix entries from L2
+        g = torch.Generator().manual_seed(7)
+        xy = torch.rand(256, 2, generator=g)
+        xo = "ox" if name.endswith("ox") else "pmx"
+        return M.TSPEuclidean(xy), 1 << 18, None, dict(elitism=1, crossover=xo), 50
     if name in ("tsp256_ox", "tsp256_pmx"):
         g = torch.Generator().manual_seed(7)
         xy = torch.rand(256, 2, generator=g)
@@ -67,7 +75,7 @@ def make(name: str):
 
 
 NAMES = ["onemax64_cpu", "onemax1024", "rastrigin30", "rastrigin30_rot", "tsp256_ox", "tsp256_pmx", "e1_sum100_refops",
-         "e2_knap_refops", "onemax64_gpu", "onemax1024_jit"]
+         "tsp256_euc_ox", "tsp256_euc_pmx", "e2_knap_refops", "onemax64_gpu", "onemax1024_jit"]
 
 
 def run_one(name: str, steps_scale: float) -> dict:

@@ -100,7 +100,7 @@ uint32_t perm_run(int mode, const GenArgs& a, unsigned long long* best_parts) {
         float d;
         if (a.objective == OBJ_TSP_EUC) {
           const float dx = a.obj_data[2 * u] - a.obj_data[2 * w], dy = a.obj_data[2 * u + 1] - a.obj_data[2 * w + 1];
-          d = std::sqrt(dx * dx + dy * dy);
+          d = std::sqrt(std::fma(dx, dx, dy * dy));  // explicit: same rounding as the kernels
         } else {
           d = a.obj_data[u * L + w];
         }

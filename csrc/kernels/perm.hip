@@ -246,7 +246,7 @@ __global__ __launch_bounds__(kBlock) void perm_kernel(GenArgs a, unsigned long l
                            w = min((e < 7 && p + 1 < L) ? e8[e + 1] : (uint32_t)Cc[(p + 1 == L) ? 0 : p + 1], L - 1);
             if (OBJ == OBJ_TSP_EUC) {
               const float dx = coords[2 * u] - coords[2 * w], dy = coords[2 * u + 1] - coords[2 * w + 1];
-              len += sqrtf(dx * dx + dy * dy);
+              len += sqrtf(fmaf(dx, dx, dy * dy));
             } else {
               len += a.obj_data[u * L + w];
             }
@@ -266,6 +266,229 @@ __global__ __launch_bounds__(kBlock) void perm_kernel(GenArgs a, unsigned long l
     unsigned long long b = block_max_u64(my_best, lds_red);
     if (threadIdx.x == 0) best_parts[blockIdx.x] = b;
   }
+}
+
+
+// ---------------------------------------------------------------------------
+// Fast GEN path for rows of at most 64 chunks (L <= 512 cities): one chunk per
+// lane, so a child never leaves its wave.  Everything a child needs from LDS
+// (parent B for PMX chains, the city -> position map, the OX scatter target)
+// is exchanged inside the wave with wave-level barriers instead of
+// __syncthreads: the four waves of a block drift independently and hide each
+// other's latency.  Parent chunks, the child chunk and the tour edges live in
+// registers (one dwordx4 per row per lane; the edge to the next lane's first
+// city is a shuffle).  Same operator semantics as perm_kernel (bit-exact).
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// u16 gene e (0..7, a compile-time constant after unrolling) of a packed chunk
+__device__ __forceinline__ uint32_t get16(const uint4& v, uint32_t e) {
+  const uint32_t w = e < 2 ? v.x : (e < 4 ? v.y : (e < 6 ? v.z : v.w));
+  return (e & 1u) ? (w >> 16) : (w & 0xFFFFu);
+}
+__device__ __forceinline__ uint4 set16(uint4 v, uint32_t e, uint32_t x) {
+  const uint32_t sh = (e & 1u) * 16u, m = 0xFFFFu << sh;
+  if (e < 2) v.x = (v.x & ~m) | (x << sh);
+  else if (e < 4) v.y = (v.y & ~m) | (x << sh);
+  else if (e < 6) v.z = (v.z & ~m) | (x << sh);
+  else v.w = (v.w & ~m) | (x << sh);
+  return v;
+}
+
+template <int GS, int OBJ>
+__global__ __launch_bounds__(kBlock) void perm_gen_fast(GenArgs a, unsigned long long* best_parts) {
+  resolve_gen(a);
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  unsigned long long* lds_red = (unsigned long long*)smem;
+  uint32_t* lds_elite = (uint32_t*)(smem + 8);
+  const uint32_t L = a.L, nch = a.chunks, lp = 8 * nch;
+  float* coords = smem + kHdrF;
+  uint16_t* arena = (uint16_t*)(coords + (OBJ == OBJ_TSP_EUC ? 16 * nch : 0));
+
+  const uint32_t lane = lane_id();
+  const uint32_t q = lane & (GS - 1);
+  const uint32_t gbase = lane & ~(uint32_t)(GS - 1);
+  constexpr uint32_t GPB = kBlock / GS;
+  const uint32_t g = threadIdx.x / GS;
+  uint16_t* B = arena + (size_t)g * 4 * lp + lp;
+  uint16_t* Cc = B + lp;
+  uint16_t* Mp = Cc + lp;
+  const uint64_t rs = a.row_words >> 2;
+  const uint4* cur = (const uint4*)a.cur;
+  uint4* nxt = (uint4*)a.next;
+  const bool have = q < nch;
+  const uint32_t qc = have ? q : nch - 1;
+  const bool mut_on = a.mutation == MUT_SWAP || a.mutation == MUT_INVERSION;
+  const bool xo_kind = a.crossover == XO_PMX || a.crossover == XO_OX;
+  const bool pmx = a.crossover == XO_PMX;
+  const uint32_t S32 = (uint32_t)a.S;
+
+  if (a.n_elite > 0 && a.elite_idx == nullptr && blockIdx.x == 0) {
+    unsigned long long b = block_reduce_parts(a.best_cur, a.n_best_cur, lds_red);
+    if (threadIdx.x == 0) *lds_elite = (uint32_t)best_index(b);
+  }
+  if (OBJ == OBJ_TSP_EUC)
+    for (uint32_t i = threadIdx.x; i < 2 * L; i += kBlock) coords[i] = a.obj_data[i];
+  __syncthreads();
+
+  unsigned long long my_best = 0;
+  for (uint64_t base = (uint64_t)blockIdx.x * GPB; base < a.S; base += (uint64_t)gridDim.x * GPB) {
+    const uint64_t child = base + g;
+    const bool valid = child < a.S;  // group-uniform
+    const uint64_t ch = valid ? child : a.S - 1;
+    const Pool<GS> pool{draw(a.key, ST_CHILD, ch, q), gbase};
+    uint32_t pa, pb;
+    select_parents<GS>(a, pool, ch, pa, pb);
+    const bool elite = ch < a.n_elite;
+    if (elite) {
+      pa = a.elite_idx ? a.elite_idx[ch] : *lds_elite;
+      pb = pa;
+    }
+    const bool xo = !elite && xo_kind && do_crossover(a, pool.get(W_XOPROB, a.key, ch));
+    uint32_t lo, hi;
+    perm_segment(pool.get(W_CUT1, a.key, ch), pool.get(W_CUT2, a.key, ch), L, lo, hi);
+    // parent / child chunks stay packed (8 x u16 in 4 VGPRs each)
+    const uint4 Av = cur[(uint64_t)pa * rs + qc];
+    const uint4 Bv = cur[(uint64_t)pb * rs + qc];
+    uint4 Cv = Av;
+    float score = 0.f;
+    if (elite) score = a.score_cur[pa];
+
+    if (xo) {  // group-uniform
+      if (have) {
+        *(uint4*)(Mp + 8 * q) = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu);
+        if (pmx) *(uint4*)(B + 8 * q) = Bv;  // PMX follows chains through B
+      }
+      wave_sync();
+#pragma unroll
+      for (uint32_t e = 0; e < 8; ++e) {
+        const uint32_t k = 8 * q + e;
+        if (have && k >= lo && k < hi) Mp[get16(Av, e)] = (uint16_t)k;  // city -> its position in A's segment
+      }
+      wave_sync();
+      if (pmx) {
+#pragma unroll
+        for (uint32_t e = 0; e < 8; ++e) {
+          const uint32_t p = 8 * q + e;
+          uint32_t v = get16(Bv, e);
+          if (p < L && !(p >= lo && p < hi))
+            for (uint32_t guard = 0; Mp[v] != kNone && guard < L; ++guard) v = B[Mp[v]];
+          Cv = set16(Cv, e, p >= L ? 0u : ((p >= lo && p < hi) ? get16(Av, e) : v));
+        }
+      } else {  // OX1 (same ranks as perm_kernel)
+        uint32_t keep = 0, eb_part = 0;
+#pragma unroll
+        for (uint32_t e = 0; e < 8; ++e) {
+          const uint32_t p = 8 * q + e;
+          const bool k = have && p < L && Mp[get16(Bv, e)] == kNone;
+          keep |= k ? (1u << e) : 0u;
+          eb_part += (k && p < hi) ? 1u : 0u;
+        }
+        const uint32_t Eb = group_sum_u<GS>(eb_part);
+        const uint32_t K = L - (hi - lo), tail = L - hi;
+        uint32_t seg_total;
+        uint32_t run = group_excl_scan<GS>(__popc(keep), q, seg_total);
+#pragma unroll
+        for (uint32_t e = 0; e < 8; ++e) {
+          const uint32_t p = 8 * q + e;
+          if (have && p >= L) Cc[p] = 0;
+          if (have && p < L && p >= lo && p < hi) Cc[p] = (uint16_t)get16(Av, e);
+          if ((keep >> e) & 1u) {
+            const uint32_t r = p >= hi ? run - Eb : (K - Eb) + run;
+            const uint32_t pos = r < tail ? hi + r : r - tail;
+            Cc[pos] = (uint16_t)get16(Bv, e);
+            ++run;
+          }
+        }
+        wave_sync();
+        Cv = *(const uint4*)(Cc + 8 * qc);
+      }
+    }
+
+    if (!elite && mut_on && pool.get(W_MUTIND, a.key, ch) < a.mut_ind_thresh) {  // group-uniform
+      uint32_t i, j;
+      perm_mut_positions(pool.get(W_MUTPOS, a.key, ch), pool.get(W_SEL + sel_words(a), a.key, ch), L, i, j);
+      wave_sync();  // earlier readers of C are done
+      if (have) *(uint4*)(Cc + 8 * q) = Cv;
+      wave_sync();
+      if (a.mutation == MUT_SWAP) {
+        if (q == 0) {
+          const uint16_t t = Cc[i];
+          Cc[i] = Cc[j];
+          Cc[j] = t;
+        }
+      } else {
+        const uint32_t half = (j - i + 1) / 2;
+        for (uint32_t t = q; t < half; t += GS) {
+          const uint16_t x = Cc[i + t];
+          Cc[i + t] = Cc[j - t];
+          Cc[j - t] = x;
+        }
+      }
+      wave_sync();
+      Cv = *(const uint4*)(Cc + 8 * qc);
+    }
+    wave_sync();  // the next child of this group rewrites B / C / M
+
+    if (valid && have) nxt[child * rs + q] = Cv;
+    if (!elite) {
+      // edges (p, p+1) and the closing edge; the city after a lane's chunk is
+      // the next lane's first city
+      const uint32_t c0 = Cv.x & 0xFFFFu;
+      const uint32_t next_first = (uint32_t)__shfl((int)c0, (int)(gbase + ((q + 1) & (GS - 1))), 64);
+      const uint32_t first = (uint32_t)__shfl((int)c0, (int)gbase, 64);
+      const uint32_t last = (OBJ == OBJ_TSP_OPEN) ? L - 1 : L;
+      float len = 0.f;
+      if (OBJ == OBJ_TSP_EUC) {
+        // one float2 per city of the chunk (+ the following city), reused by both edge ends
+        const float2* xy = (const float2*)coords;
+        float2 pu = xy[min(get16(Cv, 0), L - 1)];
+#pragma unroll
+        for (uint32_t e = 0; e < 8; ++e) {
+          const uint32_t p = 8 * q + e;
+          const uint32_t nx = p + 1 < L ? (e < 7 ? get16(Cv, e + 1) : next_first) : first;
+          const float2 pw = xy[min(nx, L - 1)];
+          if (have && p < last) {
+            const float dx = pu.x - pw.x, dy = pu.y - pw.y;
+            len += sqrtf(fmaf(dx, dx, dy * dy));
+          }
+          pu = pw;
+        }
+      } else {
+#pragma unroll
+        for (uint32_t e = 0; e < 8; ++e) {
+          const uint32_t p = 8 * q + e;
+          if (have && p < last) {
+            const uint32_t nx = p + 1 < L ? (e < 7 ? get16(Cv, e + 1) : next_first) : first;
+            const uint32_t u = min(get16(Cv, e), L - 1), w = min(nx, L - 1);
+            len += a.obj_data[u * L + w];
+          }
+        }
+      }
+      score = -group_sum<GS>(len);
+    }
+    if (valid && q == 0) {
+      a.score_next[child] = score;
+      const unsigned long long pb2 = pack_best(score, child);
+      my_best = pb2 > my_best ? pb2 : my_best;
+    }
+  }
+  if (best_parts) {
+    unsigned long long b = block_max_u64(my_best, lds_red);
+    if (threadIdx.x == 0) best_parts[blockIdx.x] = b;
+  }
+}
+
+bool perm_fast_enabled() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("PGA_PERM_FAST");
+    v = (e && e[0] == '0') ? 0 : 1;
+  }
+  return v == 1;
 }
 
 template <int GS, int MODE, int OBJ>
@@ -290,9 +513,32 @@ uint32_t go(const GenArgs& a, unsigned long long* parts, hipStream_t s) {
 }
 
 template <int GS, int OBJ>
+uint32_t go_fast(const GenArgs& a, unsigned long long* parts, hipStream_t s) {
+  const size_t lds = perm_lds_bytes(GS, a.chunks, OBJ == OBJ_TSP_EUC);
+  auto k = perm_gen_fast<GS, OBJ>;
+  static bool configured = false;
+  if (!configured) {
+    PGA_HIP_CHECK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    configured = true;
+  }
+  const uint32_t gpb = kBlock / GS;
+  const uint64_t need = (a.S + gpb - 1) / gpb;
+  int per_cu = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)k, kBlock, lds) != hipSuccess || per_cu <= 0)
+    per_cu = 1;
+  uint64_t cap = (uint64_t)device_cu_count() * per_cu;
+  if (cap > kMaxGrid) cap = kMaxGrid;
+  const uint32_t grid = (uint32_t)(need < cap ? need : cap);
+  hipLaunchKernelGGL(k, grid, kBlock, lds, s, a, parts);
+  return grid;
+}
+
+template <int GS, int OBJ>
 uint32_t launch_mode(int mode, const GenArgs& a, unsigned long long* parts, hipStream_t s) {
   switch (mode) {
-    case MODE_GEN: return go<GS, MODE_GEN, OBJ>(a, parts, s);
+    case MODE_GEN:
+      if (OBJ != OBJ_NONE && a.chunks <= (uint32_t)GS && perm_fast_enabled()) return go_fast<GS, OBJ>(a, parts, s);
+      return go<GS, MODE_GEN, OBJ>(a, parts, s);
     case MODE_INIT: return go<GS, MODE_INIT, OBJ>(a, parts, s);
     case MODE_EVAL: return go<GS, MODE_EVAL, OBJ>(a, parts, s);
     case MODE_CROSS: return go<GS, MODE_CROSS, OBJ_NONE>(a, parts, s);
