@@ -123,8 +123,24 @@ PGA_HD bool real_obj_rotatable(int32_t obj) {
          obj == OBJ_GRIEWANK || obj == OBJ_SCHWEFEL;
 }
 
-// term for dimension g (z = its value, zn = value of dimension g+1 when it exists)
-PGA_HD void real_obj_term(const GenArgs& a, uint32_t g, float z, float zn, float x, RealAcc& acc) {
+// per-dimension problem data of the objectives that have any (LINEAR weight;
+// KNAPSACK_REAL value w0 and weight w1) — loop-invariant per lane, so the
+// pipelined kernel loads them once instead of inside its loop
+PGA_HD void real_obj_data(const GenArgs& a, uint32_t g, float& w0, float& w1) {
+  w0 = 1.f;
+  w1 = 0.f;
+  if (a.objective == OBJ_LINEAR) {
+    w0 = a.obj_data ? a.obj_data[g] : 1.f;
+  } else if (a.objective == OBJ_KNAPSACK_REAL) {
+    w0 = a.obj_data[g];
+    w1 = a.obj_data[a.L + g];
+  }
+}
+
+// term for dimension g (z = its value, zn = value of dimension g+1 when it
+// exists, w0/w1 = real_obj_data(g))
+PGA_HD void real_obj_term_w(const GenArgs& a, uint32_t g, float z, float zn, float x, float w0, float w1,
+                            RealAcc& acc) {
   switch (a.objective) {
     case OBJ_SPHERE: acc.s0 += z * z; break;
     case OBJ_RASTRIGIN: acc.s0 += z * z - 10.f * cosf(2.f * kPi * z) + 10.f; break;
@@ -143,15 +159,21 @@ PGA_HD void real_obj_term(const GenArgs& a, uint32_t g, float z, float zn, float
       acc.s2 *= cosf(z / sqrtf((float)(g + 1)));
       break;
     case OBJ_SCHWEFEL: acc.s0 += z * sinf(sqrtf(fabsf(z))); break;
-    case OBJ_LINEAR: acc.s0 += (a.obj_data ? a.obj_data[g] : 1.f) * x; break;
+    case OBJ_LINEAR: acc.s0 += w0 * x; break;
     case OBJ_KNAPSACK_REAL: {  // reference E2: count = (int)(g * max_count)
       const float cnt = (float)(int)(x * (float)a.obj_i);
-      acc.s0 += a.obj_data[g] * cnt;
-      acc.s1 += a.obj_data[a.L + g] * cnt;
+      acc.s0 += w0 * cnt;
+      acc.s1 += w1 * cnt;
       break;
     }
     default: break;
   }
+}
+
+PGA_HD void real_obj_term(const GenArgs& a, uint32_t g, float z, float zn, float x, RealAcc& acc) {
+  float w0, w1;
+  real_obj_data(a, g, w0, w1);
+  real_obj_term_w(a, g, z, zn, x, w0, w1, acc);
 }
 
 PGA_HD float real_obj_finish(const GenArgs& a, const RealAcc& t) {

@@ -276,7 +276,9 @@ template <typename K>
 uint32_t launch_occ(K k, uint32_t children_per_block, size_t lds, const GenArgs& a, unsigned long long* parts,
                     hipStream_t s, bool& configured) {
   if (!configured) {
-    PGA_HIP_CHECK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    // only the dynamic-LDS kernels may need more than the default 64 KiB
+    if (lds > 0)
+      PGA_HIP_CHECK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     configured = true;
   }
   uint64_t need = (a.S + children_per_block - 1) / children_per_block;
@@ -531,6 +533,200 @@ __global__ __launch_bounds__(kBlock) void real_gen_fast(GenArgs a, unsigned long
   }
 }
 
+
+// ---------------------------------------------------------------------------
+// Software-pipelined GEN kernel (non-rotated objectives), the REAL analogue of
+// binary_gen_pipe: three children per lane group in flight — contestant score
+// loads of c+2, parent-row loads of c+1 and the variation / objective of c in
+// one loop body, three static register sets rotating X -> Y -> Z so hipcc's
+// vmcnt waits stay exact (every load is issued unconditionally; tail children
+// are clamped, lanes without a chunk re-read the last chunk).  Tournament-2 or
+// random selection, any crossover / mutation, objectives that need no
+// neighbouring dimension.  Same semantics as real_kernel (bit-exact).
+template <int GS, int OBJ>
+__global__ __launch_bounds__(kBlock) void real_gen_pipe(GenArgs a, unsigned long long* best_parts) {
+  resolve_gen(a);
+  a.objective = OBJ;  // compile-time objective: the term switches fold away
+  __shared__ unsigned long long lds_red[kBlock / 64];
+  __shared__ uint32_t lds_elite;
+  __shared__ uint32_t lds_thr[kMutCap];
+
+  const uint32_t lane = lane_id();
+  const uint32_t q = lane & (GS - 1);
+  const uint32_t gbase = lane & ~(uint32_t)(GS - 1);
+  constexpr uint32_t GPB = kBlock / GS;
+  const uint64_t rs = a.row_words >> 2;
+  const float4* cur = (const float4*)a.cur;
+  float4* nxt = (float4*)a.next;
+  const uint32_t L = a.L;
+  const uint32_t S32 = (uint32_t)a.S;
+  const bool have = q < a.chunks;
+  const uint32_t qc = have ? q : a.chunks - 1;
+  const uint32_t clen = have ? (L - 4 * q >= 4 ? 4u : L - 4 * q) : 0u;
+  const bool tour2 = a.selection == SEL_TOURNAMENT;
+  const bool xo_on = a.crossover != XO_NONE;
+  const bool per_gene_mut = (a.mutation == MUT_GAUSSIAN || a.mutation == MUT_UNIFORM) && a.mut_rate > 0.f;
+  const bool reset_one = a.mutation == MUT_RESET_ONE;
+  const bool evals = a.objective != OBJ_NONE;
+  const bool shift = (a.obj_i & 1) && a.obj_data2 && real_obj_rotatable(a.objective);
+  // loop-invariant per-lane problem data (no conditional loads inside the pipeline)
+  float sh[4], w0[4], w1[4];
+#pragma unroll
+  for (uint32_t j = 0; j < 4; ++j) {
+    const uint32_t d = 4 * q + j;
+    sh[j] = (shift && d < L) ? a.obj_data2[d] : 0.f;
+    w0[j] = 1.f;
+    w1[j] = 0.f;
+    if (evals && d < L) real_obj_data(a, d, w0[j], w1[j]);
+  }
+
+  if (a.n_elite > 0 && a.elite_idx == nullptr && blockIdx.x == 0) {
+    unsigned long long b = block_reduce_parts(a.best_cur, a.n_best_cur, lds_red);
+    if (threadIdx.x == 0) lds_elite = (uint32_t)best_index(b);
+  }
+  if (per_gene_mut)
+    for (uint32_t i = threadIdx.x; i < kMutCap; i += kBlock) lds_thr[i] = a.mut_thr[i];
+  __syncthreads();
+
+  unsigned long long my_best = 0;
+  const uint64_t stride = (uint64_t)gridDim.x * GPB;
+  uint64_t c0 = (uint64_t)blockIdx.x * GPB + threadIdx.x / GS;
+  while (c0 < a.n_elite && c0 < a.S) {  // elites: copy row and score
+    const uint32_t src = a.elite_idx ? a.elite_idx[c0] : lds_elite;
+    if (have) nxt[c0 * rs + q] = cur[(uint64_t)src * rs + q];
+    const float sc = a.score_cur[src];
+    if (q == 0) {
+      a.score_next[c0] = sc;
+      const unsigned long long pb = pack_best(sc, c0);
+      my_best = pb > my_best ? pb : my_best;
+    }
+    c0 += stride;
+  }
+
+#define R_SET(P)                                                      \
+  u32x4 P##w{0, 0, 0, 0};                                             \
+  uint32_t P##i0 = 0, P##i1 = 0, P##i2 = 0, P##i3 = 0;                \
+  float P##t0 = 0.f, P##t1 = 0.f, P##t2 = 0.f, P##t3 = 0.f;           \
+  float4 P##A = make_float4(0.f, 0.f, 0.f, 0.f), P##B = P##A;         \
+  bool P##xo = false;
+  R_SET(X)
+  R_SET(Y)
+  R_SET(Z)
+#undef R_SET
+
+#define R_STAGE1(c, P)                                                 \
+  {                                                                    \
+    const uint64_t cc_ = (c) < a.S ? (c) : a.S - 1;                    \
+    P##w = draw(a.key, ST_CHILD, cc_, q);                              \
+    const Pool<GS> pool_{P##w, gbase};                                 \
+    P##i0 = word_to_index(pool_.get(W_SEL + 0, a.key, cc_), S32);      \
+    P##i1 = word_to_index(pool_.get(W_SEL + 1, a.key, cc_), S32);      \
+    P##i2 = word_to_index(pool_.get(W_SEL + 2, a.key, cc_), S32);      \
+    P##i3 = word_to_index(pool_.get(W_SEL + 3, a.key, cc_), S32);      \
+    P##t0 = a.score_cur[P##i0];                                        \
+    P##t1 = a.score_cur[P##i1];                                        \
+    P##t2 = a.score_cur[P##i2];                                        \
+    P##t3 = a.score_cur[P##i3];                                        \
+  }
+
+#define R_STAGE2(c, P)                                                                          \
+  {                                                                                             \
+    const uint64_t cc_ = (c) < a.S ? (c) : a.S - 1;                                             \
+    uint32_t pa_, pb_;                                                                          \
+    if (tour2) {                                                                                \
+      pa_ = P##i0 ^ ((P##i0 ^ P##i1) & (0u - (uint32_t)(P##t0 < P##t1)));                       \
+      pb_ = P##i2 ^ ((P##i2 ^ P##i3) & (0u - (uint32_t)(P##t2 < P##t3)));                       \
+    } else {                                                                                    \
+      pa_ = P##i0;                                                                              \
+      pb_ = P##i1;                                                                              \
+    }                                                                                           \
+    const Pool<GS> pool_{P##w, gbase};                                                          \
+    P##xo = xo_on && do_crossover(a, pool_.get(W_XOPROB, a.key, cc_));                          \
+    P##A = cur[(uint64_t)pa_ * rs + qc];                                                        \
+    P##B = cur[(uint64_t)pb_ * rs + qc];                                                        \
+  }
+
+#define R_STAGE3(c, P)                                                                          \
+  if ((c) < a.S) {                                                                              \
+    const Pool<GS> pool_{P##w, gbase};                                                          \
+    uint32_t lo_ = 0, hi_ = 0;                                                                  \
+    float ua_ = 0.f;                                                                            \
+    if (a.crossover == XO_ONE_POINT) {                                                          \
+      lo_ = word_to_index(pool_.get(W_CUT1, a.key, (c)), L);                                    \
+      hi_ = L;                                                                                  \
+    } else if (a.crossover == XO_TWO_POINT) {                                                   \
+      const uint32_t x1_ = word_to_index(pool_.get(W_CUT1, a.key, (c)), L);                     \
+      const uint32_t x2_ = word_to_index(pool_.get(W_CUT2, a.key, (c)), L);                     \
+      lo_ = x1_ < x2_ ? x1_ : x2_;                                                              \
+      hi_ = x1_ < x2_ ? x2_ : x1_;                                                              \
+    } else if (a.crossover == XO_ARITHMETIC) {                                                  \
+      ua_ = word_to_unit(pool_.get(W_CUT1, a.key, (c)));                                        \
+    }                                                                                           \
+    const float A_[4] = {P##A.x, P##A.y, P##A.z, P##A.w};                                       \
+    const float B_[4] = {P##B.x, P##B.y, P##B.z, P##B.w};                                       \
+    float v_[4];                                                                                \
+    real_cross_chunk(a, (c), q, A_, B_, P##xo, lo_, hi_, ua_, v_);                              \
+    if (per_gene_mut) {                                                                         \
+      if (have) real_mutate_chunk(a, (c), q, clen, P##w.w, lds_thr, v_);                        \
+    } else if (reset_one && pool_.get(W_MUTIND, a.key, (c)) < a.mut_ind_thresh) {               \
+      const uint32_t pos_ = word_to_index(pool_.get(W_MUTPOS, a.key, (c)), L);                  \
+      const float x_ = real_reset_value(a, pool_.get(W_SEL + sel_words(a), a.key, (c)));        \
+      if ((pos_ >> 2) == q) {                                                                   \
+        v_[0] = fsel(pos_ == 4 * q + 0, x_, v_[0]);                                             \
+        v_[1] = fsel(pos_ == 4 * q + 1, x_, v_[1]);                                             \
+        v_[2] = fsel(pos_ == 4 * q + 2, x_, v_[2]);                                             \
+        v_[3] = fsel(pos_ == 4 * q + 3, x_, v_[3]);                                             \
+      }                                                                                         \
+    }                                                                                           \
+    for (uint32_t j = 0; j < 4; ++j) v_[j] = j < clen ? v_[j] : 0.f;                            \
+    if (have) nxt[(c) * rs + q] = make_float4(v_[0], v_[1], v_[2], v_[3]);                      \
+    if (evals) {                                                                                \
+      RealAcc acc_{0.f, 0.f, 1.f};                                                              \
+      _Pragma("unroll") for (uint32_t j = 0; j < 4; ++j) {                                      \
+        const uint32_t d_ = 4 * q + j;                                                          \
+        if (d_ < L) real_obj_term_w(a, d_, v_[j] - sh[j], 0.f, v_[j], w0[j], w1[j], acc_);      \
+      }                                                                                         \
+      acc_.s0 = group_sum<GS>(acc_.s0);                                                         \
+      acc_.s1 = group_sum<GS>(acc_.s1);                                                         \
+      acc_.s2 = group_prod<GS>(acc_.s2);                                                        \
+      const float sc_ = real_obj_finish(a, acc_);                                               \
+      if (q == 0) {                                                                             \
+        a.score_next[(c)] = sc_;                                                                \
+        const unsigned long long pb_ = pack_best(sc_, (c));                                     \
+        my_best = pb_ > my_best ? pb_ : my_best;                                                \
+      }                                                                                         \
+    }                                                                                           \
+  }
+
+  R_STAGE1(c0, X)
+  R_STAGE2(c0, X)
+  R_STAGE1(c0 + stride, Y)
+  while (c0 < a.S) {  // group-uniform
+    R_STAGE1(c0 + 2 * stride, Z)
+    R_STAGE2(c0 + stride, Y)
+    R_STAGE3(c0, X)
+    c0 += stride;
+    if (c0 >= a.S) break;
+    R_STAGE1(c0 + 2 * stride, X)
+    R_STAGE2(c0 + stride, Z)
+    R_STAGE3(c0, Y)
+    c0 += stride;
+    if (c0 >= a.S) break;
+    R_STAGE1(c0 + 2 * stride, Y)
+    R_STAGE2(c0 + stride, X)
+    R_STAGE3(c0, Z)
+    c0 += stride;
+  }
+#undef R_STAGE1
+#undef R_STAGE2
+#undef R_STAGE3
+
+  if (evals && best_parts) {
+    unsigned long long b = block_max_u64(my_best, lds_red);
+    if (threadIdx.x == 0) best_parts[blockIdx.x] = b;
+  }
+}
+
 template <int GS, int U, bool ROT>
 uint32_t go_fast(const GenArgs& a, unsigned long long* parts, hipStream_t s) {
   constexpr uint32_t ROWS = (kBlock / GS) * U;
@@ -563,8 +759,32 @@ bool real_fast_eligible(int mode, const GenArgs& a, bool rot) {
   return true;
 }
 
+bool real_pipe_enabled() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("PGA_REAL_PIPE");
+    v = (e && e[0] == '0') ? 0 : 1;
+  }
+  return v == 1;
+}
+
 template <int GS, bool ROT>
 uint32_t launch_fast(const GenArgs& a, unsigned long long* parts, hipStream_t s) {
+  if (!ROT && real_pipe_enabled()) {
+    static bool c[8] = {false, false, false, false, false, false, false, false};
+    switch (a.objective) {
+      case OBJ_SPHERE: return launch_occ(real_gen_pipe<GS, OBJ_SPHERE>, kBlock / GS, 0, a, parts, s, c[0]);
+      case OBJ_RASTRIGIN: return launch_occ(real_gen_pipe<GS, OBJ_RASTRIGIN>, kBlock / GS, 0, a, parts, s, c[1]);
+      case OBJ_ACKLEY: return launch_occ(real_gen_pipe<GS, OBJ_ACKLEY>, kBlock / GS, 0, a, parts, s, c[2]);
+      case OBJ_GRIEWANK: return launch_occ(real_gen_pipe<GS, OBJ_GRIEWANK>, kBlock / GS, 0, a, parts, s, c[3]);
+      case OBJ_SCHWEFEL: return launch_occ(real_gen_pipe<GS, OBJ_SCHWEFEL>, kBlock / GS, 0, a, parts, s, c[4]);
+      case OBJ_LINEAR: return launch_occ(real_gen_pipe<GS, OBJ_LINEAR>, kBlock / GS, 0, a, parts, s, c[5]);
+      case OBJ_KNAPSACK_REAL:
+        return launch_occ(real_gen_pipe<GS, OBJ_KNAPSACK_REAL>, kBlock / GS, 0, a, parts, s, c[6]);
+      case OBJ_NONE: return launch_occ(real_gen_pipe<GS, OBJ_NONE>, kBlock / GS, 0, a, parts, s, c[7]);
+      default: break;  // Rosenbrock needs the neighbouring dimension: fast path below
+    }
+  }
   switch (real_fast_u()) {
     case 1: return go_fast<GS, 1, ROT>(a, parts, s);
     case 4: return go_fast<GS, 4, ROT>(a, parts, s);
