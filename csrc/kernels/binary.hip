@@ -284,8 +284,10 @@ __device__ __forceinline__ uint4 load_row(const uint4* p) {
   return *p;
 }
 
-template <int GS, int OBJ, int XOK, bool KEY>
-__global__ __launch_bounds__(kBlock) void binary_gen_pipe(GenArgs a, unsigned long long* best_parts) {
+// RESET: the per-individual reset mutation is possible (otherwise only
+// bit-flip / none, and the pool words are dead after stage 2: fewer VGPRs)
+template <int GS, int OBJ, int XOK, bool KEY, bool RESET>
+__global__ __launch_bounds__(kBlock, RESET ? 5 : 6) void binary_gen_pipe(GenArgs a, unsigned long long* best_parts) {
   resolve_gen(a);
   __shared__ unsigned long long lds_red[kBlock / 64];
   __shared__ uint32_t lds_elite;
@@ -306,7 +308,7 @@ __global__ __launch_bounds__(kBlock) void binary_gen_pipe(GenArgs a, unsigned lo
   const bool k2 = a.selection == SEL_TOURNAMENT;  // tour_k == 2 guaranteed by the launcher
   const bool xo_on = a.crossover != XO_NONE;
   const bool bitflip = a.mutation == MUT_BIT_FLIP && a.mut_rate > 0.f;
-  const bool reset_one = a.mutation == MUT_RESET_ONE;
+  const bool reset_one = RESET && a.mutation == MUT_RESET_ONE;
   const uint4 lmask = u4(a.last_mask);
 
   if (a.n_elite > 0 && a.elite_idx == nullptr && blockIdx.x == 0) {
@@ -500,12 +502,17 @@ uint32_t launch_mode(int mode, const GenArgs& a, unsigned long long* parts, hipS
         constexpr bool INT_OBJ = OBJ == OBJ_ONEMAX || OBJ == OBJ_LEADING_ONES || OBJ == OBJ_TRAP;
         const bool key = INT_OBJ && a.key_cur != nullptr;
         const bool range = a.crossover == XO_ONE_POINT || a.crossover == XO_TWO_POINT;
+        const bool reset = a.mutation == MUT_RESET_ONE;
+#define PGA_PIPE(XK, KY)                                                        \
+  return reset ? go(binary_gen_pipe<GS, OBJ, XK, KY, true>, a, parts, gpb, s)   \
+               : go(binary_gen_pipe<GS, OBJ, XK, KY, false>, a, parts, gpb, s);
         if (key) {
-          return range ? go(binary_gen_pipe<GS, OBJ, XOK_RANGE, INT_OBJ>, a, parts, gpb, s)
-                       : go(binary_gen_pipe<GS, OBJ, XOK_UNIFORM, INT_OBJ>, a, parts, gpb, s);
+          if (range) { PGA_PIPE(XOK_RANGE, INT_OBJ) }
+          PGA_PIPE(XOK_UNIFORM, INT_OBJ)
         }
-        return range ? go(binary_gen_pipe<GS, OBJ, XOK_RANGE, false>, a, parts, gpb, s)
-                     : go(binary_gen_pipe<GS, OBJ, XOK_UNIFORM, false>, a, parts, gpb, s);
+        if (range) { PGA_PIPE(XOK_RANGE, false) }
+        PGA_PIPE(XOK_UNIFORM, false)
+#undef PGA_PIPE
       }
       return go(binary_kernel<GS, OBJ, MODE_GEN>, a, parts, gpb, s);
     }
