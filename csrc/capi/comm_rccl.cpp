@@ -1,16 +1,25 @@
-// comm_rccl.cpp — RCCL backend of the C API island model (one process per
-// GPU, xGMI point-to-point links).  The python layer uses torch.distributed
-// (backend "nccl" = RCCL) instead; both speak the same migration protocol:
-// a ring of ranks, top-k emigrants out, worst-k replaced.
+// comm_rccl.cpp — RCCL transports of the C API island model (pga/comm.hpp).
+//
+// MI355X shape: the 8 GPUs of a node are fully connected by xGMI (7
+// point-to-point links per GPU).  A ring migration moves k rows over ONE link
+// per direction; all-to-all spreads k/(n-1) rows over all 7, which is what a
+// large migration wants.  Every transfer of an epoch is posted inside one
+// ncclGroupStart/End, so RCCL schedules the sends and receives of all peers
+// (and, in the one-process ncclCommInitAll mode, of all local GPUs) together.
+// The python layer uses torch.distributed (backend "nccl" = RCCL) instead and
+// speaks the same protocol (libpga_amd/parallel/islands.py).
 //
 // Reference: the original claims "CUDA GPUs+MPI" (README.md:4) but contains no
 // communication code at all.
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <chrono>
 #include <cstring>
+#include <exception>
 #include <stdexcept>
 #include <string>
+#include <thread>
 
 #include "pga/comm.hpp"
 
@@ -20,13 +29,144 @@ namespace {
 void nccl_check(ncclResult_t r, const char* what) {
   if (r != ncclSuccess) throw std::runtime_error(std::string("RCCL ") + what + ": " + ncclGetErrorString(r));
 }
-}  // namespace
 
-struct RcclComm {
-  ncclComm_t comm = nullptr;
-  int nranks = 1, rank = 0;
-  float* dscratch = nullptr;
+struct Group {
+  Group() { nccl_check(ncclGroupStart(), "ncclGroupStart"); }
+  ~Group() noexcept(false) {
+    const ncclResult_t r = ncclGroupEnd();
+    if (!std::uncaught_exceptions()) nccl_check(r, "ncclGroupEnd");  // never throw while unwinding
+  }
 };
+
+class RcclComm final : public Comm {
+ public:
+  // comms_[i] is the communicator of local rank ranks_[i] (one entry per process
+  // in InitRank mode, one per GPU in InitAll mode)
+  RcclComm(std::vector<ncclComm_t> comms, std::vector<int> ranks, int nranks, bool all)
+      : comms_(std::move(comms)), ranks_(std::move(ranks)), n_(nranks), all_(all) {
+    events_.resize(comms_.size(), nullptr);
+  }
+  ~RcclComm() override {
+    for (hipEvent_t e : events_)
+      if (e) (void)hipEventDestroy(e);
+    for (ncclComm_t c : comms_)
+      if (c) (aborted_ ? ncclCommAbort(c) : ncclCommDestroy(c));
+  }
+  int size() const override { return n_; }
+  const char* name() const override { return all_ ? "rccl-all" : "rccl"; }
+  bool drives_all_ranks() const override { return all_; }
+
+  void exchange(const std::vector<Xfer>& plan, std::vector<LocalRank>& local) override {
+    if (aborted_) throw std::runtime_error("RCCL communicator was aborted");
+    {
+      Group g;
+      for (LocalRank& l : local) {
+        ncclComm_t c = comm_of(l.rank);
+        const size_t rb = l.row_bytes;
+        for (const Xfer& x : plan) {
+          if (x.src == l.rank) {
+            nccl_check(ncclSend((const char*)l.send_rows + rb * x.src_off, rb * x.n, ncclUint8, x.dst, c, l.stream),
+                       "ncclSend");
+            nccl_check(ncclSend(l.send_scores + x.src_off, x.n, ncclFloat32, x.dst, c, l.stream), "ncclSend");
+            bytes_sent += (rb + 4) * x.n;
+          }
+          if (x.dst == l.rank) {
+            nccl_check(ncclRecv((char*)l.recv_rows + rb * x.dst_off, rb * x.n, ncclUint8, x.src, c, l.stream),
+                       "ncclRecv");
+            nccl_check(ncclRecv(l.recv_scores + x.dst_off, x.n, ncclFloat32, x.src, c, l.stream), "ncclRecv");
+          }
+        }
+      }
+    }
+    for (size_t i = 0; i < local.size(); ++i) {
+      const size_t j = slot_of(local[i].rank);
+      if (!events_[j]) {
+        PGA_COMM_HIP(hipSetDevice(local[i].device));
+        PGA_COMM_HIP(hipEventCreateWithFlags(&events_[j], hipEventDisableTiming));
+      }
+      PGA_COMM_HIP(hipEventRecord(events_[j], local[i].stream));
+    }
+  }
+
+  // Poll the exchange's completion events and RCCL's asynchronous error
+  // state; on an error or after timeout_s, abort the communicators so no
+  // rank stays blocked in a transfer whose peer is gone.
+  bool wait(std::vector<LocalRank>& local, double timeout_s) override {
+    if (aborted_) return false;
+    if (timeout_s <= 0) {  // asynchronous mode: only surface errors RCCL already saw
+      for (ncclComm_t c : comms_) {
+        ncclResult_t st = ncclSuccess;
+        if (ncclCommGetAsyncError(c, &st) != ncclSuccess || (st != ncclSuccess && st != ncclInProgress))
+          return abort_all();
+      }
+      return true;
+    }
+    const auto t0 = std::chrono::steady_clock::now();
+    for (;;) {
+      bool done = true;
+      for (const LocalRank& l : local) {
+        hipEvent_t e = events_[slot_of(l.rank)];
+        if (!e) continue;
+        const hipError_t q = hipEventQuery(e);
+        if (q == hipErrorNotReady) done = false;
+        else if (q != hipSuccess) return abort_all();
+      }
+      for (ncclComm_t c : comms_) {
+        ncclResult_t st = ncclSuccess;
+        if (ncclCommGetAsyncError(c, &st) != ncclSuccess || (st != ncclSuccess && st != ncclInProgress))
+          return abort_all();
+      }
+      if (done) return true;
+      const double dt = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+      if (dt > timeout_s) return abort_all();
+      std::this_thread::sleep_for(std::chrono::microseconds(50));
+    }
+  }
+
+  std::vector<float> allgather(const std::vector<LocalRank>& local, const std::vector<float>& mine) override {
+    std::vector<float> all(n_, 0.f);
+    std::vector<float*> dbuf(local.size(), nullptr);
+    for (size_t i = 0; i < local.size(); ++i) {
+      PGA_COMM_HIP(hipSetDevice(local[i].device));
+      PGA_COMM_HIP(hipMalloc(&dbuf[i], sizeof(float) * (n_ + 1)));
+      PGA_COMM_HIP(hipMemcpyAsync(dbuf[i] + n_, &mine[i], sizeof(float), hipMemcpyHostToDevice, local[i].stream));
+    }
+    {
+      Group g;
+      for (size_t i = 0; i < local.size(); ++i)
+        nccl_check(ncclAllGather(dbuf[i] + n_, dbuf[i], 1, ncclFloat32, comm_of(local[i].rank), local[i].stream),
+                   "ncclAllGather");
+    }
+    for (size_t i = 0; i < local.size(); ++i) {
+      PGA_COMM_HIP(hipSetDevice(local[i].device));
+      PGA_COMM_HIP(hipMemcpyAsync(all.data(), dbuf[i], sizeof(float) * n_, hipMemcpyDeviceToHost, local[i].stream));
+      PGA_COMM_HIP(hipStreamSynchronize(local[i].stream));
+      PGA_COMM_HIP(hipFree(dbuf[i]));
+    }
+    return all;
+  }
+
+ private:
+  size_t slot_of(int rank) const {
+    for (size_t i = 0; i < ranks_.size(); ++i)
+      if (ranks_[i] == rank) return i;
+    throw std::runtime_error("rank " + std::to_string(rank) + " is not local to this communicator");
+  }
+  ncclComm_t comm_of(int rank) const { return comms_[slot_of(rank)]; }
+  bool abort_all() {
+    aborted_ = true;
+    return false;
+  }
+
+  std::vector<ncclComm_t> comms_;
+  std::vector<int> ranks_;
+  std::vector<hipEvent_t> events_;
+  int n_;
+  bool all_;
+  bool aborted_ = false;
+};
+
+}  // namespace
 
 int rccl_unique_id(char out[128]) {
   static_assert(sizeof(ncclUniqueId) <= 128, "unique id too large");
@@ -37,57 +177,24 @@ int rccl_unique_id(char out[128]) {
   return 0;
 }
 
-RcclComm* rccl_init(int nranks, int rank, const char id[128], int device) {
+std::shared_ptr<Comm> rccl_comm_rank(int nranks, int rank, const char id[128], int device) {
   if (nranks < 1 || rank < 0 || rank >= nranks) throw std::invalid_argument("bad rank / nranks");
   PGA_COMM_HIP(hipSetDevice(device));
-  auto* c = new RcclComm;
-  c->nranks = nranks;
-  c->rank = rank;
   ncclUniqueId uid;
   std::memcpy(&uid, id, sizeof(uid));
-  try {
-    nccl_check(ncclCommInitRank(&c->comm, nranks, uid, rank), "ncclCommInitRank");
-    PGA_COMM_HIP(hipMalloc(&c->dscratch, 64));
-  } catch (...) {
-    delete c;
-    throw;
-  }
-  return c;
+  ncclComm_t c = nullptr;
+  nccl_check(ncclCommInitRank(&c, nranks, uid, rank), "ncclCommInitRank");
+  return std::make_shared<RcclComm>(std::vector<ncclComm_t>{c}, std::vector<int>{rank}, nranks, false);
 }
 
-void rccl_destroy(RcclComm* c) {
-  if (!c) return;
-  if (c->comm) ncclCommDestroy(c->comm);
-  if (c->dscratch) (void)hipFree(c->dscratch);
-  delete c;
-}
-
-int rccl_rank(const RcclComm* c) { return c ? c->rank : 0; }
-int rccl_size(const RcclComm* c) { return c ? c->nranks : 1; }
-
-// send `bytes` to rank+1, receive the same from rank-1 (grouped, one link each way)
-void rccl_ring_exchange(RcclComm* c, const void* send, void* recv, size_t bytes, hipStream_t s) {
-  if (!c || c->nranks == 1) return;
-  const int to = (c->rank + 1) % c->nranks, from = (c->rank + c->nranks - 1) % c->nranks;
-  nccl_check(ncclGroupStart(), "ncclGroupStart");
-  nccl_check(ncclSend(send, bytes, ncclUint8, to, c->comm, s), "ncclSend");
-  nccl_check(ncclRecv(recv, bytes, ncclUint8, from, c->comm, s), "ncclRecv");
-  nccl_check(ncclGroupEnd(), "ncclGroupEnd");
-}
-
-// all-gather one float per rank (host in/out, synchronises the stream)
-void rccl_allgather_f32(RcclComm* c, float v, float* out, hipStream_t s) {
-  if (!c || c->nranks == 1) {
-    out[0] = v;
-    return;
-  }
-  float* d = nullptr;
-  PGA_COMM_HIP(hipMalloc(&d, sizeof(float) * (c->nranks + 1)));
-  PGA_COMM_HIP(hipMemcpyAsync(d + c->nranks, &v, sizeof(float), hipMemcpyHostToDevice, s));
-  nccl_check(ncclAllGather(d + c->nranks, d, 1, ncclFloat32, c->comm, s), "ncclAllGather");
-  PGA_COMM_HIP(hipMemcpyAsync(out, d, sizeof(float) * c->nranks, hipMemcpyDeviceToHost, s));
-  PGA_COMM_HIP(hipStreamSynchronize(s));
-  PGA_COMM_HIP(hipFree(d));
+std::shared_ptr<Comm> rccl_comm_all(const std::vector<int>& devices) {
+  const int n = (int)devices.size();
+  if (n < 1) throw std::invalid_argument("rccl_comm_all: no devices");
+  std::vector<ncclComm_t> comms(n, nullptr);
+  nccl_check(ncclCommInitAll(comms.data(), n, devices.data()), "ncclCommInitAll");
+  std::vector<int> ranks(n);
+  for (int i = 0; i < n; ++i) ranks[i] = i;
+  return std::make_shared<RcclComm>(std::move(comms), std::move(ranks), n, true);
 }
 
 }  // namespace pga

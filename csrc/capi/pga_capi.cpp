@@ -58,10 +58,24 @@ struct pga_solver {
   crossover_f crossover = nullptr;
   hipStream_t stream = nullptr;
   uint32_t migration_epoch = 0;
-  pga::RcclComm* comm = nullptr;
-  void* mig_send = nullptr;
-  void* mig_recv = nullptr;
-  size_t mig_bytes = 0;
+  // inter-rank island model (pga_comm_*): the communicator may be shared by
+  // several solvers of this process (InitAll / loopback groups)
+  std::shared_ptr<pga::Comm> comm;
+  std::shared_ptr<std::vector<pga_t*>> comm_members;  // solvers driven together (drives_all_ranks)
+  int comm_rank = 0;
+  int topology = pga::TOPO_RING;
+  double comm_timeout = 0.0;
+  bool validate_migrants = true;
+  bool degraded = false;
+  uint32_t comm_failures = 0;
+  uint32_t comm_epoch = 0;
+  uint64_t migrants_received = 0;
+  // migration staging (device of population 0)
+  void* mig_send_rows = nullptr;
+  void* mig_recv_rows = nullptr;
+  float* mig_send_scores = nullptr;
+  float* mig_recv_scores = nullptr;
+  uint32_t mig_cap = 0;
 };
 
 namespace {
@@ -262,18 +276,25 @@ pga_t* pga_init_device(int device) {
 
 pga_t* pga_init(void) { return pga_init_device(default_device()); }
 
+int pga_device_count(void) {
+  int n = 0;
+  return hipGetDeviceCount(&n) == hipSuccess ? n : 0;
+}
+
 void pga_deinit(pga_t* p) {
   if (!p) return;
-  for (population_t* pop : p->pops) {
-    if (p->mig_send) {
-      dev_free(*pop->isl, p->mig_send);
-      dev_free(*pop->isl, p->mig_recv);
-      p->mig_send = p->mig_recv = nullptr;
-    }
-    delete pop;
+  if (!p->pops.empty() && p->mig_cap) {
+    pga::Island& isl = *p->pops[0]->isl;
+    for (void* b : {p->mig_send_rows, p->mig_recv_rows, (void*)p->mig_send_scores, (void*)p->mig_recv_scores})
+      dev_free(isl, b);
   }
+  for (population_t* pop : p->pops) delete pop;
   p->pops.clear();
-  if (p->comm) pga::rccl_destroy(p->comm);
+  if (p->comm_members) {
+    auto& m = *p->comm_members;
+    m.erase(std::remove(m.begin(), m.end(), p), m.end());
+  }
+  p->comm.reset();
   if (p->stream) (void)hipStreamDestroy(p->stream);
   delete p;
 }
@@ -562,26 +583,92 @@ void pga_migrate(pga_t* p, float pct) {
 }
 
 namespace {
-void migrate_ranks(pga_t* p, float pct) {
-  if (!p->comm || pga::rccl_size(p->comm) == 1 || p->pops.empty()) return;
-  pga::Island& isl = *p->pops[0]->isl;
-  isl.stream = p->stream;
-  const uint32_t k = migrants(isl.config().S, isl.config().S, pct);
+void use_device(pga_t* p) {
+  if (p->device >= 0) PGA_HIP_CHECK(hipSetDevice(p->device));
+}
+
+void ensure_staging(pga_t* p, pga::Island& isl, uint32_t k) {
+  if (p->mig_cap >= k) return;
+  for (void* b : {p->mig_send_rows, p->mig_recv_rows, (void*)p->mig_send_scores, (void*)p->mig_recv_scores})
+    dev_free(isl, b);
+  p->mig_send_rows = p->mig_recv_rows = nullptr;
+  p->mig_send_scores = p->mig_recv_scores = nullptr;
+  p->mig_cap = 0;
+  p->mig_send_rows = dev_alloc(isl, isl.row_bytes() * k);
+  p->mig_recv_rows = dev_alloc(isl, isl.row_bytes() * k);
+  p->mig_send_scores = (float*)dev_alloc(isl, 4ull * k);
+  p->mig_recv_scores = (float*)dev_alloc(isl, 4ull * k);
+  p->mig_cap = k;
+}
+
+// Inter-rank migration of population 0 of every solver in `solvers` (all the
+// ranks this call drives: one per process with ncclCommInitRank, all of them
+// with InitAll / loopback).  Per rank: top-k emigrants (device radix select)
+// -> packed send buffers -> the epoch's plan over the transport ->
+// [optional host check with timeout] -> re-score the received rows with the
+// LOCAL objective (a forged score never enters) -> replace the bottom-k.
+// Everything is stream-ordered; with no timeout nothing waits on the host,
+// so the exchange overlaps whatever the GPUs run next.
+void migrate_ranks(const std::vector<pga_t*>& solvers, float pct) {
+  pga_t* p0 = solvers.front();
+  if (!p0->comm || p0->comm->size() == 1 || p0->degraded) return;
+  pga::Comm& comm = *p0->comm;
+  const uint64_t S = p0->pops[0]->isl->config().S;
+  const uint32_t k0 = migrants(S, S, pct);
+  const uint32_t k = pga::plan_migrants(p0->topology, comm.size(), k0);
   if (!k) return;
-  const size_t rows = isl.row_bytes() * k, bytes = rows + 4ull * k;
-  if (p->mig_bytes < bytes) {
-    dev_free(isl, p->mig_send);
-    dev_free(isl, p->mig_recv);
-    p->mig_send = dev_alloc(isl, bytes);
-    p->mig_recv = dev_alloc(isl, bytes);
-    p->mig_bytes = bytes;
+  if (k > S / 2) throw std::invalid_argument("migration: too many migrants for the population size");
+  const std::vector<pga::Xfer> plan = pga::migration_plan(p0->topology, comm.size(), k0, p0->seed, p0->comm_epoch);
+  std::vector<pga::LocalRank> local;
+  for (pga_t* p : solvers) {
+    use_device(p);
+    pga::Island& isl = *p->pops[0]->isl;
+    if (isl.config().S != S || isl.row_bytes() != p0->pops[0]->isl->row_bytes())
+      throw std::invalid_argument("migration: ranks need populations of the same size and genome length");
+    isl.stream = p->stream;
+    ensure_staging(p, isl, k);
+    uint32_t* idx = (uint32_t*)isl.scratch(4ull * k);
+    isl.topk(k, true, idx, false);
+    isl.gather(idx, k, p->mig_send_rows, p->mig_send_scores);
+    pga::LocalRank l;
+    l.rank = p->comm_rank;
+    l.device = p->device;
+    l.stream = p->stream;
+    l.row_bytes = isl.row_bytes();
+    l.send_rows = p->mig_send_rows;
+    l.send_scores = p->mig_send_scores;
+    l.recv_rows = p->mig_recv_rows;
+    l.recv_scores = p->mig_recv_scores;
+    local.push_back(l);
   }
-  uint32_t* idx = (uint32_t*)isl.scratch(4ull * k);
-  isl.topk(k, true, idx, false);
-  isl.gather(idx, k, p->mig_send, (float*)((char*)p->mig_send + rows));
-  pga::rccl_ring_exchange(p->comm, p->mig_send, p->mig_recv, bytes, p->stream);
-  isl.topk(k, false, idx, false);
-  isl.scatter(idx, k, p->mig_recv, (const float*)((const char*)p->mig_recv + rows));
+  bool ok = true;
+  try {
+    comm.exchange(plan, local);
+    ok = comm.wait(local, p0->comm_timeout);
+  } catch (const std::exception& e) {
+    g_last_error = e.what();
+    ok = false;
+  }
+  for (pga_t* p : solvers) ++p->comm_epoch;
+  if (!ok) {
+    // islands are loosely coupled: each keeps evolving alone (degraded mode)
+    for (pga_t* p : solvers) {
+      p->degraded = true;
+      ++p->comm_failures;
+    }
+    std::fprintf(stderr, "pga: migration over %s failed (%s); islands continue without migration\n", comm.name(),
+                 g_last_error.c_str());
+    return;
+  }
+  for (pga_t* p : solvers) {
+    use_device(p);
+    pga::Island& isl = *p->pops[0]->isl;
+    if (p->validate_migrants) isl.evaluate_rows(p->mig_recv_rows, p->mig_recv_scores, k);
+    uint32_t* idx = (uint32_t*)isl.scratch(4ull * k);
+    isl.topk(k, false, idx, false);
+    isl.scatter(idx, k, p->mig_recv_rows, p->mig_recv_scores);
+    p->migrants_received += k;
+  }
 }
 }  // namespace
 
@@ -624,32 +711,71 @@ void join_islands(pga_t* p) {
 }
 }  // namespace
 
-void pga_run_islands(pga_t* p, unsigned n, unsigned m, float pct) {
-  if (!p || p->pops.empty()) return;
-  guard(p, [&]() {
-    const bool gpu = p->device >= 0;
+namespace {
+// n generations of every population of every solver in `solvers`, migrating
+// every m generations: first between the populations of each solver
+// (pga_migrate), then between ranks (migrate_ranks).  Each solver's islands
+// run on their own streams; solvers on different GPUs run concurrently
+// because nothing here waits on the host between migration points.
+void run_islands(const std::vector<pga_t*>& solvers, unsigned n, unsigned m, float pct) {
+  for (pga_t* p : solvers) {
+    use_device(p);
     for (population_t* pop : p->pops) {
       sync_callbacks(p, pop);
       pop->isl->stream = p->stream;
       pop->isl->evaluate();
     }
-    unsigned g = 0;
-    while (g < n) {
-      // generations until the next migration point (or the end)
-      unsigned step = n - g;
-      if (m > 0) {
-        const unsigned next = (g / m + 1) * m;
-        if (next < n) step = next - g;
-      }
+  }
+  unsigned g = 0;
+  while (g < n) {
+    // generations until the next migration point (or the end)
+    unsigned step = n - g;
+    if (m > 0) {
+      const unsigned next = (g / m + 1) * m;
+      if (next < n) step = next - g;
+    }
+    for (pga_t* p : solvers) {
+      use_device(p);
+      const bool gpu = p->device >= 0;
       if (gpu) fork_islands(p);
       for (population_t* pop : p->pops) pop->isl->run(step);
       if (gpu) join_islands(p);
-      g += step;
-      if (m > 0 && g % m == 0 && g < n) {
-        pga_migrate(p, pct);
-        migrate_ranks(p, pct);
-      }
     }
+    g += step;
+    if (m > 0 && g % m == 0 && g < n) {
+      for (pga_t* p : solvers) {
+        use_device(p);
+        pga_migrate(p, pct);
+      }
+      migrate_ranks(solvers, pct);
+    }
+  }
+}
+}  // namespace
+
+void pga_run_islands(pga_t* p, unsigned n, unsigned m, float pct) {
+  if (!p || p->pops.empty()) return;
+  guard(p, [&]() {
+    if (p->comm && p->comm->drives_all_ranks() && p->comm->size() > 1)
+      throw std::invalid_argument("this communicator drives all ranks from one process: use pga_run_islands_multi");
+    run_islands({p}, n, m, pct);
+  });
+}
+
+int pga_run_islands_multi(pga_t** solvers, int count, unsigned n, unsigned m, float pct) {
+  if (!solvers || count < 1) return -1;
+  pga_t* p0 = solvers[0];
+  return guard_r<int>(p0, -1, [&]() {
+    std::vector<pga_t*> v(solvers, solvers + count);
+    for (pga_t* p : v) {
+      if (!p || p->pops.empty()) throw std::invalid_argument("pga_run_islands_multi: solver without populations");
+      if (p->comm != p0->comm) throw std::invalid_argument("pga_run_islands_multi: solvers of different communicators");
+    }
+    if (p0->comm && p0->comm->size() > 1 && (!p0->comm->drives_all_ranks() || count != p0->comm->size()))
+      throw std::invalid_argument("pga_run_islands_multi: pass every rank of an InitAll / loopback group");
+    std::sort(v.begin(), v.end(), [](pga_t* a, pga_t* b) { return a->comm_rank < b->comm_rank; });
+    run_islands(v, n, m, pct);
+    return 0;
   });
 }
 
@@ -738,27 +864,112 @@ int pga_comm_unique_id(char id[128]) {
 }
 
 int pga_comm_init(pga_t* p, int nranks, int rank, const char id[128]) {
-  if (!p || p->device < 0) return -1;
+  if (!p || p->device < 0 || !id) return -1;
   return guard_r<int>(p, -1, [&]() {
-    p->comm = pga::rccl_init(nranks, rank, id, p->device);
+    p->comm = pga::rccl_comm_rank(nranks, rank, id, p->device);
+    p->comm_rank = rank;
+    p->comm_members.reset();
     return 0;
   });
 }
 
-int pga_comm_rank(const pga_t* p) { return p ? pga::rccl_rank(p->comm) : 0; }
-int pga_comm_size(const pga_t* p) { return p ? pga::rccl_size(p->comm) : 1; }
+namespace {
+int init_group(pga_t** solvers, int n, bool loopback) {
+  if (!solvers || n < 1) return -1;
+  for (int i = 0; i < n; ++i)
+    if (!solvers[i]) return -1;
+  return guard_r<int>(solvers[0], -1, [&]() {
+    std::shared_ptr<pga::Comm> c;
+    if (loopback) {
+      c = pga::loopback_comm(n);
+    } else {
+      std::vector<int> devs(n);
+      for (int i = 0; i < n; ++i) {
+        if (solvers[i]->device < 0) throw std::invalid_argument("pga_comm_init_local needs GPU solvers");
+        devs[i] = solvers[i]->device;
+      }
+      c = pga::rccl_comm_all(devs);
+    }
+    auto members = std::make_shared<std::vector<pga_t*>>(solvers, solvers + n);
+    for (int i = 0; i < n; ++i) {
+      solvers[i]->comm = c;
+      solvers[i]->comm_rank = i;
+      solvers[i]->comm_members = members;
+      solvers[i]->topology = solvers[0]->topology;
+      solvers[i]->seed = solvers[0]->seed;  // identical random-ring draws on every rank
+    }
+    return 0;
+  });
+}
+}  // namespace
+
+int pga_comm_init_local(pga_t** solvers, int n) { return init_group(solvers, n, false); }
+int pga_comm_init_loopback(pga_t** solvers, int n) { return init_group(solvers, n, true); }
+
+int pga_comm_rank(const pga_t* p) { return p && p->comm ? p->comm_rank : 0; }
+int pga_comm_size(const pga_t* p) { return p && p->comm ? p->comm->size() : 1; }
+
+int pga_comm_set_topology(pga_t* p, enum pga_topology t) {
+  if (!p || (t != PGA_TOPO_RING && t != PGA_TOPO_RANDOM && t != PGA_TOPO_ALL_TO_ALL)) return -1;
+  if (p->comm_members)
+    for (pga_t* q : *p->comm_members) q->topology = (int)t;
+  p->topology = (int)t;
+  return 0;
+}
+
+int pga_comm_set_timeout(pga_t* p, double seconds) {
+  if (!p || seconds < 0) return -1;
+  p->comm_timeout = seconds;
+  return 0;
+}
+
+int pga_comm_set_validation(pga_t* p, int on) {
+  if (!p) return -1;
+  p->validate_migrants = on != 0;
+  return 0;
+}
+
+int pga_comm_degraded(const pga_t* p) { return p && p->degraded ? 1 : 0; }
+
+int pga_comm_info(const pga_t* p, struct pga_comm_stats* out) {
+  if (!p || !out) return -1;
+  out->epochs = p->comm_epoch;
+  out->failures = p->comm_failures;
+  out->degraded = p->degraded ? 1 : 0;
+  out->migrants_received = p->migrants_received;
+  out->bytes_sent = p->comm ? p->comm->bytes_sent : 0;
+  return 0;
+}
+
+int pga_comm_set_fault(pga_t* p, int every, int mode) {
+  if (!p || !p->comm) return -1;
+  return guard_r<int>(p, -1, [&]() {
+    pga::loopback_set_fault(p->comm.get(), every, mode);
+    return 0;
+  });
+}
 
 int pga_comm_best(pga_t* p, float* score, int* rank) {
   if (!p || p->pops.empty()) return -1;
   return guard_r<int>(p, -1, [&]() {
-    pga::Island& isl = *p->pops[0]->isl;
-    isl.stream = p->stream;
-    const float mine = isl.best_score();
-    const int n = pga::rccl_size(p->comm);
-    std::vector<float> all(n);
-    pga::rccl_allgather_f32(p->comm, mine, all.data(), p->stream);
+    std::vector<pga_t*> solvers{p};
+    if (p->comm && p->comm->drives_all_ranks() && p->comm_members) solvers = *p->comm_members;
+    std::vector<pga::LocalRank> local;
+    std::vector<float> mine;
+    for (pga_t* q : solvers) {
+      use_device(q);
+      pga::Island& isl = *q->pops[0]->isl;
+      isl.stream = q->stream;
+      mine.push_back(isl.best_score());
+      pga::LocalRank l;
+      l.rank = q->comm_rank;
+      l.device = q->device;
+      l.stream = q->stream;
+      local.push_back(l);
+    }
+    std::vector<float> all = p->comm ? p->comm->allgather(local, mine) : mine;
     int br = 0;
-    for (int i = 1; i < n; ++i)
+    for (int i = 1; i < (int)all.size(); ++i)
       if (all[i] > all[br]) br = i;
     if (score) *score = all[br];
     if (rank) *rank = br;

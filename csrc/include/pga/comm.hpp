@@ -1,10 +1,32 @@
-// comm.hpp — inter-rank communication used by the C API island model.
+// comm.hpp — inter-island communication of the C API island model.
+//
+// The reference claims "CUDA GPUs+MPI" (README.md:4) but ships no
+// communication code; its migration entry points are empty
+// (src/pga.cu:368-374, :393-395).  Here migration is a
+// list of row transfers (a *plan*) executed by one of three transports:
+//
+//   RCCL, one process per GPU     ncclCommInitRank; every process posts the
+//                                 transfers of its own rank (grouped
+//                                 ncclSend/ncclRecv over xGMI)
+//   RCCL, one process, n GPUs     ncclCommInitAll; the driver posts the
+//                                 transfers of all ranks in ONE group
+//   loopback                      in-process ranks (CPU or GPU islands),
+//                                 plain copies; the test transport, with
+//                                 fault injection (drop / corrupt)
+//
+// Plans are computed identically on every rank from (topology, epoch, seed),
+// so no rank ever has to tell another whom it talks to.  Transfers are
+// stream-ordered and asynchronous; Comm::wait() is the optional host-side
+// completion check with a timeout (RCCL: event polling +
+// ncclCommGetAsyncError, ncclCommAbort on expiry).
 #pragma once
 
 #include <hip/hip_runtime.h>
 
+#include <memory>
 #include <stdexcept>
 #include <string>
+#include <vector>
 
 #define PGA_COMM_HIP(expr)                                                                     \
   do {                                                                                         \
@@ -14,13 +36,62 @@
 
 namespace pga {
 
-struct RcclComm;
+enum Topology : int32_t {
+  TOPO_RING = 0,        // rank r -> r+1
+  TOPO_RANDOM = 1,      // a fresh random ring per epoch (shared Philox draw)
+  TOPO_ALL_TO_ALL = 2,  // every rank sends k/(n-1) emigrants to every other rank
+};
+
+// rows [src_off, src_off+n) of src's send buffer -> rows [dst_off, ...) of dst's receive buffer
+struct Xfer {
+  int src, dst;
+  uint32_t src_off, dst_off, n;
+};
+
+// migrants per rank actually exchanged for k requested (all-to-all rounds to a multiple of n-1)
+uint32_t plan_migrants(int topology, int nranks, uint32_t k);
+std::vector<Xfer> migration_plan(int topology, int nranks, uint32_t k, uint64_t seed, uint32_t epoch);
+
+// one rank's staging buffers (device memory for GPU islands, host for CPU ones)
+struct LocalRank {
+  int rank = 0;
+  int device = -1;
+  hipStream_t stream = nullptr;
+  size_t row_bytes = 0;
+  void* send_rows = nullptr;
+  float* send_scores = nullptr;
+  void* recv_rows = nullptr;
+  float* recv_scores = nullptr;
+};
+
+class Comm {
+ public:
+  virtual ~Comm() = default;
+  virtual int size() const = 0;
+  virtual const char* name() const = 0;
+  // true when the caller drives every rank (InitAll / loopback)
+  virtual bool drives_all_ranks() const = 0;
+  // enqueue the plan's transfers that touch `local`
+  virtual void exchange(const std::vector<Xfer>& plan, std::vector<LocalRank>& local) = 0;
+  // host-side completion check of the last exchange; false: failed or timed
+  // out (the communicator is then unusable and the islands run on alone)
+  virtual bool wait(std::vector<LocalRank>& local, double timeout_s) = 0;
+  // one float per rank; `local[i]` contributes mine[i]; returns all ranks' values
+  virtual std::vector<float> allgather(const std::vector<LocalRank>& local, const std::vector<float>& mine) = 0;
+  uint64_t bytes_sent = 0;
+};
+
+// ---- RCCL ----
 int rccl_unique_id(char out[128]);
-RcclComm* rccl_init(int nranks, int rank, const char id[128], int device);
-void rccl_destroy(RcclComm* c);
-int rccl_rank(const RcclComm* c);
-int rccl_size(const RcclComm* c);
-void rccl_ring_exchange(RcclComm* c, const void* send, void* recv, size_t bytes, hipStream_t s);
-void rccl_allgather_f32(RcclComm* c, float v, float* out, hipStream_t s);
+std::shared_ptr<Comm> rccl_comm_rank(int nranks, int rank, const char id[128], int device);
+std::shared_ptr<Comm> rccl_comm_all(const std::vector<int>& devices);
+
+// ---- loopback ----
+// fault injection: every `every`-th exchange (1-based count) is dropped
+// (mode 1: nothing arrives and wait() reports the failure) or corrupted
+// (mode 2: the received scores are overwritten with +3e38, which re-scoring
+// must undo)
+std::shared_ptr<Comm> loopback_comm(int nranks);
+void loopback_set_fault(Comm* c, int every, int mode);
 
 }  // namespace pga

@@ -35,6 +35,7 @@ enum pga_objective {
 
 /* ---- solver options (call before creating populations) ---- */
 pga_t *pga_init_device(int device);            /* device < 0: CPU reference backend */
+int pga_device_count(void);                      /* visible GPUs (0 without a GPU) */
 void pga_set_seed(pga_t *p, uint64_t seed);      /* default: PGA_SEED env or time(NULL) */
 void pga_set_quiet(pga_t *p, int quiet);         /* 1: pga_get_best does not print */
 /* 1 (default, reference behaviour): print the error and exit; 0: record it and return */
@@ -76,16 +77,51 @@ int pga_synchronize(pga_t *p);
 int pga_save(pga_t *p, population_t *pop, const char *path);
 int pga_load(pga_t *p, population_t *pop, const char *path);
 
-/* ---- multi-GPU island model over RCCL (one process per GPU) ----
- * Rank 0 creates an id (128 bytes) and shares it (file, env, MPI, ...);
- * every rank calls pga_comm_init.  pga_run_islands then also migrates
- * population 0 of each rank around a ring of ranks. */
+/* ---- inter-rank island model ----
+ * Population 0 of every rank takes part; every m generations of
+ * pga_run_islands each rank exports its top pct% and replaces its worst
+ * pct% with what it receives (after re-scoring it with its own objective).
+ *
+ * Transports:
+ *  - RCCL, one process per GPU: rank 0 creates an id (128 bytes) with
+ *    pga_comm_unique_id and shares it (file, env, MPI, ...); every rank calls
+ *    pga_comm_init and then pga_run_islands.
+ *  - RCCL, one process driving n GPUs: pga_comm_init_local(solvers, n) over
+ *    solvers created with pga_init_device(0..n-1), then
+ *    pga_run_islands_multi(solvers, n, ...).
+ *  - loopback: pga_comm_init_loopback(solvers, n), in-process copies between
+ *    any solvers (CPU or GPU): tests, and fault injection. */
+enum pga_topology {
+  PGA_TOPO_RING = 0,       /* rank r -> r+1 (one xGMI link per direction) */
+  PGA_TOPO_RANDOM = 1,     /* a fresh random ring per epoch, from the shared seed */
+  PGA_TOPO_ALL_TO_ALL = 2  /* k/(n-1) emigrants to every other rank (all links) */
+};
+struct pga_comm_stats {
+  uint64_t epochs, failures, migrants_received, bytes_sent;
+  int degraded;
+};
 int pga_comm_unique_id(char id[128]);
 int pga_comm_init(pga_t *p, int nranks, int rank, const char id[128]);
+int pga_comm_init_local(pga_t **solvers, int n);
+int pga_comm_init_loopback(pga_t **solvers, int n);
 int pga_comm_rank(const pga_t *p);
 int pga_comm_size(const pga_t *p);
+int pga_comm_set_topology(pga_t *p, enum pga_topology t); /* applies to the whole local group */
+/* > 0: after each exchange wait at most `seconds` on the host (RCCL: event
+ * polling + async error check); a failed or late exchange aborts the
+ * communicator and the islands continue alone (degraded).  0 (default):
+ * fully asynchronous, errors are only checked. */
+int pga_comm_set_timeout(pga_t *p, double seconds);
+int pga_comm_set_validation(pga_t *p, int on);             /* re-score received migrants (default 1) */
+int pga_comm_degraded(const pga_t *p);
+int pga_comm_info(const pga_t *p, struct pga_comm_stats *out);
+/* loopback only (tests): every `every`-th exchange is dropped (mode 1) or
+ * arrives with forged scores (mode 2) */
+int pga_comm_set_fault(pga_t *p, int every, int mode);
 /* global best over ranks (score, owning rank) */
 int pga_comm_best(pga_t *p, float *score, int *rank);
+/* pga_run_islands over every rank of an InitAll / loopback group at once */
+int pga_run_islands_multi(pga_t **solvers, int n, unsigned generations, unsigned m, float pct);
 
 #ifdef __cplusplus
 }

@@ -1,0 +1,245 @@
+"""Inter-rank island model of the C API (pga_comm_*, csrc/capi/comm*.cpp).
+
+CPU tests drive several solvers of the CPU reference backend through the
+loopback transport (the same migration plans and protocol as RCCL: ring,
+random ring, all-to-all; re-scoring of received migrants; fault injection
+and degraded mode).  GPU tests run the loopback between GPU solvers and the
+one-process RCCL transport (ncclCommInitAll) on the box's device.
+
+Reference: the migration entry points are empty stubs
+(src/pga.cu:368-374, :393-395) and the README's "GPUs+MPI" has no code
+(README.md:4); there is no reference output to pin these against, so the
+checks are semantic (parity unpinned)."""
+import ctypes as C
+import os
+
+import pytest
+import torch  # noqa: F401  (loads the HIP runtime the library links against)
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB = os.path.join(ROOT, "build", "libpga.so")
+PGA_BINARY = 0
+OBJ_ONEMAX = 1
+RING, RANDOM, A2A = 0, 1, 2
+
+
+class Stats(C.Structure):
+    _fields_ = [("epochs", C.c_uint64), ("failures", C.c_uint64), ("migrants_received", C.c_uint64),
+                ("bytes_sent", C.c_uint64), ("degraded", C.c_int)]
+
+
+@pytest.fixture(scope="module")
+def lib():
+    if not os.path.exists(LIB):
+        pytest.skip("build/libpga.so not built (python tools/build.py)")
+    L = C.CDLL(LIB)
+    vp = C.c_void_p
+    L.pga_init_device.restype = vp
+    L.pga_init_device.argtypes = [C.c_int]
+    L.pga_deinit.argtypes = [vp]
+    L.pga_set_seed.argtypes = [vp, C.c_uint64]
+    L.pga_set_quiet.argtypes = [vp, C.c_int]
+    L.pga_set_abort_on_error.argtypes = [vp, C.c_int]
+    L.pga_last_error.restype = C.c_char_p
+    L.pga_create_population_ext.restype = vp
+    L.pga_create_population_ext.argtypes = [vp, C.c_ulong, C.c_uint, C.c_int]
+    L.pga_set_objective_builtin.argtypes = [vp, vp, C.c_int, C.POINTER(C.c_float), C.c_size_t,
+                                            C.POINTER(C.c_float), C.c_size_t, C.c_int, C.c_float, C.c_float]
+    L.pga_set_operators.argtypes = [vp, vp, C.c_int, C.c_uint, C.c_int, C.c_float, C.c_int, C.c_float, C.c_float,
+                                    C.c_uint]
+    L.pga_run.argtypes = [vp, C.c_uint]
+    L.pga_run_islands.argtypes = [vp, C.c_uint, C.c_uint, C.c_float]
+    L.pga_best_score.restype = C.c_float
+    L.pga_best_score.argtypes = [vp, vp]
+    L.pga_get_scores.argtypes = [vp, vp, C.POINTER(C.c_float)]
+    L.pga_comm_init_loopback.argtypes = [C.POINTER(vp), C.c_int]
+    L.pga_comm_init_local.argtypes = [C.POINTER(vp), C.c_int]
+    L.pga_run_islands_multi.argtypes = [C.POINTER(vp), C.c_int, C.c_uint, C.c_uint, C.c_float]
+    L.pga_comm_set_topology.argtypes = [vp, C.c_int]
+    L.pga_comm_set_timeout.argtypes = [vp, C.c_double]
+    L.pga_comm_set_validation.argtypes = [vp, C.c_int]
+    L.pga_comm_set_fault.argtypes = [vp, C.c_int, C.c_int]
+    L.pga_comm_degraded.argtypes = [vp]
+    L.pga_comm_info.argtypes = [vp, C.POINTER(Stats)]
+    L.pga_comm_best.argtypes = [vp, C.POINTER(C.c_float), C.POINTER(C.c_int)]
+    L.pga_comm_rank.argtypes = [vp]
+    L.pga_comm_size.argtypes = [vp]
+    return L
+
+
+S, LEN = 256, 64
+
+
+def make_group(lib, n, device=-1, seed=100):
+    """n solvers, one OneMax population each (elitism 1), seeds differ per rank."""
+    solvers, pops = [], []
+    for r in range(n):
+        p = lib.pga_init_device(device)
+        assert p
+        lib.pga_set_seed(p, seed + r)
+        lib.pga_set_quiet(p, 1)
+        lib.pga_set_abort_on_error(p, 0)
+        pop = lib.pga_create_population_ext(p, S, LEN, PGA_BINARY)
+        assert lib.pga_set_objective_builtin(p, pop, OBJ_ONEMAX, None, 0, None, 0, 0, 0.0, 0.0) == 0
+        assert lib.pga_set_operators(p, pop, 0, 2, 0, 1.0, 0, -1.0, 0.0, 1) == 0
+        solvers.append(p)
+        pops.append(pop)
+    arr = (C.c_void_p * n)(*solvers)
+    return solvers, pops, arr
+
+
+def info(lib, p):
+    st = Stats()
+    assert lib.pga_comm_info(p, C.byref(st)) == 0
+    return st
+
+
+def test_ring_delivers_the_best(lib):
+    solvers, pops, arr = make_group(lib, 3)
+    assert lib.pga_comm_init_loopback(arr, 3) == 0
+    assert [lib.pga_comm_rank(p) for p in solvers] == [0, 1, 2]
+    assert lib.pga_comm_size(solvers[0]) == 3
+    lib.pga_run(solvers[1], 60)  # rank 1 far ahead of the others
+    b1 = lib.pga_best_score(solvers[1], pops[1])
+    assert b1 > lib.pga_best_score(solvers[2], pops[2])
+    # 2 generations, one migration at generation 1: ring 1 -> 2 carries rank 1's best
+    assert lib.pga_run_islands_multi(arr, 3, 2, 1, 0.05) == 0, lib.pga_last_error()
+    assert lib.pga_best_score(solvers[2], pops[2]) >= b1
+    for p in solvers:
+        st = info(lib, p)
+        assert st.epochs == 1 and st.failures == 0 and not st.degraded
+        assert st.migrants_received == round(0.05 * S)
+    assert info(lib, solvers[0]).bytes_sent == 3 * round(0.05 * S) * (16 + 4)  # 64-bit rows pad to 16 B
+    score, rank = C.c_float(), C.c_int()
+    assert lib.pga_comm_best(solvers[0], C.byref(score), C.byref(rank)) == 0
+    assert score.value == max(lib.pga_best_score(p, q) for p, q in zip(solvers, pops))
+    for p in solvers:
+        lib.pga_deinit(p)
+
+
+def test_all_to_all_and_random_ring(lib):
+    for topo in (A2A, RANDOM):
+        solvers, pops, arr = make_group(lib, 4, seed=7)
+        assert lib.pga_comm_init_loopback(arr, 4) == 0
+        assert lib.pga_comm_set_topology(solvers[0], topo) == 0  # applies to the group
+        assert lib.pga_run_islands_multi(arr, 4, 31, 10, 0.05) == 0, lib.pga_last_error()
+        k = round(0.05 * S)
+        want = (k // 3) * 3 if topo == A2A else k
+        for p in solvers:
+            st = info(lib, p)
+            assert st.epochs == 3 and st.migrants_received == 3 * want and not st.degraded
+        # elitism + migration never lose the global best
+        assert max(lib.pga_best_score(p, q) for p, q in zip(solvers, pops)) >= 50
+        for p in solvers:
+            lib.pga_deinit(p)
+
+
+def test_random_ring_is_reproducible(lib):
+    finals = []
+    for _ in range(2):
+        solvers, pops, arr = make_group(lib, 3, seed=21)
+        lib.pga_comm_init_loopback(arr, 3)
+        lib.pga_comm_set_topology(solvers[0], RANDOM)
+        lib.pga_run_islands_multi(arr, 3, 20, 4, 0.1)
+        sc = []
+        for p, q in zip(solvers, pops):
+            buf = (C.c_float * S)()
+            lib.pga_get_scores(p, q, buf)
+            sc.append(list(buf))
+            lib.pga_deinit(p)
+        finals.append(sc)
+    assert finals[0] == finals[1]
+
+
+def test_dropped_exchange_degrades(lib):
+    solvers, pops, arr = make_group(lib, 2)
+    lib.pga_comm_init_loopback(arr, 2)
+    assert lib.pga_comm_set_fault(solvers[0], 2, 1) == 0  # the 2nd exchange is lost
+    assert lib.pga_run_islands_multi(arr, 2, 40, 5, 0.05) == 0
+    for p in solvers:
+        st = info(lib, p)
+        assert st.degraded == 1 and st.failures == 1
+        assert st.epochs == 2 and st.migrants_received == round(0.05 * S)
+        assert lib.pga_comm_degraded(p) == 1
+    # the islands kept evolving alone
+    assert all(lib.pga_best_score(p, q) >= 50 for p, q in zip(solvers, pops))
+    for p in solvers:
+        lib.pga_deinit(p)
+
+
+@pytest.mark.parametrize("validate", [1, 0])
+def test_forged_scores_are_rescored(lib, validate):
+    solvers, pops, arr = make_group(lib, 2)
+    lib.pga_comm_init_loopback(arr, 2)
+    lib.pga_comm_set_fault(solvers[0], 1, 2)  # every exchange arrives with scores 3e38
+    for p in solvers:
+        lib.pga_comm_set_validation(p, validate)
+    lib.pga_run_islands_multi(arr, 2, 3, 1, 0.05)
+    best = max(lib.pga_best_score(p, q) for p, q in zip(solvers, pops))
+    if validate:
+        assert best <= LEN  # a forged fitness never enters
+    else:
+        assert best > 1e37  # without re-scoring it would
+    for p in solvers:
+        lib.pga_deinit(p)
+
+
+def test_group_needs_the_multi_driver(lib):
+    solvers, pops, arr = make_group(lib, 2)
+    lib.pga_comm_init_loopback(arr, 2)
+    lib.pga_run_islands(solvers[0], 5, 2, 0.05)
+    assert b"pga_run_islands_multi" in lib.pga_last_error()
+    sub = (C.c_void_p * 1)(solvers[0])
+    assert lib.pga_run_islands_multi(sub, 1, 5, 2, 0.05) == -1  # every rank must be passed
+    for p in solvers:
+        lib.pga_deinit(p)
+
+
+def test_single_rank_without_comm_is_plain_islands(lib):
+    solvers, pops, arr = make_group(lib, 1)
+    assert lib.pga_run_islands_multi(arr, 1, 10, 3, 0.05) == 0
+    assert info(lib, solvers[0]).epochs == 0
+    lib.pga_deinit(solvers[0])
+
+
+@pytest.mark.gpu
+def test_gpu_loopback_matches_cpu(lib):
+    """The same loopback ring on GPU solvers reproduces the CPU backend's run
+    bit for bit (BINARY generations are bit-exact CPU/GPU)."""
+    out = []
+    for dev in (-1, 0):
+        solvers, pops, arr = make_group(lib, 2, device=dev, seed=3)
+        assert lib.pga_comm_init_loopback(arr, 2) == 0
+        assert lib.pga_run_islands_multi(arr, 2, 12, 4, 0.05) == 0, lib.pga_last_error()
+        sc = []
+        for p, q in zip(solvers, pops):
+            buf = (C.c_float * S)()
+            lib.pga_get_scores(p, q, buf)
+            sc.append(sorted(buf))
+            lib.pga_deinit(p)
+        out.append(sc)
+    assert out[0] == out[1]
+
+
+@pytest.mark.gpu
+def test_gpu_rccl_init_all_single_rank(lib):
+    """ncclCommInitAll over the box's one GPU: the RCCL transport initialises,
+    the group driver runs, and the global best query goes through
+    ncclAllGather (one rank: no exchange)."""
+    solvers, pops, arr = make_group(lib, 1, device=0)
+    assert lib.pga_comm_init_local(arr, 1) == 0, lib.pga_last_error()
+    lib.pga_comm_set_timeout(solvers[0], 30.0)
+    assert lib.pga_run_islands_multi(arr, 1, 20, 5, 0.05) == 0, lib.pga_last_error()
+    score, rank = C.c_float(), C.c_int()
+    assert lib.pga_comm_best(solvers[0], C.byref(score), C.byref(rank)) == 0
+    assert rank.value == 0 and score.value == lib.pga_best_score(solvers[0], pops[0])
+    lib.pga_deinit(solvers[0])
+
+
+@pytest.mark.gpu
+def test_example_islands_multi_gpu():
+    import subprocess
+    exe = os.path.join(ROOT, "build", "examples", "islands_multi_gpu")
+    r = subprocess.run([exe, "65536", "30", "all_to_all"], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "GPU islands" in r.stdout

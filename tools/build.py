@@ -30,7 +30,7 @@ ARCH = os.environ.get("PGA_ARCH", "gfx950")
 KERNELS = ["csrc/kernels/binary.hip", "csrc/kernels/real.hip", "csrc/kernels/perm.hip",
            "csrc/kernels/util.hip", "csrc/kernels/compat.hip"]
 HOST = ["csrc/engine/island.cpp", "csrc/engine/trace.cpp", "csrc/engine/jit.cpp", "csrc/cpu/cpu_ops.cpp", "csrc/cpu/cpu_real.cpp", "csrc/cpu/cpu_perm.cpp"]
-CAPI = ["csrc/capi/pga_capi.cpp", "csrc/capi/comm_rccl.cpp"]
+CAPI = ["csrc/capi/pga_capi.cpp", "csrc/capi/comm.cpp", "csrc/capi/comm_rccl.cpp"]
 COMPAT = []
 BINDINGS = ["csrc/python/bindings.cpp"]
 
@@ -144,7 +144,7 @@ def write_ninja(opt: str, with_torch: bool) -> str:
         lines.append(f"  extra = -fgpu-rdc --hip-link")
         lines.append("  ldflags = -lpthread -L/opt/rocm/lib -lrccl")
         ex.append(exe)
-    for name in ("onemax_bits",):
+    for name in ("onemax_bits", "islands_multi_gpu"):
         src = f"examples/{name}.c"
         if not os.path.exists(os.path.join(ROOT, src)):
             continue
