@@ -408,6 +408,16 @@ int pga_set_blend_alpha(pga_t* p, population_t* pop, float alpha) {
   });
 }
 
+int pga_set_rank_pressure(pga_t* p, population_t* pop, float sp) {
+  if (!valid_pop(p, pop) || !(sp >= 1.f && sp <= 2.f)) return -1;
+  return guard_r<int>(p, -1, [&]() {
+    pga::Config c = pop->isl->config();
+    c.rank_pressure = sp;
+    pop->isl->set_operators(c);
+    return 0;
+  });
+}
+
 // -------------------------------------------------------------------- stages
 void pga_evaluate(pga_t* p, population_t* pop) {
   if (!valid_pop(p, pop)) return;

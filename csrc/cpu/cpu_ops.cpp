@@ -54,6 +54,10 @@ void select_parents(const GenArgs& a, uint64_t child, uint32_t& pa, uint32_t& pb
   } else if (a.selection == SEL_ROULETTE) {
     pa = roulette_pick(a.cumfit, S, pool_word(a.key, child, W_SEL + 0));
     pb = roulette_pick(a.cumfit, S, pool_word(a.key, child, W_SEL + 1));
+  } else if (a.selection == SEL_RANK) {
+    auto w = [&](uint32_t t) { return pool_word(a.key, child, W_SEL + t); };
+    pa = a.rank_order[rank_pick(w(0), w(1), w(2), S, a.rank_thresh)];
+    pb = a.rank_order[rank_pick(w(3), w(4), w(5), S, a.rank_thresh)];
   } else {
     pa = word_to_index(pool_word(a.key, child, W_SEL + 0), S);
     pb = word_to_index(pool_word(a.key, child, W_SEL + 1), S);
@@ -255,6 +259,17 @@ void roulette_prefix(const float* s, uint64_t S, float* cumfit) {
     acc += std::fmax(s[i] - st[0], 0.f);
     cumfit[i] = acc;
   }
+}
+
+// ascending (score_key, index): the order a stable LSD radix sort of the
+// keys produces on the GPU (util.hip rank_order_launch)
+void rank_order(const float* s, uint64_t S, uint32_t* order) {
+  std::vector<uint32_t> key(S);
+  for (uint64_t i = 0; i < S; ++i) {
+    key[i] = score_key(s[i]);
+    order[i] = (uint32_t)i;
+  }
+  std::stable_sort(order, order + S, [&](uint32_t x, uint32_t y) { return key[x] < key[y]; });
 }
 
 void topk(const float* scores, uint64_t S, uint32_t k, bool largest, uint32_t* idx_out, bool sorted) {

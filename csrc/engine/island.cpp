@@ -66,7 +66,7 @@ Island::Island(const Config& cfg, int device) : cfg_(cfg), device_(device) {
 Island::~Island() {
   Buffer* all[] = {&rows_[0],   &rows_[1],     &scores_[0],   &scores_[1],  &best_[0],  &best_[1],   &mut_thr_,
                    &obj_data_[0], &obj_data_[1], &keys_[0], &keys_[1], &elite_idx_, &cumfit_, &cum_ws_, &topk_ws_, &stats_,
-                   &out_best_,  &scratch_, &compat_rand_, &ev_parts_, &gen_dev_};
+                   &out_best_,  &scratch_, &compat_rand_, &ev_parts_, &gen_dev_, &rank_order_, &rank_ws_};
   drop_graph();
   if (cap_stream_) (void)hipStreamDestroy(cap_stream_);
   for (Buffer* b : all) {
@@ -148,6 +148,9 @@ void Island::set_operators(const Config& c) {
   if (c.selection == SEL_TOURNAMENT && (c.tour_k < 1 || c.tour_k > 64))
     throw std::invalid_argument("tournament size must be in [1, 64]");
   if (c.n_elite > c.S) throw std::invalid_argument("elitism count exceeds population");
+  if (c.selection < SEL_TOURNAMENT || c.selection > SEL_RANK) throw std::invalid_argument("unknown selection");
+  if (c.selection == SEL_RANK && !(c.rank_pressure >= 1.f && c.rank_pressure <= 2.f))
+    throw std::invalid_argument("rank pressure must be in [1, 2]");
   const float old_rate = cfg_.mut_rate;
   const int32_t old_mut = cfg_.mutation;
   cfg_ = c;
@@ -159,6 +162,10 @@ void Island::set_operators(const Config& c) {
   if (cfg_.selection == SEL_ROULETTE && !cumfit_.ptr) {
     cumfit_ = alloc(4ull * cfg_.S);
     cum_ws_ = alloc(4ull * (4 + 3 * 1024 + 1024));
+  }
+  if (cfg_.selection == SEL_RANK && !rank_order_.ptr) {
+    rank_order_ = alloc(4ull * cfg_.S);
+    if (on_gpu()) rank_ws_ = alloc(rank_order_workspace_bytes(cfg_.S));
   }
 }
 
@@ -209,6 +216,8 @@ GenArgs Island::make_args(int mode) {
   a.selection = cfg_.selection;
   a.tour_k = cfg_.tour_k;
   a.cumfit = (const float*)cumfit_.ptr;
+  a.rank_order = (const uint32_t*)rank_order_.ptr;
+  a.rank_thresh = rank_thresh_of(cfg_.rank_pressure);
   a.crossover = cfg_.crossover;
   a.xo_always = cfg_.xo_prob >= 1.f ? 1u : 0u;
   a.xo_thresh_hi = prob_thresh(cfg_.xo_prob);
@@ -287,6 +296,11 @@ void Island::prepare_generation() {
     const float* sc = (const float*)scores_[cur_].ptr;
     if (on_gpu()) roulette_prefix_launch(sc, cfg_.S, (float*)cumfit_.ptr, (float*)cum_ws_.ptr, stream);
     else cpu::roulette_prefix(sc, cfg_.S, (float*)cumfit_.ptr);
+  }
+  if (cfg_.selection == SEL_RANK) {
+    const float* sc = (const float*)scores_[cur_].ptr;
+    if (on_gpu()) rank_order_launch(sc, cfg_.S, (uint32_t*)rank_order_.ptr, rank_ws_.ptr, stream);
+    else cpu::rank_order(sc, cfg_.S, (uint32_t*)rank_order_.ptr);
   }
   if (cfg_.n_elite > 1) topk(cfg_.n_elite, true, (uint32_t*)elite_idx_.ptr, /*sorted=*/false);
 }

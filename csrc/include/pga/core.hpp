@@ -43,6 +43,7 @@ enum Selection : int32_t {
   SEL_TOURNAMENT = 0,  // k-way tournament, with replacement, first max wins
   SEL_ROULETTE = 1,    // fitness proportional (scores shifted by the minimum)
   SEL_RANDOM = 2,      // uniform parent choice (no pressure) — testing/baseline
+  SEL_RANK = 3,        // linear ranking, pressure sp in [1, 2] (Config::rank_pressure)
 };
 
 enum Crossover : int32_t {
@@ -238,6 +239,8 @@ struct GenArgs {
   int32_t selection;
   uint32_t tour_k;
   const float* cumfit;  // roulette: inclusive prefix sums of shifted scores (S)
+  const uint32_t* rank_order;  // rank: individuals by ascending (score_key, index)
+  uint32_t rank_thresh;        // rank: uniform-branch threshold (2 - sp) * 2^32
 
   // crossover
   int32_t crossover;
@@ -290,7 +293,25 @@ struct GenArgs {
 };
 
 PGA_HD uint32_t sel_words(const GenArgs& a) {
-  return a.selection == SEL_TOURNAMENT ? 2u * a.tour_k : 2u;
+  return a.selection == SEL_TOURNAMENT ? 2u * a.tour_k : (a.selection == SEL_RANK ? 6u : 2u);
+}
+
+// Linear ranking selection, exactly and without floating point: the rank
+// density of pressure sp, P(r) = (2-sp)/S + (sp-1)(2r+1)/S^2 (r = 0 worst),
+// is a mixture of the uniform rank (weight 2-sp) and the maximum of two
+// uniform ranks (weight sp-1, P(max = r) = (2r+1)/S^2).  Three words per
+// parent: branch, first rank, second rank.  Integer-only, so the CPU backend
+// and the kernels agree bit for bit.
+PGA_HD uint32_t rank_thresh_of(float sp) {
+  const double b = 2.0 - (double)(sp < 1.f ? 1.f : (sp > 2.f ? 2.f : sp));
+  const double t = b * 4294967296.0;
+  return t >= 4294967295.0 ? 0xFFFFFFFFu : (uint32_t)t;
+}
+PGA_HD uint32_t rank_pick(uint32_t w_branch, uint32_t w1, uint32_t w2, uint32_t S, uint32_t thresh) {
+  const uint32_t r1 = word_to_index(w1, S);
+  if (w_branch < thresh) return r1;
+  const uint32_t r2 = word_to_index(w2, S);
+  return r1 > r2 ? r1 : r2;
 }
 
 // Bernoulli(p) flips over positions [0, clen) of chunk c (clen <= kMutCap):

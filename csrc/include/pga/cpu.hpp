@@ -24,6 +24,7 @@ unsigned long long reduce_best(const unsigned long long* parts, uint32_t n);
 unsigned long long best_of_scores(const float* scores, uint64_t S);
 void score_stats(const float* scores, uint64_t S, float* out4);
 void roulette_prefix(const float* scores, uint64_t S, float* cumfit);
+void rank_order(const float* scores, uint64_t S, uint32_t* order);
 void topk(const float* scores, uint64_t S, uint32_t k, bool largest, uint32_t* idx_out, bool sorted = true);
 void gather_rows(const void* rows, const float* scores, uint32_t row_words, const uint32_t* idx, uint32_t n,
                  void* out_rows, float* out_scores);

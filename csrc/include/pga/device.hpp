@@ -134,6 +134,13 @@ __device__ __forceinline__ void select_parents(const GenArgs& a, const Pool<GS>&
   } else if (a.selection == SEL_ROULETTE) {
     pa = roulette_pick(a.cumfit, S, pool.get(W_SEL + 0, a.key, child));
     pb = roulette_pick(a.cumfit, S, pool.get(W_SEL + 1, a.key, child));
+  } else if (a.selection == SEL_RANK) {
+    const uint32_t ra = rank_pick(pool.get(W_SEL + 0, a.key, child), pool.get(W_SEL + 1, a.key, child),
+                                  pool.get(W_SEL + 2, a.key, child), S, a.rank_thresh);
+    const uint32_t rb = rank_pick(pool.get(W_SEL + 3, a.key, child), pool.get(W_SEL + 4, a.key, child),
+                                  pool.get(W_SEL + 5, a.key, child), S, a.rank_thresh);
+    pa = a.rank_order[ra];
+    pb = a.rank_order[rb];
   } else {
     pa = word_to_index(pool.get(W_SEL + 0, a.key, child), S);
     pb = word_to_index(pool.get(W_SEL + 1, a.key, child), S);

@@ -35,6 +35,7 @@ struct Config {
   int32_t mutation = MUT_BIT_FLIP;
   float mut_rate = -1.f;  // < 0: 1/L per gene (BIT_FLIP/GAUSSIAN/UNIFORM), 0.01 per individual (RESET_ONE...)
   float sigma = 0.1f;
+  float rank_pressure = 1.5f;  // SEL_RANK: expected copies of the best individual, in [1, 2]
   float lo = 0.f, hi = 1.f;
   int32_t objective = OBJ_ONEMAX;
   int32_t obj_i = 0;
@@ -159,6 +160,7 @@ class Island {
   Buffer rows_[2], scores_[2], best_[2], keys_[2];
   uint32_t n_best_[2] = {0, 0};
   Buffer mut_thr_, obj_data_[2], elite_idx_, cumfit_, cum_ws_, topk_ws_, stats_, out_best_, scratch_;
+  Buffer rank_order_, rank_ws_;
   size_t obj_len_[2] = {0, 0};
   float mut_inv_ = 0.f;
   float mut_rate_eff_ = 0.f;

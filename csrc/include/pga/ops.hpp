@@ -70,6 +70,9 @@ void advance_counter_launch(uint32_t* counter, uint32_t delta, hipStream_t s);
 void score_stats_launch(const float* scores, uint64_t S, float* stats, hipStream_t s);
 // roulette: cumfit = inclusive prefix sum of max(score - min, 0); workspace >= 2*kMaxGrid floats
 void roulette_prefix_launch(const float* scores, uint64_t S, float* cumfit, float* workspace, hipStream_t s);
+// rank selection: order = indices by ascending (score_key, index); workspace: rank_order_workspace_bytes(S)
+size_t rank_order_workspace_bytes(uint64_t S);
+void rank_order_launch(const float* scores, uint64_t S, uint32_t* order, void* workspace, hipStream_t s);
 // top-k by score (descending, ties -> lower index); idx_out[k]; workspace: topk_workspace_bytes(S)
 size_t topk_workspace_bytes(uint64_t S, uint32_t k);
 // sorted = false: the k indices in selection order (keys above the threshold by

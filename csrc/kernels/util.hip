@@ -602,6 +602,45 @@ void roulette_prefix_launch(const float* scores, uint64_t S, float* cumfit, floa
   PGA_HIP_CHECK(hipGetLastError());
 }
 
+// ---------------- rank order (linear ranking selection) ----------------
+// order = individuals by ascending (score_key, index): keys + iota, then one
+// stable LSD radix sort of 32-bit keys (hipcub; 4 passes of 8 bits on gfx950)
+__global__ __launch_bounds__(kBlock) void rank_keys_kernel(const float* s, uint64_t S, uint32_t* keys, uint32_t* idx) {
+  for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < S; i += (uint64_t)gridDim.x * kBlock) {
+    keys[i] = score_key(s[i]);
+    idx[i] = (uint32_t)i;
+  }
+}
+
+namespace {
+size_t rank_cub_bytes(uint64_t S) {
+  size_t b = 0;
+  PGA_HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(nullptr, b, (uint32_t*)nullptr, (uint32_t*)nullptr,
+                                                   (uint32_t*)nullptr, (uint32_t*)nullptr, (int)S));
+  return (b + 255) & ~(size_t)255;
+}
+}  // namespace
+
+size_t rank_order_workspace_bytes(uint64_t S) {
+  const size_t arr = ((4 * S) + 255) & ~(size_t)255;
+  return 3 * arr + rank_cub_bytes(S);
+}
+
+void rank_order_launch(const float* scores, uint64_t S, uint32_t* order, void* ws, hipStream_t s) {
+  if (S >= (1ull << 31)) throw std::runtime_error("rank selection: population too large for the device sort");
+  const size_t arr = ((4 * S) + 255) & ~(size_t)255;
+  uint32_t* keys_in = (uint32_t*)ws;
+  uint32_t* keys_out = (uint32_t*)((char*)ws + arr);
+  uint32_t* idx_in = (uint32_t*)((char*)ws + 2 * arr);
+  void* tmp = (char*)ws + 3 * arr;
+  size_t tb = rank_cub_bytes(S);
+  uint32_t grid = launch_grid(S, kBlock * 4);
+  if (grid > 2048) grid = 2048;
+  hipLaunchKernelGGL(rank_keys_kernel, grid, kBlock, 0, s, scores, S, keys_in, idx_in);
+  PGA_HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(tmp, tb, keys_in, keys_out, idx_in, order, (int)S, 0, 32, s));
+  PGA_HIP_CHECK(hipGetLastError());
+}
+
 size_t topk_workspace_bytes(uint64_t S, uint32_t k) {
   size_t cub_bytes = 0;
   PGA_HIP_CHECK(hipcub::DeviceRadixSort::SortPairsDescending(nullptr, cub_bytes, (uint32_t*)nullptr,

@@ -48,7 +48,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
 
 #define E(name) m.attr(#name) = (int)pga::name
   E(ENC_BINARY); E(ENC_REAL); E(ENC_PERMUTATION);
-  E(SEL_TOURNAMENT); E(SEL_ROULETTE); E(SEL_RANDOM);
+  E(SEL_TOURNAMENT); E(SEL_ROULETTE); E(SEL_RANDOM); E(SEL_RANK);
   E(XO_UNIFORM); E(XO_ONE_POINT); E(XO_TWO_POINT); E(XO_BLEND); E(XO_ARITHMETIC); E(XO_PMX); E(XO_OX); E(XO_NONE);
   E(MUT_BIT_FLIP); E(MUT_GAUSSIAN); E(MUT_UNIFORM); E(MUT_RESET_ONE); E(MUT_SWAP); E(MUT_INVERSION); E(MUT_NONE);
   E(OBJ_NONE); E(OBJ_ONEMAX); E(OBJ_KNAPSACK); E(OBJ_TRAP); E(OBJ_LEADING_ONES);
@@ -71,6 +71,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def_readwrite("mutation", &pga::Config::mutation)
       .def_readwrite("mut_rate", &pga::Config::mut_rate)
       .def_readwrite("sigma", &pga::Config::sigma)
+      .def_readwrite("rank_pressure", &pga::Config::rank_pressure)
       .def_readwrite("lo", &pga::Config::lo)
       .def_readwrite("hi", &pga::Config::hi)
       .def_readwrite("objective", &pga::Config::objective)

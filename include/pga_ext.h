@@ -16,7 +16,7 @@ extern "C" {
 #endif
 
 enum pga_encoding { PGA_BINARY = 0, PGA_REAL = 1, PGA_PERMUTATION = 2 };
-enum pga_selection { PGA_SEL_TOURNAMENT = 0, PGA_SEL_ROULETTE = 1, PGA_SEL_RANDOM = 2 };
+enum pga_selection { PGA_SEL_TOURNAMENT = 0, PGA_SEL_ROULETTE = 1, PGA_SEL_RANDOM = 2, PGA_SEL_RANK = 3 };
 enum pga_crossover {
   PGA_XO_UNIFORM = 0, PGA_XO_ONE_POINT = 1, PGA_XO_TWO_POINT = 2, PGA_XO_BLEND = 3,
   PGA_XO_ARITHMETIC = 4, PGA_XO_PMX = 5, PGA_XO_OX = 6, PGA_XO_NONE = 7
@@ -60,6 +60,8 @@ int pga_set_operators(pga_t *p, population_t *pop, enum pga_selection selection,
                       float mutation_rate /* < 0: default */, float sigma, unsigned elitism);
 int pga_set_bounds(pga_t *p, population_t *pop, float lo, float hi);
 int pga_set_blend_alpha(pga_t *p, population_t *pop, float alpha);
+/* PGA_SEL_RANK: linear ranking pressure sp in [1, 2] (expected copies of the best; default 1.5) */
+int pga_set_rank_pressure(pga_t *p, population_t *pop, float sp);
 
 /* ---- queries ---- */
 unsigned long pga_population_size(const population_t *pop);

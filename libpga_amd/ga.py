@@ -23,7 +23,7 @@ import torch
 from ._ext import C
 from .models.base import ENCODINGS, Operators, Problem
 
-SELECTIONS = {"tournament": C.SEL_TOURNAMENT, "roulette": C.SEL_ROULETTE, "random": C.SEL_RANDOM}
+SELECTIONS = {"tournament": C.SEL_TOURNAMENT, "roulette": C.SEL_ROULETTE, "random": C.SEL_RANDOM, "rank": C.SEL_RANK}
 CROSSOVERS = {
     "uniform": C.XO_UNIFORM, "one_point": C.XO_ONE_POINT, "two_point": C.XO_TWO_POINT, "blend": C.XO_BLEND,
     "arithmetic": C.XO_ARITHMETIC, "pmx": C.XO_PMX, "ox": C.XO_OX, "none": C.XO_NONE,
@@ -110,6 +110,7 @@ class GeneticAlgorithm:
         cfg.mutation = MUTATIONS[ops.mutation]
         cfg.mut_rate = -1.0 if ops.mutation_rate is None else float(ops.mutation_rate)
         cfg.sigma = float(ops.sigma)
+        cfg.rank_pressure = float(ops.rank_pressure)
         cfg.n_elite = int(ops.elitism)
 
     def set_operators(self, **kw) -> None:

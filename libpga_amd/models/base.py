@@ -33,6 +33,7 @@ class Operators:
     mutation_rate: Optional[float] = None  # None: 1/L per gene, 0.01 per individual
     sigma: float = 0.1
     elitism: int = 0
+    rank_pressure: float = 1.5  # selection="rank": linear ranking pressure in [1, 2]
 
 
 class Problem:

@@ -223,3 +223,37 @@ def test_uniform_crossover_bit_balance():
     g = ga.genomes()[mixed].double()
     per_bit = g.mean(0)  # every position balanced
     assert (per_bit - 0.5).abs().max().item() < 6 * math.sqrt(0.25 / g.shape[0])
+
+
+@pytest.mark.parametrize("sp", [1.0, 1.5, 2.0])
+def test_rank_selection_pressure(sp):
+    """Linear ranking with distinct scores: a copied parent's rank r has
+    P(r) = (2-sp)/S + (sp-1)(2r+1)/S^2 exactly (core.hpp rank_pick)."""
+    S, L = 4096, 24
+    ga = make(_value_problem(L), S=S, selection="rank", rank_pressure=sp, crossover="none", mutation="none")
+    vals = torch.randperm(S)
+    bits = ((vals[:, None] >> torch.arange(L)) & 1).to(torch.uint8)
+    _set_population(ga, bits)
+    ga.run(1)
+    r = torch.arange(S, dtype=torch.float64)
+    pmf = (2 - sp) / S + (sp - 1) * (2 * r + 1) / S ** 2
+    assert abs(pmf.sum().item() - 1) < 1e-12
+    mean = (pmf * r).sum().item()
+    sd = math.sqrt((pmf * (r - mean) ** 2).sum().item())
+    got = ga.scores.double()
+    assert abs(got.mean().item() - mean) < 5 * sd / math.sqrt(S), (sp, got.mean().item(), mean)
+    # the best individual is copied sp times on average
+    top = (got == S - 1).double().sum().item()
+    assert abs(top - sp) < 6 * math.sqrt(sp) + 1
+
+
+def test_rank_selection_converges_and_is_deterministic():
+    runs = []
+    for _ in range(2):
+        ga = make(pga.models.OneMax(64), S=512, selection="rank", rank_pressure=2.0, elitism=1)
+        ga.run(60)
+        runs.append(ga.scores.clone())
+    assert torch.equal(runs[0], runs[1])
+    assert runs[0].max().item() == 64.0
+    with pytest.raises(Exception):
+        make(pga.models.OneMax(64), S=64, selection="rank", rank_pressure=2.5)

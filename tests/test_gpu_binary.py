@@ -159,3 +159,13 @@ def test_gpu_topk_matches_cpu(problem, sorted_):
             a = g.island.topk(k, largest, sorted_).cpu()
             b = c.island.topk(k, largest, sorted_)
             assert torch.equal(a, b), (k, largest, sorted_)
+
+
+@pytest.mark.parametrize("sp", [1.25, 2.0])
+def test_rank_selection_bitexact(sp):
+    """Device rank order (hipcub stable radix sort of score keys) + integer
+    rank sampling reproduce the CPU backend bit for bit, ties included."""
+    g, c = pair(pga.models.OneMax(300), 5000, selection="rank", rank_pressure=sp, elitism=2)
+    g.run(4)
+    c.run(4)
+    same(g, c)

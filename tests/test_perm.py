@@ -83,3 +83,26 @@ def test_gpu_tsp256_pop256k():
     assert is_perm(g)
     assert torch.allclose(p.reference_fitness(g), ga.scores[idx], rtol=1e-4, atol=0.5)
     assert ga.best_score() > b0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("sel", ["rank", "roulette"])
+def test_gpu_bitexact_selections(sel):
+    p = M.TSP.random_euclidean(64, seed=3)
+    kw = dict(seed=6, crossover="pmx", mutation="swap", mutation_rate=0.3, elitism=1, selection=sel)
+    g = pga.GeneticAlgorithm(p, 1500, device="cuda:0", **kw)
+    c = pga.GeneticAlgorithm(p, 1500, device="cpu", **kw)
+    g.run(3)
+    c.run(3)
+    torch.cuda.synchronize()
+    assert torch.equal(g.rows.cpu(), c.rows)
+    assert torch.equal(g.scores.cpu(), c.scores)
+
+
+def test_cpu_rank_selection_tsp():
+    p = M.TSP.random_euclidean(32, seed=4)
+    ga = pga.GeneticAlgorithm(p, 512, seed=1, device="cpu", selection="rank", rank_pressure=1.8, elitism=1)
+    s0 = ga.best_score()
+    ga.run(30)
+    assert ga.best_score() > s0
+    assert is_perm(ga.genomes())
