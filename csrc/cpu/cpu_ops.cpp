@@ -14,9 +14,42 @@
 namespace pga {
 namespace cpu {
 
+// x^T Q x of S bit rows with the kernels' coefficient rule (qubo_coef) and
+// integer accumulation: bit-identical to qubo.hip
+uint32_t qubo_eval(const void* rows, uint32_t row_words, uint64_t S, uint32_t L, const float* q, float sign,
+                   float* scores, unsigned long long* best_parts) {
+  std::vector<int32_t> Q((size_t)L * L);
+  for (size_t i = 0; i < Q.size(); ++i) Q[i] = qubo_coef(q[i]);
+  const uint32_t* r = (const uint32_t*)rows;
+  std::vector<uint32_t> on;
+  unsigned long long best = 0;
+  for (uint64_t c = 0; c < S; ++c) {
+    on.clear();
+    for (uint32_t k = 0; k < L; ++k)
+      if ((r[c * row_words + k / 32] >> (k % 32)) & 1u) on.push_back(k);
+    int64_t f = 0;
+    for (uint32_t k : on)
+      for (uint32_t n : on) f += Q[(size_t)k * L + n];
+    const float sc = sign * (float)(int32_t)f;
+    scores[c] = sc;
+    const unsigned long long pb = pack_best(sc, c);
+    best = pb > best ? pb : best;
+  }
+  if (best_parts) best_parts[0] = best;
+  return 1;
+}
+
 uint32_t encoding_run(int mode, const GenArgs& a, unsigned long long* best_parts) {
   switch (a.encoding) {
-    case ENC_BINARY: return binary_run(mode, a, best_parts);
+    case ENC_BINARY:
+      if (a.objective == OBJ_QUBO && (mode == MODE_GEN || mode == MODE_INIT || mode == MODE_EVAL)) {
+        GenArgs b = a;
+        b.objective = OBJ_NONE;
+        b.key_next = nullptr;
+        if (mode != MODE_EVAL) binary_run(mode, b, best_parts);
+        return qubo_eval(a.next, a.row_words, a.S, a.L, a.obj_data, a.obj_f0, a.score_next, best_parts);
+      }
+      return binary_run(mode, a, best_parts);
     case ENC_REAL: return real_run(mode, a, best_parts);
     default: return perm_run(mode, a, best_parts);
   }

@@ -66,7 +66,7 @@ Island::Island(const Config& cfg, int device) : cfg_(cfg), device_(device) {
 Island::~Island() {
   Buffer* all[] = {&rows_[0],   &rows_[1],     &scores_[0],   &scores_[1],  &best_[0],  &best_[1],   &mut_thr_,
                    &obj_data_[0], &obj_data_[1], &keys_[0], &keys_[1], &elite_idx_, &cumfit_, &cum_ws_, &topk_ws_, &stats_,
-                   &out_best_,  &scratch_, &compat_rand_, &ev_parts_, &gen_dev_, &rank_order_, &rank_ws_};
+                   &out_best_,  &scratch_, &compat_rand_, &ev_parts_, &gen_dev_, &rank_order_, &rank_ws_, &qubo_qt_};
   drop_graph();
   if (cap_stream_) (void)hipStreamDestroy(cap_stream_);
   for (Buffer* b : all) {
@@ -187,11 +187,29 @@ void Island::set_objective_data(const float* host, size_t n, int which) {
   obj_data_[which] = alloc(4ull * (n ? n : 1));
   if (n) copy_to_device(obj_data_[which].ptr, host, 4ull * n);
   obj_len_[which] = n;
+  ++obj_version_;
+}
+
+void Island::prepare_objective() {
+  if (cfg_.objective != OBJ_QUBO) return;
+  if (cfg_.encoding != ENC_BINARY) throw std::invalid_argument("the QUBO objective needs the BINARY encoding");
+  if (obj_len_[0] < (size_t)cfg_.L * cfg_.L) throw std::invalid_argument("QUBO: objective data must hold the L x L matrix Q");
+  if (!on_gpu() || qubo_version_ == obj_version_) return;
+  const uint32_t lp = qubo_padded_length(cfg_.L);
+  if (lp > kQuboMaxBits) throw std::invalid_argument("QUBO objective supports genomes of at most 1024 bits");
+  if (qubo_qt_.bytes < (size_t)lp * lp) {
+    release(qubo_qt_);
+    qubo_qt_ = alloc((size_t)lp * lp);
+  }
+  qubo_pack_launch((const float*)obj_data_[0].ptr, cfg_.L, (int8_t*)qubo_qt_.ptr, stream);
+  qubo_version_ = obj_version_;
 }
 
 GenArgs Island::make_args(int mode) {
+  prepare_objective();
   GenArgs a;
   std::memset(&a, 0, sizeof(a));
+  a.qubo_qt = (const int8_t*)qubo_qt_.ptr;
   const int nx = cur_ ^ 1;
   a.cur = rows_[cur_].ptr;
   a.next = rows_[nx].ptr;

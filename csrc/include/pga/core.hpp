@@ -73,6 +73,7 @@ enum Objective : int32_t {
   OBJ_KNAPSACK = 2,      // BINARY: 0/1 knapsack, data = [values L | weights L], p0 = capacity
   OBJ_TRAP = 3,          // BINARY: concatenated deceptive trap, block size param_i (2,4,8)
   OBJ_LEADING_ONES = 4,  // BINARY: number of leading one bits
+  OBJ_QUBO = 5,          // BINARY: obj_f0 * x^T Q x, data = L*L Q (integers in [-128,127]); int8 MFMA
   OBJ_SPHERE = 16,       // REAL: -sum z^2
   OBJ_RASTRIGIN = 17,    // REAL: -(10 D + sum z^2 - 10 cos(2 pi z))
   OBJ_ROSENBROCK = 18,   // REAL: -sum 100 (z_{i+1} - z_i^2)^2 + (1 - z_i)^2
@@ -282,6 +283,10 @@ struct GenArgs {
   const uint16_t* key_cur;
   uint16_t* key_next;
 
+  // derived objective data built by the runtime (QUBO: int8 Q^T padded to
+  // qubo_padded_length(L) square); nullptr when unused
+  const int8_t* qubo_qt;
+
   // padding mask for the last chunk (BINARY)
   u32x4 last_mask;
 
@@ -368,6 +373,13 @@ enum Mode : int32_t {
 // objectives whose scores are exact integers in [0, L] (u16 tournament keys)
 PGA_HD bool integer_objective(int32_t obj, uint32_t L) {
   return (obj == OBJ_ONEMAX || obj == OBJ_LEADING_ONES || obj == OBJ_TRAP) && L <= 65535u;
+}
+
+// QUBO coefficient as used by every backend: round half away from zero, clamp to int8
+PGA_HD int32_t qubo_coef(float q) {
+  float r = q < 0.f ? -__builtin_floorf(-q + 0.5f) : __builtin_floorf(q + 0.5f);
+  r = r < -128.f ? -128.f : (r > 127.f ? 127.f : r);
+  return (int32_t)r;
 }
 
 // orderable encoding of a float score (monotone, -NaN < -inf < ... < +inf)

@@ -161,6 +161,9 @@ class Island {
   uint32_t n_best_[2] = {0, 0};
   Buffer mut_thr_, obj_data_[2], elite_idx_, cumfit_, cum_ws_, topk_ws_, stats_, out_best_, scratch_;
   Buffer rank_order_, rank_ws_;
+  Buffer qubo_qt_;               // QUBO: int8 Q^T packed from objective data slot 0 (GPU)
+  uint32_t obj_version_ = 0, qubo_version_ = ~0u;
+  void prepare_objective();      // derived objective data (QUBO packing)
   size_t obj_len_[2] = {0, 0};
   float mut_inv_ = 0.f;
   float mut_rate_eff_ = 0.f;

@@ -46,9 +46,27 @@ uint32_t perm_launch(int mode, const GenArgs& a, unsigned long long* best_parts,
 // function pointers (crossover_f / mutate_f / obj_f), REAL encoding only
 uint32_t compat_launch(int mode, const GenArgs& a, unsigned long long* best_parts, hipStream_t s);
 
+// QUBO on the int8 matrix cores (qubo.hip): genomes up to kQuboMaxBits bits
+constexpr uint32_t kQuboMaxBits = 1024;
+uint32_t qubo_padded_length(uint32_t L);  // 64, 128, 256, 512 or 1024
+// qt: Lp x Lp int8 (Lp = qubo_padded_length(L)), Q^T of round/clamped q
+void qubo_pack_launch(const float* q, uint32_t L, int8_t* qt, hipStream_t s);
+// scores[i] = sign * x_i^T Q x_i for S bit rows; per-block bests -> parts; returns the grid
+uint32_t qubo_eval_launch(const void* rows, uint32_t row_words, uint64_t S, uint32_t L, const int8_t* qt, float sign,
+                          float* scores, unsigned long long* parts, hipStream_t s);
+
 inline uint32_t encoding_launch(int mode, const GenArgs& a, unsigned long long* best_parts, hipStream_t s) {
   switch (a.encoding) {
-    case ENC_BINARY: return binary_launch(mode, a, best_parts, s);
+    case ENC_BINARY:
+      if (a.objective == OBJ_QUBO && (mode == MODE_GEN || mode == MODE_INIT || mode == MODE_EVAL)) {
+        // the fused kernel writes the children, the matrix cores score them
+        GenArgs b = a;
+        b.objective = OBJ_NONE;
+        b.key_next = nullptr;
+        if (mode != MODE_EVAL) binary_launch(mode, b, best_parts, s);
+        return qubo_eval_launch(a.next, a.row_words, a.S, a.L, a.qubo_qt, a.obj_f0, a.score_next, best_parts, s);
+      }
+      return binary_launch(mode, a, best_parts, s);
     case ENC_REAL:
       if (a.user_xo_fn || a.user_mut_fn) return compat_launch(mode, a, best_parts, s);
       return real_launch(mode, a, best_parts, s);

@@ -51,7 +51,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   E(SEL_TOURNAMENT); E(SEL_ROULETTE); E(SEL_RANDOM); E(SEL_RANK);
   E(XO_UNIFORM); E(XO_ONE_POINT); E(XO_TWO_POINT); E(XO_BLEND); E(XO_ARITHMETIC); E(XO_PMX); E(XO_OX); E(XO_NONE);
   E(MUT_BIT_FLIP); E(MUT_GAUSSIAN); E(MUT_UNIFORM); E(MUT_RESET_ONE); E(MUT_SWAP); E(MUT_INVERSION); E(MUT_NONE);
-  E(OBJ_NONE); E(OBJ_ONEMAX); E(OBJ_KNAPSACK); E(OBJ_TRAP); E(OBJ_LEADING_ONES);
+  E(OBJ_NONE); E(OBJ_ONEMAX); E(OBJ_KNAPSACK); E(OBJ_TRAP); E(OBJ_LEADING_ONES); E(OBJ_QUBO);
   E(OBJ_SPHERE); E(OBJ_RASTRIGIN); E(OBJ_ROSENBROCK); E(OBJ_ACKLEY); E(OBJ_GRIEWANK); E(OBJ_SCHWEFEL);
   E(OBJ_LINEAR); E(OBJ_KNAPSACK_REAL); E(OBJ_TSP_RANDOM_KEY); E(OBJ_TSP); E(OBJ_TSP_OPEN); E(OBJ_TSP_EUC); E(OBJ_USER_FNPTR);
   E(MODE_GEN); E(MODE_INIT); E(MODE_EVAL); E(MODE_CROSS); E(MODE_MUTATE);

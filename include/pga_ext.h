@@ -27,6 +27,7 @@ enum pga_mutation {
 };
 enum pga_objective {
   PGA_OBJ_NONE = 0, PGA_OBJ_ONEMAX = 1, PGA_OBJ_KNAPSACK = 2, PGA_OBJ_TRAP = 3, PGA_OBJ_LEADING_ONES = 4,
+  PGA_OBJ_QUBO = 5, /* BINARY, data = L*L integer Q in [-128,127], fparam0 = sign (+1 max x^TQx, -1 min) */
   PGA_OBJ_SPHERE = 16, PGA_OBJ_RASTRIGIN = 17, PGA_OBJ_ROSENBROCK = 18, PGA_OBJ_ACKLEY = 19,
   PGA_OBJ_GRIEWANK = 20, PGA_OBJ_SCHWEFEL = 21, PGA_OBJ_LINEAR = 22, PGA_OBJ_KNAPSACK_REAL = 23,
   PGA_OBJ_TSP_RANDOM_KEY = 24, PGA_OBJ_TSP = 32, PGA_OBJ_TSP_OPEN = 33, PGA_OBJ_TSP_EUC = 34,

@@ -104,6 +104,82 @@ class LeadingOnes(Problem):
         return first0.to(torch.float32)
 
 
+class QUBO(Problem):
+    """Quadratic unconstrained binary optimisation: ``sign * x^T Q x``.
+
+    ``Q`` is an ``L x L`` integer matrix with entries in [-128, 127]
+    (L <= 1024).  On the GPU the population is scored on the int8 matrix
+    cores (``v_mfma_i32_16x16x64_i8``, csrc/kernels/qubo.hip) with exact i32
+    accumulation, so GPU and CPU scores agree bit for bit.  ``maximize=False``
+    (the QUBO convention) scores ``-x^T Q x``."""
+
+    def __init__(self, Q, maximize: bool = False):
+        q = torch.as_tensor(Q)
+        if q.ndim != 2 or q.shape[0] != q.shape[1]:
+            raise ValueError("Q must be a square matrix")
+        if q.shape[0] > 1024:
+            raise ValueError("QUBO supports at most 1024 variables")
+        qf = q.to(torch.float64)
+        if not torch.equal(qf, qf.round()) or qf.min() < -128 or qf.max() > 127:
+            raise ValueError("Q entries must be integers in [-128, 127] (int8 matrix cores)")
+        self.encoding = "binary"
+        self.Q = q.to(torch.float32).contiguous()
+        self.length = int(q.shape[0])
+        self.objective = C.OBJ_QUBO
+        self.sign = 1.0 if maximize else -1.0
+        self.obj_f0 = self.sign
+
+    def data(self) -> torch.Tensor:
+        return self.Q.reshape(-1)
+
+    def reference_fitness(self, genomes: torch.Tensor) -> torch.Tensor:
+        g = genomes.to(torch.float64)
+        q = self.Q.to(device=g.device, dtype=torch.float64)
+        f = ((g @ q) * g).sum(-1)
+        return (self.sign * f.to(torch.int64).to(torch.float32))
+
+    @staticmethod
+    def random(n: int, seed: int = 0, lo: int = -8, hi: int = 8, maximize: bool = False) -> "QUBO":
+        gen = torch.Generator().manual_seed(seed)
+        return QUBO(torch.randint(lo, hi + 1, (n, n), generator=gen), maximize=maximize)
+
+
+class MaxCut(QUBO):
+    """Maximum cut of an undirected graph with integer edge weights, as the
+    QUBO ``cut(x) = x^T (diag(deg) - W) x`` (maximised).  Weighted degrees
+    must stay within 127 (int8 diagonal)."""
+
+    def __init__(self, W):
+        w = torch.as_tensor(W).to(torch.int64)
+        if w.ndim != 2 or w.shape[0] != w.shape[1] or not torch.equal(w, w.T):
+            raise ValueError("W must be a symmetric square matrix")
+        w = w.clone()
+        w.fill_diagonal_(0)
+        deg = w.sum(1)
+        if deg.max() > 127 or w.min() < -128:
+            raise ValueError("weighted degrees must be <= 127 for the int8 QUBO form")
+        self.W = w
+        super().__init__(torch.diag(deg) - w, maximize=True)
+
+    def cut_value(self, genomes: torch.Tensor) -> torch.Tensor:
+        g = genomes.to(torch.int64)
+        w = self.W.to(g.device)
+        diff = (g[:, :, None] != g[:, None, :]).to(torch.int64)
+        return (diff * w).sum((1, 2)) // 2
+
+    @staticmethod
+    def random_graph(n: int, degree: float = 8.0, seed: int = 0) -> "MaxCut":
+        gen = torch.Generator().manual_seed(seed)
+        p = min(1.0, degree / max(1, n - 1))
+        upper = (torch.rand(n, n, generator=gen) < p).triu(1).to(torch.int64)
+        w = upper + upper.T
+        over = w.sum(1) > 127
+        if over.any():  # drop edges of over-full vertices (dense graphs)
+            w[over] = 0
+            w[:, over] = 0
+        return MaxCut(w)
+
+
 class BinaryTorchObjective(Problem):
     """User objective written in PyTorch over decoded bit genomes ``[N, L]``.
 
