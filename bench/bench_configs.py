@@ -71,11 +71,27 @@ def make(name: str):
         d = torch.cdist(xy, xy)
         xo = "ox" if name.endswith("ox") else "pmx"
         return M.TSP(d), 1 << 18, None, dict(elitism=1, crossover=xo), 50
+    if name == "maxcut512_qubo":
+        # Max-Cut of a random 512-vertex graph as a QUBO on the int8 matrix cores
+        return M.MaxCut.random_graph(512, degree=16, seed=1), 1 << 20, None, dict(elitism=1), 50
+    if name == "qubo1024":
+        # dense 1024-variable QUBO (1M int8 MACs per individual)
+        return M.QUBO.random(1024, seed=1, lo=-128, hi=127), 1 << 18, None, dict(elitism=1), 20
+    if name == "onemax1024_rank":
+        return M.OneMax(1024), 1 << 20, None, dict(elitism=1, selection="rank", rank_pressure=1.5), 100
     raise KeyError(name)
 
 
 NAMES = ["onemax64_cpu", "onemax1024", "rastrigin30", "rastrigin30_rot", "tsp256_ox", "tsp256_pmx", "e1_sum100_refops",
-         "tsp256_euc_ox", "tsp256_euc_pmx", "e2_knap_refops", "onemax64_gpu", "onemax1024_jit"]
+         "tsp256_euc_ox", "tsp256_euc_pmx", "e2_knap_refops", "onemax64_gpu", "onemax1024_jit", "maxcut512_qubo",
+         "qubo1024", "onemax1024_rank"]
+
+
+def qubo_padded(L: int) -> int:
+    lp = 64
+    while lp < L:
+        lp *= 2
+    return lp
 
 
 def run_one(name: str, steps_scale: float) -> dict:
@@ -98,7 +114,9 @@ def run_one(name: str, steps_scale: float) -> dict:
     return {"config": name, "device": dev if dev == "cpu" else torch.cuda.get_device_name(), "pop": S,
             "length": problem.length, "encoding": problem.encoding, "gens_per_sec": gens, "evals_per_sec": gens * S,
             "ms_per_gen": dt / steps * 1e3, "best": ga.best_score(), "steps": steps,
-            "effective_GBps": min_bytes * gens / 1e9}
+            "effective_GBps": min_bytes * gens / 1e9,
+            **({"int8_TOPS": 2.0 * qubo_padded(problem.length) ** 2 * S * gens / 1e12}
+               if problem.objective == pga._ext.C.OBJ_QUBO else {})}
 
 
 def main() -> int:

@@ -317,7 +317,9 @@ void Island::prepare_generation() {
   }
   if (cfg_.selection == SEL_RANK) {
     const float* sc = (const float*)scores_[cur_].ptr;
-    if (on_gpu()) rank_order_launch(sc, cfg_.S, (uint32_t*)rank_order_.ptr, rank_ws_.ptr, stream);
+    if (on_gpu() && integer_objective(cfg_.objective, cfg_.L) && keys_[cur_].ptr)
+      rank_order16_launch((const uint16_t*)keys_[cur_].ptr, cfg_.S, (uint32_t*)rank_order_.ptr, rank_ws_.ptr, stream);
+    else if (on_gpu()) rank_order_launch(sc, cfg_.S, (uint32_t*)rank_order_.ptr, rank_ws_.ptr, stream);
     else cpu::rank_order(sc, cfg_.S, (uint32_t*)rank_order_.ptr);
   }
   if (cfg_.n_elite > 1) topk(cfg_.n_elite, true, (uint32_t*)elite_idx_.ptr, /*sorted=*/false);

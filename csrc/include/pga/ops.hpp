@@ -91,6 +91,8 @@ void roulette_prefix_launch(const float* scores, uint64_t S, float* cumfit, floa
 // rank selection: order = indices by ascending (score_key, index); workspace: rank_order_workspace_bytes(S)
 size_t rank_order_workspace_bytes(uint64_t S);
 void rank_order_launch(const float* scores, uint64_t S, uint32_t* order, void* workspace, hipStream_t s);
+// the same order from the u16 tournament keys of an integer objective (2 radix passes)
+void rank_order16_launch(const uint16_t* keys16, uint64_t S, uint32_t* order, void* workspace, hipStream_t s);
 // top-k by score (descending, ties -> lower index); idx_out[k]; workspace: topk_workspace_bytes(S)
 size_t topk_workspace_bytes(uint64_t S, uint32_t k);
 // sorted = false: the k indices in selection order (keys above the threshold by

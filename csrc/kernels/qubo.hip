@@ -47,7 +47,7 @@ __device__ __forceinline__ v4i expand16(uint32_t h) {
 }
 
 template <int KS, int MT>
-__global__ __launch_bounds__(kBlock) void qubo_eval_kernel(const uint32_t* __restrict__ rows, uint32_t row_words,
+__global__ __launch_bounds__(kBlock, 2) void qubo_eval_kernel(const uint32_t* __restrict__ rows, uint32_t row_words,
                                                            uint64_t S, const int8_t* __restrict__ qt, float sign,
                                                            float* __restrict__ scores,
                                                            unsigned long long* __restrict__ parts) {
@@ -91,6 +91,7 @@ __global__ __launch_bounds__(kBlock) void qubo_eval_kernel(const uint32_t* __res
 #pragma unroll
       for (int i = 0; i < 4; ++i) fsum[t][i] = 0;
 
+#pragma unroll 1
     for (uint32_t nb = 0; nb < (uint32_t)KS; ++nb) {  // 64-column n-blocks of Q^T
       __syncthreads();
       constexpr uint32_t C16 = Lp / 16u;  // 16-byte chunks per Q^T row
@@ -107,7 +108,7 @@ __global__ __launch_bounds__(kBlock) void qubo_eval_kernel(const uint32_t* __res
 #pragma unroll
         for (int i = 0; i < 4; ++i)
           xb[t][i] = *(const unsigned long long*)(bits + (wave * 16u * MT + 16u * t + 4u * g + i) * BROW + 8u * nb);
-#pragma unroll
+#pragma unroll 2
       for (int jj = 0; jj < 4; ++jj) {  // 16-column n-tiles
         v4i acc[MT];
 #pragma unroll

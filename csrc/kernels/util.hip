@@ -626,6 +626,30 @@ size_t rank_order_workspace_bytes(uint64_t S) {
   return 3 * arr + rank_cub_bytes(S);
 }
 
+__global__ __launch_bounds__(kBlock) void iota_kernel(uint64_t S, uint32_t* idx) {
+  for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < S; i += (uint64_t)gridDim.x * kBlock)
+    idx[i] = (uint32_t)i;
+}
+
+// integer objectives: the u16 tournament keys order exactly like the scores
+// (non-negative integers <= 65535), so two 8-bit radix passes suffice
+void rank_order16_launch(const uint16_t* keys16, uint64_t S, uint32_t* order, void* ws, hipStream_t s) {
+  if (S >= (1ull << 31)) throw std::runtime_error("rank selection: population too large for the device sort");
+  const size_t arr = ((4 * S) + 255) & ~(size_t)255;
+  uint16_t* keys_out = (uint16_t*)((char*)ws + arr);
+  uint32_t* idx_in = (uint32_t*)((char*)ws + 2 * arr);
+  void* tmp = (char*)ws + 3 * arr;
+  size_t tb = 0;
+  PGA_HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, keys16, keys_out, idx_in, order, (int)S, 0, 16, s));
+  if (tb > rank_cub_bytes(S)) throw std::runtime_error("rank selection: workspace too small");
+  tb = rank_cub_bytes(S);
+  uint32_t grid = launch_grid(S, kBlock * 4);
+  if (grid > 2048) grid = 2048;
+  hipLaunchKernelGGL(iota_kernel, grid, kBlock, 0, s, S, idx_in);
+  PGA_HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(tmp, tb, keys16, keys_out, idx_in, order, (int)S, 0, 16, s));
+  PGA_HIP_CHECK(hipGetLastError());
+}
+
 void rank_order_launch(const float* scores, uint64_t S, uint32_t* order, void* ws, hipStream_t s) {
   if (S >= (1ull << 31)) throw std::runtime_error("rank selection: population too large for the device sort");
   const size_t arr = ((4 * S) + 255) & ~(size_t)255;
