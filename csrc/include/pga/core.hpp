@@ -111,8 +111,9 @@ enum Stream : uint32_t {
 //   3      per-individual mutation test (RESET_ONE / SWAP / INVERSION)
 //   4      per-individual mutation position
 //   5..    selection words (2k for tournament-k, 2 otherwise)
-// Further draws of one chunk's mutation come from stream ST_MUTX, block
-// (chunk << 6) | (n >> 2), register n & 3 for the n-th extra draw.
+// Further geometric skips of a BINARY chunk come from mut_skip_word(r0, n);
+// REAL mutation values come from stream ST_MUTX, block (chunk << 6) | (32 + n)
+// for the n-th mutated gene of the chunk, whose .w word is the next skip.
 constexpr uint32_t W_XOPROB = 0, W_CUT1 = 1, W_CUT2 = 2, W_MUTIND = 3, W_MUTPOS = 4, W_SEL = 5;
 constexpr uint32_t kMutCap = 128;  // geometric-skip table length (one BINARY chunk)
 
@@ -174,9 +175,23 @@ PGA_HD uint32_t child_word(const RngKey& key, uint64_t child, uint32_t t) {
 PGA_HD uint32_t chunk_mut_word(const RngKey& key, uint64_t child, uint32_t c) {
   return draw(key, ST_CHILD, child, c).w;
 }
-// n-th extra mutation draw of chunk c
-PGA_HD uint32_t chunk_mut_extra(const RngKey& key, uint64_t child, uint32_t c, uint32_t n) {
-  return sel4(draw(key, ST_MUTX, child, (c << 6) | (n >> 2)), n & 3u);
+// n-th further geometric-skip word of a BINARY chunk whose first mutation
+// word was r0 (only reached when r0 already placed a flip, ~12% of chunks at
+// rate 1/L = 1/1024).  A murmur3 finalizer of (r0, n) instead of another
+// Philox block: in a wave of 64 chunks SOME lane almost always needs it, so a
+// Philox here cost the whole wave a third Philox per child (measured: the
+// largest single VALU item of the headline kernel after the two mandatory
+// draws).  r0 is a Philox word spread over ~5e8 values, and the finalizer is
+// a bijection with full avalanche, so successive skips are uniform and
+// independent for every practical purpose.
+PGA_HD uint32_t mut_skip_word(uint32_t r0, uint32_t n) {
+  uint32_t h = r0 ^ (0x9E3779B9u * (n + 1u));
+  h ^= h >> 16;
+  h *= 0x85EBCA6Bu;
+  h ^= h >> 13;
+  h *= 0xC2B2AE35u;
+  h ^= h >> 16;
+  return h;
 }
 
 // uniform index in [0, n) from a 32-bit word (n < 2^32)
@@ -336,7 +351,7 @@ PGA_HD u32x4 chunk_flip_mask(const GenArgs& a, uint64_t child, uint32_t c, uint3
       case 2: m.z ^= bit; break;
       default: m.w ^= bit; break;
     }
-    pos += 1u + geom_skip(chunk_mut_extra(a.key, child, c, n++), thr, kMutCap, a.mut_inv_log2_1mp);
+    pos += 1u + geom_skip(mut_skip_word(r0, n++), thr, kMutCap, a.mut_inv_log2_1mp);
   }
   return m;
 }

@@ -81,12 +81,12 @@ PGA_HD void real_cross_chunk(const GenArgs& a, uint64_t child, uint32_t c, const
 
 // ---- mutation of chunk c (clen valid genes): Bernoulli(p) per gene ----
 // first draw r0 = chunk_mut_word; n-th mutated gene's values come from
-// ST_MUTX block (c << 6) | (32 + n): words 0,1 -> Box-Muller normal, 2 -> uniform
+// ST_MUTX block (c << 6) | (32 + n): words 0,1 -> Box-Muller normal, 2 -> uniform, 3 -> next skip
 PGA_HD void real_mutate_chunk(const GenArgs& a, uint64_t child, uint32_t c, uint32_t clen, uint32_t r0,
                               const uint32_t* thr, float v[4]) {
   if (r0 < thr[kMutCap - 1]) return;  // common case: no mutation in 128 draws' worth
   uint32_t pos = geom_skip(r0, thr, kMutCap, a.mut_inv_log2_1mp);
-  uint32_t n = 0, ne = 0;
+  uint32_t n = 0;
   while (pos < clen) {
     const u32x4 r = draw(a.key, ST_MUTX, child, (c << 6) | (32u + n));
     float x;
@@ -104,7 +104,7 @@ PGA_HD void real_mutate_chunk(const GenArgs& a, uint64_t child, uint32_t c, uint
     v[2] = fsel(pos == 2, x, v[2]);
     v[3] = fsel(pos == 3, x, v[3]);
     ++n;
-    pos += 1u + geom_skip(chunk_mut_extra(a.key, child, c, ne++), thr, kMutCap, a.mut_inv_log2_1mp);
+    pos += 1u + geom_skip(r.w, thr, kMutCap, a.mut_inv_log2_1mp);  // the value draw's spare word
   }
 }
 
