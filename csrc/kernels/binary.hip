@@ -24,6 +24,10 @@
 //                                three children deep (see below)
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+#include <cstdio>
+#include <vector>
+
 #include "pga/device.hpp"
 #include "pga/ops.hpp"
 
@@ -284,6 +288,15 @@ __device__ __forceinline__ uint4 load_row(const uint4* p) {
   return *p;
 }
 
+// PGA_STAMP builds (bench/micro only): per-wave start/end wall-clock stamps of
+// the pipelined kernel, dumped by pga_stamp_report() (ramp-up / tail study)
+#ifndef PGA_STAMP
+#define PGA_STAMP 0
+#endif
+#if PGA_STAMP
+__device__ unsigned long long g_stamps[2 * 65536];
+#endif
+
 // RESET: the per-individual reset mutation is possible (otherwise only
 // bit-flip / none, and the pool words are dead after stage 2: fewer VGPRs)
 template <int GS, int OBJ, int XOK, bool KEY, bool RESET>
@@ -319,6 +332,10 @@ __global__ __launch_bounds__(kBlock, RESET ? 5 : 6) void binary_gen_pipe(GenArgs
     for (uint32_t i = threadIdx.x; i < kMutCap; i += kBlock) lds_thr[i] = a.mut_thr[i];
   __syncthreads();
 
+#if PGA_STAMP
+  const uint32_t wid_ = blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
+  if (lane == 0 && wid_ < 65536) g_stamps[2 * wid_] = wall_clock64();
+#endif
   unsigned long long my_best = 0;
   const uint64_t stride = (uint64_t)gridDim.x * GPB;
   uint64_t c0 = (uint64_t)blockIdx.x * GPB + threadIdx.x / GS;
@@ -478,6 +495,9 @@ __global__ __launch_bounds__(kBlock, RESET ? 5 : 6) void binary_gen_pipe(GenArgs
 #undef PGA_STAGE1
 #undef PGA_STAGE2
 #undef PGA_STAGE3
+#if PGA_STAMP
+  if (lane == 0 && wid_ < 65536) g_stamps[2 * wid_ + 1] = wall_clock64();
+#endif
 
   unsigned long long b = block_max_u64(my_best, lds_red);
   if (threadIdx.x == 0 && best_parts) best_parts[blockIdx.x] = b;
@@ -535,6 +555,31 @@ uint32_t launch_obj(int mode, const GenArgs& a, unsigned long long* parts, hipSt
 }
 
 }  // namespace
+
+#if PGA_STAMP
+// wave start/end distribution of the last pipelined launch (100 MHz wall clock)
+void pga_stamp_report(uint32_t nwaves) {
+  std::vector<unsigned long long> h(2ull * nwaves);
+  PGA_HIP_CHECK(hipDeviceSynchronize());
+  PGA_HIP_CHECK(hipMemcpyFromSymbol(h.data(), HIP_SYMBOL(g_stamps), 16ull * nwaves));
+  unsigned long long t0 = ~0ull;
+  for (uint32_t i = 0; i < nwaves; ++i) t0 = h[2 * i] < t0 ? h[2 * i] : t0;
+  std::vector<double> st, en, du;
+  for (uint32_t i = 0; i < nwaves; ++i) {
+    st.push_back((h[2 * i] - t0) * 0.01);
+    en.push_back((h[2 * i + 1] - t0) * 0.01);
+    du.push_back((h[2 * i + 1] - h[2 * i]) * 0.01);
+  }
+  auto pr = [](const char* n, std::vector<double> v) {
+    std::sort(v.begin(), v.end());
+    std::printf("%s us: min %.1f p10 %.1f p50 %.1f p90 %.1f max %.1f\n", n, v[0], v[v.size() / 10], v[v.size() / 2],
+                v[v.size() * 9 / 10], v.back());
+  };
+  pr("wave start", st);
+  pr("wave end  ", en);
+  pr("wave life ", du);
+}
+#endif
 
 uint32_t binary_launch(int mode, const GenArgs& a, unsigned long long* best_parts, hipStream_t s) {
   uint32_t grid = 0;

@@ -54,7 +54,12 @@ uint32_t occupancy_blocks(const void* kernel, int block) {
 
 uint32_t launch_grid_occ(uint64_t S, uint32_t per_block, const void* kernel) {
   uint64_t need = (S + per_block - 1) / per_block;
-  uint64_t cap = (uint64_t)device_cu_count() * occupancy_blocks(kernel, dev::kBlock);
+  static int mult = -1;
+  if (mult < 0) {  // PGA_GRID_MULT: launch k x the resident grid (load-balance experiments)
+    const char* e = getenv("PGA_GRID_MULT");
+    mult = e && atoi(e) > 0 ? atoi(e) : 1;
+  }
+  uint64_t cap = (uint64_t)device_cu_count() * occupancy_blocks(kernel, dev::kBlock) * mult;
   if (cap > kMaxGrid) cap = kMaxGrid;
   uint64_t g = need < cap ? need : cap;
   return (uint32_t)(g == 0 ? 1 : g);
