@@ -12,9 +12,11 @@
 // BASELINE config 3) multiply the whole child tile by M^T with
 // v_mfma_f32_16x16x4_f32: 16 children x 16 dims per wave tile, K = 4 per
 // instruction, exact f32 (bit-for-bit a k-ordered fma chain, so the CPU
-// reference reproduces it), M staged once per block in LDS.  For the 30-D
-// Rastrigin config a block iteration is 32 children x 32 dims = 4 tiles, one
-// per wave, 8 MFMAs each.
+// reference reproduces it), M staged once per block in LDS (real_gen_fast,
+// L <= 128).  For L <= 32 (the 30-D Rastrigin config) the software-pipelined
+// kernel does the rotation wave-locally instead, with v_mfma_f32_4x4x1_16b_f32
+// (64/GS children x 4 GS dims = 16 blocks of 4x4 per wave, no empty rows),
+// the same exact fma chain, and no block barrier (real_gen_pipe, ROT).
 //
 // Reference parity: float genes, user objective via device function pointer
 // (OBJ_USER_FNPTR, include/pga.h:46 obj_f), E1 sum / E2 knapsack / E3 random-key
@@ -535,7 +537,7 @@ __global__ __launch_bounds__(kBlock) void real_gen_fast(GenArgs a, unsigned long
 
 
 // ---------------------------------------------------------------------------
-// Software-pipelined GEN kernel (non-rotated objectives), the REAL analogue of
+// Software-pipelined GEN kernel, the REAL analogue of
 // binary_gen_pipe: three children per lane group in flight — contestant score
 // loads of c+2, parent-row loads of c+1 and the variation / objective of c in
 // one loop body, three static register sets rotating X -> Y -> Z so hipcc's
@@ -543,13 +545,73 @@ __global__ __launch_bounds__(kBlock) void real_gen_fast(GenArgs a, unsigned long
 // are clamped, lanes without a chunk re-read the last chunk).  Tournament-2 or
 // random selection, any crossover / mutation, objectives that need no
 // neighbouring dimension.  Same semantics as real_kernel (bit-exact).
-template <int GS, int OBJ>
-__global__ __launch_bounds__(kBlock) void real_gen_pipe(GenArgs a, unsigned long long* best_parts) {
+//
+// ROT (GS 4 or 8, i.e. L <= 16 / 32): rotated objective f(M (x - o)) with the
+// rotation on the matrix cores, wave-local — no block barrier in the loop.
+// Per stage 3 the wave's 64/GS children are transposed through a private
+// 16 x 36 LDS tile, multiplied by M^T (rot_tile4), and the outputs go back
+// through the same tile to the lanes' own 4-gene chunks.  Same k-ordered
+// accumulation as real_gen_fast (bit-exact).  The loop condition is
+// wave-uniform here: every lane of the wave takes part in the tile even when
+// its own child is past S.  4 waves/SIMD (launch bounds; 3 without them:
+// rastrigin30_rot 211 -> 193 us/gen).
+constexpr uint32_t kRotTW = 36;  // tile row stride (floats): conflict-free column reads, 16-byte rows
+
+__device__ __forceinline__ void rot_wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// z (4 genes of this lane's chunk, shifted) -> rotated z, in place, with
+// v_mfma_f32_4x4x1_16b_f32 (16 independent 4x4 blocks, K = 1): the wave's
+// C = 64/GS children x DP = 4 GS dims are exactly 16 blocks (C/4 row groups x
+// GS column groups), so no tile row is wasted — a 16x16x4 tile leaves half its
+// rows empty at GS 8 and measured 4% slower (rastrigin30_rot 201 vs 193 us/gen).
+// One k per instruction: each output is the same sequential fma chain as the
+// CPU reference.  A = X[child][k] and B = M[n][k] come from LDS as dwordx4 runs
+// of 4 k (xw: this wave's tile, ms: the block's M tile, row stride kRotTW).
+template <int GS>
+__device__ __forceinline__ void rot_tile4(float* xw, const float* ms, float z[4]) {
+  constexpr int DP = 4 * GS;
+  const uint32_t lane = lane_id();
+  const uint32_t row = lane / GS, q = lane % GS;
+  const uint32_t b = lane >> 2, rg = b / GS, cg = b % GS;
+  const uint32_t ca = 4 * rg + (lane & 3);   // A row (child) of this lane
+  const uint32_t nb = 4 * cg + (lane & 3);   // B column (output dim) of this lane
+  *(float4*)(xw + row * kRotTW + 4 * q) = make_float4(z[0], z[1], z[2], z[3]);
+  rot_wave_sync();
+  floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int k4 = 0; k4 < DP / 4; ++k4) {
+    const float4 xa = *(const float4*)(xw + ca * kRotTW + 4 * k4);
+    const float4 mb = *(const float4*)(ms + nb * kRotTW + 4 * k4);
+    acc = __builtin_amdgcn_mfma_f32_4x4x1f32(xa.x, mb.x, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_4x4x1f32(xa.y, mb.y, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_4x4x1f32(xa.z, mb.z, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_4x4x1f32(xa.w, mb.w, acc, 0, 0, 0);
+  }
+  rot_wave_sync();
+#pragma unroll
+  for (int i = 0; i < 4; ++i) xw[(4 * rg + i) * kRotTW + nb] = acc[i];
+  rot_wave_sync();
+  const float4 r = *(const float4*)(xw + row * kRotTW + 4 * q);
+  z[0] = r.x;
+  z[1] = r.y;
+  z[2] = r.z;
+  z[3] = r.w;
+  rot_wave_sync();
+}
+
+template <int GS, int OBJ, bool ROT = false>
+__global__ __launch_bounds__(kBlock, ROT ? 4 : 1) void real_gen_pipe(GenArgs a, unsigned long long* best_parts) {
+  static_assert(!ROT || GS == 4 || GS == 8, "wave-local rotation: 16 or 32 padded dims");
   resolve_gen(a);
   a.objective = OBJ;  // compile-time objective: the term switches fold away
   __shared__ unsigned long long lds_red[kBlock / 64];
   __shared__ uint32_t lds_elite;
   __shared__ uint32_t lds_thr[kMutCap];
+  __shared__ __attribute__((aligned(16))) float lds_rot[ROT ? (kBlock / 64 + 2) * 16 * kRotTW : 1];  // 4 wave tiles + M
 
   const uint32_t lane = lane_id();
   const uint32_t q = lane & (GS - 1);
@@ -579,6 +641,13 @@ __global__ __launch_bounds__(kBlock) void real_gen_pipe(GenArgs a, unsigned long
     w1[j] = 0.f;
     if (evals && d < L) real_obj_data(a, d, w0[j], w1[j]);
   }
+  float* xw = lds_rot + (ROT ? (threadIdx.x >> 6) * 16 * kRotTW : 0);  // this wave's X/Z tile
+  float* ms = lds_rot + (ROT ? (kBlock / 64) * 16 * kRotTW : 0);        // M[n][k], block-shared
+  if (ROT)
+    for (uint32_t i = threadIdx.x; i < 32 * kRotTW; i += kBlock) {
+      const uint32_t n = i / kRotTW, k = i % kRotTW;
+      ms[i] = (n < L && k < L) ? a.obj_data[n * L + k] : 0.f;
+    }
 
   if (a.n_elite > 0 && a.elite_idx == nullptr && blockIdx.x == 0) {
     unsigned long long b = block_reduce_parts(a.best_cur, a.n_best_cur, lds_red);
@@ -646,80 +715,107 @@ __global__ __launch_bounds__(kBlock) void real_gen_pipe(GenArgs a, unsigned long
     P##B = cur[(uint64_t)pb_ * rs + qc];                                                        \
   }
 
-#define R_STAGE3(c, P)                                                                          \
-  if ((c) < a.S) {                                                                              \
-    const Pool<GS> pool_{P##w, gbase};                                                          \
-    uint32_t lo_ = 0, hi_ = 0;                                                                  \
-    float ua_ = 0.f;                                                                            \
-    if (a.crossover == XO_ONE_POINT) {                                                          \
-      lo_ = word_to_index(pool_.get(W_CUT1, a.key, (c)), L);                                    \
-      hi_ = L;                                                                                  \
-    } else if (a.crossover == XO_TWO_POINT) {                                                   \
-      const uint32_t x1_ = word_to_index(pool_.get(W_CUT1, a.key, (c)), L);                     \
-      const uint32_t x2_ = word_to_index(pool_.get(W_CUT2, a.key, (c)), L);                     \
-      lo_ = x1_ < x2_ ? x1_ : x2_;                                                              \
-      hi_ = x1_ < x2_ ? x2_ : x1_;                                                              \
-    } else if (a.crossover == XO_ARITHMETIC) {                                                  \
-      ua_ = word_to_unit(pool_.get(W_CUT1, a.key, (c)));                                        \
+#define R_VARY(c, P)                                                                            \
+  const Pool<GS> pool_{P##w, gbase};                                                            \
+  uint32_t lo_ = 0, hi_ = 0;                                                                    \
+  float ua_ = 0.f;                                                                              \
+  if (a.crossover == XO_ONE_POINT) {                                                            \
+    lo_ = word_to_index(pool_.get(W_CUT1, a.key, (c)), L);                                      \
+    hi_ = L;                                                                                    \
+  } else if (a.crossover == XO_TWO_POINT) {                                                     \
+    const uint32_t x1_ = word_to_index(pool_.get(W_CUT1, a.key, (c)), L);                       \
+    const uint32_t x2_ = word_to_index(pool_.get(W_CUT2, a.key, (c)), L);                       \
+    lo_ = x1_ < x2_ ? x1_ : x2_;                                                                \
+    hi_ = x1_ < x2_ ? x2_ : x1_;                                                                \
+  } else if (a.crossover == XO_ARITHMETIC) {                                                    \
+    ua_ = word_to_unit(pool_.get(W_CUT1, a.key, (c)));                                          \
+  }                                                                                             \
+  const float A_[4] = {P##A.x, P##A.y, P##A.z, P##A.w};                                         \
+  const float B_[4] = {P##B.x, P##B.y, P##B.z, P##B.w};                                         \
+  real_cross_chunk(a, (c), q, A_, B_, P##xo, lo_, hi_, ua_, v_);                                \
+  if (per_gene_mut) {                                                                           \
+    if (have) real_mutate_chunk(a, (c), q, clen, P##w.w, lds_thr, v_);                          \
+  } else if (reset_one && pool_.get(W_MUTIND, a.key, (c)) < a.mut_ind_thresh) {                 \
+    const uint32_t pos_ = word_to_index(pool_.get(W_MUTPOS, a.key, (c)), L);                    \
+    const float x_ = real_reset_value(a, pool_.get(W_SEL + sel_words(a), a.key, (c)));          \
+    if ((pos_ >> 2) == q) {                                                                     \
+      v_[0] = fsel(pos_ == 4 * q + 0, x_, v_[0]);                                               \
+      v_[1] = fsel(pos_ == 4 * q + 1, x_, v_[1]);                                               \
+      v_[2] = fsel(pos_ == 4 * q + 2, x_, v_[2]);                                               \
+      v_[3] = fsel(pos_ == 4 * q + 3, x_, v_[3]);                                               \
     }                                                                                           \
-    const float A_[4] = {P##A.x, P##A.y, P##A.z, P##A.w};                                       \
-    const float B_[4] = {P##B.x, P##B.y, P##B.z, P##B.w};                                       \
-    float v_[4];                                                                                \
-    real_cross_chunk(a, (c), q, A_, B_, P##xo, lo_, hi_, ua_, v_);                              \
-    if (per_gene_mut) {                                                                         \
-      if (have) real_mutate_chunk(a, (c), q, clen, P##w.w, lds_thr, v_);                        \
-    } else if (reset_one && pool_.get(W_MUTIND, a.key, (c)) < a.mut_ind_thresh) {               \
-      const uint32_t pos_ = word_to_index(pool_.get(W_MUTPOS, a.key, (c)), L);                  \
-      const float x_ = real_reset_value(a, pool_.get(W_SEL + sel_words(a), a.key, (c)));        \
-      if ((pos_ >> 2) == q) {                                                                   \
-        v_[0] = fsel(pos_ == 4 * q + 0, x_, v_[0]);                                             \
-        v_[1] = fsel(pos_ == 4 * q + 1, x_, v_[1]);                                             \
-        v_[2] = fsel(pos_ == 4 * q + 2, x_, v_[2]);                                             \
-        v_[3] = fsel(pos_ == 4 * q + 3, x_, v_[3]);                                             \
-      }                                                                                         \
+  }                                                                                             \
+  for (uint32_t j = 0; j < 4; ++j) v_[j] = j < clen ? v_[j] : 0.f;                              \
+  if (have) nxt[(c) * rs + q] = make_float4(v_[0], v_[1], v_[2], v_[3]);
+
+#define R_EVAL(c, ZE, ZN)                                                                       \
+  {                                                                                             \
+    RealAcc acc_{0.f, 0.f, 1.f};                                                                \
+    _Pragma("unroll") for (uint32_t j = 0; j < 4; ++j) {                                        \
+      const uint32_t d_ = 4 * q + j;                                                            \
+      if (d_ < L) real_obj_term_w(a, d_, ZE, ZN, v_[j], w0[j], w1[j], acc_);                    \
     }                                                                                           \
-    for (uint32_t j = 0; j < 4; ++j) v_[j] = j < clen ? v_[j] : 0.f;                            \
-    if (have) nxt[(c) * rs + q] = make_float4(v_[0], v_[1], v_[2], v_[3]);                      \
-    if (evals) {                                                                                \
-      RealAcc acc_{0.f, 0.f, 1.f};                                                              \
-      _Pragma("unroll") for (uint32_t j = 0; j < 4; ++j) {                                      \
-        const uint32_t d_ = 4 * q + j;                                                          \
-        if (d_ < L) real_obj_term_w(a, d_, v_[j] - sh[j], 0.f, v_[j], w0[j], w1[j], acc_);      \
-      }                                                                                         \
-      acc_.s0 = group_sum<GS>(acc_.s0);                                                         \
-      acc_.s1 = group_sum<GS>(acc_.s1);                                                         \
-      acc_.s2 = group_prod<GS>(acc_.s2);                                                        \
-      const float sc_ = real_obj_finish(a, acc_);                                               \
-      if (q == 0) {                                                                             \
-        a.score_next[(c)] = sc_;                                                                \
-        const unsigned long long pb_ = pack_best(sc_, (c));                                     \
-        my_best = pb_ > my_best ? pb_ : my_best;                                                \
-      }                                                                                         \
+    acc_.s0 = group_sum<GS>(acc_.s0);                                                           \
+    acc_.s1 = group_sum<GS>(acc_.s1);                                                           \
+    acc_.s2 = group_prod<GS>(acc_.s2);                                                          \
+    const float sc_ = real_obj_finish(a, acc_);                                                 \
+    if (q == 0) {                                                                               \
+      a.score_next[(c)] = sc_;                                                                  \
+      const unsigned long long pb_ = pack_best(sc_, (c));                                       \
+      my_best = pb_ > my_best ? pb_ : my_best;                                                  \
     }                                                                                           \
   }
 
+#define R_STAGE3(c, P)                                                                               \
+  if constexpr (!ROT) {                                                                              \
+    if ((c) < a.S) {                                                                                 \
+      float v_[4];                                                                                   \
+      R_VARY(c, P)                                                                                   \
+      if (evals) R_EVAL(c, v_[j] - sh[j], 0.f)                                                       \
+    }                                                                                                \
+  } else { /* wave-uniform: every lane joins the rotation tile */                                    \
+    float v_[4] = {0.f, 0.f, 0.f, 0.f};                                                              \
+    const bool live_ = (c) < a.S;                                                                    \
+    if (live_) {                                                                                     \
+      R_VARY(c, P)                                                                                   \
+    }                                                                                                \
+    float z_[4], zn_[4];                                                                             \
+    _Pragma("unroll") for (uint32_t j = 0; j < 4; ++j) z_[j] = 4 * q + j < L ? v_[j] - sh[j] : 0.f;  \
+    rot_tile4<GS>(xw, ms, z_);                                                                       \
+    zn_[0] = z_[1];                                                                                  \
+    zn_[1] = z_[2];                                                                                  \
+    zn_[2] = z_[3];                                                                                  \
+    zn_[3] = OBJ == OBJ_ROSENBROCK ? __shfl(z_[0], (int)lane + 1, 64) : 0.f;                         \
+    if (live_) R_EVAL(c, z_[j], zn_[j])                                                              \
+  }
+
+  // ROT: a wave stays in the loop while any of its groups has a child left
+#define R_MORE(c) (ROT ? __any((c) < a.S) != 0 : (c) < a.S)
   R_STAGE1(c0, X)
   R_STAGE2(c0, X)
   R_STAGE1(c0 + stride, Y)
-  while (c0 < a.S) {  // group-uniform
+  while (R_MORE(c0)) {  // group-uniform (ROT: wave-uniform)
     R_STAGE1(c0 + 2 * stride, Z)
     R_STAGE2(c0 + stride, Y)
     R_STAGE3(c0, X)
     c0 += stride;
-    if (c0 >= a.S) break;
+    if (!R_MORE(c0)) break;
     R_STAGE1(c0 + 2 * stride, X)
     R_STAGE2(c0 + stride, Z)
     R_STAGE3(c0, Y)
     c0 += stride;
-    if (c0 >= a.S) break;
+    if (!R_MORE(c0)) break;
     R_STAGE1(c0 + 2 * stride, Y)
     R_STAGE2(c0 + stride, X)
     R_STAGE3(c0, Z)
     c0 += stride;
   }
 #undef R_STAGE1
+#undef R_MORE
 #undef R_STAGE2
 #undef R_STAGE3
+#undef R_VARY
+#undef R_EVAL
 
   if (evals && best_parts) {
     unsigned long long b = block_max_u64(my_best, lds_red);
@@ -770,6 +866,24 @@ bool real_pipe_enabled() {
 
 template <int GS, bool ROT>
 uint32_t launch_fast(const GenArgs& a, unsigned long long* parts, hipStream_t s) {
+  if constexpr (ROT && (GS == 4 || GS == 8)) {
+    if (real_pipe_enabled()) {
+      static bool c[6] = {false, false, false, false, false, false};
+      switch (a.objective) {
+        case OBJ_SPHERE: return launch_occ(real_gen_pipe<GS, OBJ_SPHERE, true>, kBlock / GS, 0, a, parts, s, c[0]);
+        case OBJ_RASTRIGIN:
+          return launch_occ(real_gen_pipe<GS, OBJ_RASTRIGIN, true>, kBlock / GS, 0, a, parts, s, c[1]);
+        case OBJ_ROSENBROCK:
+          return launch_occ(real_gen_pipe<GS, OBJ_ROSENBROCK, true>, kBlock / GS, 0, a, parts, s, c[2]);
+        case OBJ_ACKLEY: return launch_occ(real_gen_pipe<GS, OBJ_ACKLEY, true>, kBlock / GS, 0, a, parts, s, c[3]);
+        case OBJ_GRIEWANK:
+          return launch_occ(real_gen_pipe<GS, OBJ_GRIEWANK, true>, kBlock / GS, 0, a, parts, s, c[4]);
+        case OBJ_SCHWEFEL:
+          return launch_occ(real_gen_pipe<GS, OBJ_SCHWEFEL, true>, kBlock / GS, 0, a, parts, s, c[5]);
+        default: break;
+      }
+    }
+  }
   if (!ROT && real_pipe_enabled()) {
     static bool c[8] = {false, false, false, false, false, false, false, false};
     switch (a.objective) {

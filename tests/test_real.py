@@ -21,6 +21,12 @@ PROBLEMS = {
     "tsp_rk": lambda: M.RandomKeyTSP.planted(40),
     "sphere_d3": lambda: M.Sphere(3, rotate=True),
     "sphere_d128": lambda: M.Sphere(128, rotate=True),
+    # wave-local MFMA rotation in the pipelined kernel: 16 (GS 4) and 32 (GS 8) padded dims
+    "rastrigin_rot16": lambda: M.Rastrigin(16, rotate=True, shift=True, seed=5),
+    "rastrigin_rot11": lambda: M.Rastrigin(11, rotate=True, seed=6),
+    "ackley_rot20": lambda: M.Ackley(20, rotate=True, shift=True, seed=7),
+    "rosenbrock_rot24": lambda: M.Rosenbrock(24, rotate=True, seed=8),
+    "griewank_rot32": lambda: M.Griewank(32, rotate=True, seed=9),
 }
 
 
