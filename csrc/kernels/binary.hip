@@ -264,6 +264,12 @@ constexpr int XOK_UNIFORM = 0, XOK_RANGE = 1;  // crossover kind template values
 
 // Diagnostic ablation switches (bench/micro/ablate builds only, see
 // bench/micro/README.md; the shipped build defines none of them).
+// Waves per SIMD the pipelined kernel is register-limited to.  Measured: a
+// fourth register set (rows of c+1 AND c+2 in flight) at 5 or 4 waves/SIMD
+// ran 96.8 / 97.9 us/gen against 92.4 for three sets at 6 waves (headline).
+#ifndef PGA_PIPE_WAVES
+#define PGA_PIPE_WAVES 6
+#endif
 #ifndef PGA_ABL
 #define PGA_ABL 0
 #endif
@@ -300,7 +306,7 @@ __device__ unsigned long long g_stamps[2 * 65536];
 // RESET: the per-individual reset mutation is possible (otherwise only
 // bit-flip / none, and the pool words are dead after stage 2: fewer VGPRs)
 template <int GS, int OBJ, int XOK, bool KEY, bool RESET>
-__global__ __launch_bounds__(kBlock, RESET ? 5 : 6) void binary_gen_pipe(GenArgs a, unsigned long long* best_parts) {
+__global__ __launch_bounds__(kBlock, RESET ? PGA_PIPE_WAVES - 1 : PGA_PIPE_WAVES) void binary_gen_pipe(GenArgs a, unsigned long long* best_parts) {
   resolve_gen(a);
   __shared__ unsigned long long lds_red[kBlock / 64];
   __shared__ uint32_t lds_elite;
