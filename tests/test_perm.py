@@ -55,10 +55,11 @@ def test_tsp_circle_converges():
 @pytest.mark.parametrize("xo", ["ox", "pmx"])
 @pytest.mark.parametrize("n,S", [(9, 333), (64, 1000), (256, 2048), (1000, 64)])
 @pytest.mark.parametrize("prob", ["matrix", "euc", "open"])
-def test_gpu_bitexact(xo, n, S, prob):
+@pytest.mark.parametrize("elitism", [1, 2])  # 1: device argmax elite; 2: elite index list
+def test_gpu_bitexact(xo, n, S, prob, elitism):
     p = {"matrix": lambda: M.TSP.random_euclidean(n, seed=2), "euc": lambda: M.TSPEuclidean.random(n, seed=2),
          "open": lambda: M.TSP.random_euclidean(n, seed=2, open_path=True)}[prob]()
-    kw = dict(seed=5, crossover=xo, mutation="inversion", mutation_rate=0.4, elitism=2)
+    kw = dict(seed=5, crossover=xo, mutation="inversion", mutation_rate=0.4, elitism=elitism)
     g = pga.GeneticAlgorithm(p, S, device="cuda:0", **kw)
     c = pga.GeneticAlgorithm(p, S, device="cpu", **kw)
     for _ in range(3):
