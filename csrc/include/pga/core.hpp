@@ -351,7 +351,14 @@ PGA_HD u32x4 chunk_flip_mask(const GenArgs& a, uint64_t child, uint32_t c, uint3
       case 2: m.z ^= bit; break;
       default: m.w ^= bit; break;
     }
-    pos += 1u + geom_skip(mut_skip_word(r0, n++), thr, kMutCap, a.mut_inv_log2_1mp);
+    // the next flip lands in this chunk iff skip(h) < rem; skip(h) >= rem
+    // <=> h < thr[rem] (1-indexed): one table read decides the common "no
+    // second flip" case without the log-seeded search (same result)
+    const uint32_t rem = clen - pos - 1u;
+    if (rem == 0u) break;
+    const uint32_t h = mut_skip_word(r0, n++);
+    if (h < thr[rem - 1u]) break;
+    pos += 1u + geom_skip(h, thr, kMutCap, a.mut_inv_log2_1mp);
   }
   return m;
 }
