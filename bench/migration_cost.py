@@ -49,7 +49,7 @@ def main():
     print(json.dumps(res))
 
 
-if __name__ == "__main__" and not os.environ.get("PGA_LOOPBACK"):
+if __name__ == "__main__" and not os.environ.get("PGA_LOOPBACK") and not os.environ.get("PGA_RCCL_SELF"):
     main()
 
 
@@ -72,10 +72,8 @@ def loopback_overhead(S=1 << 20, every=10, gens=200):
     out = {}
     for side in (False, True):
         ga = pga.GeneticAlgorithm(pga.models.OneMax(1024), S, seed=1, device="cuda:0", elitism=1)
-        m = IslandModel(ga, migrate_every=every, migrate_pct=0.01)
+        m = IslandModel(ga, migrate_every=every, migrate_pct=0.01, side_stream=side)
         m.world, m.rank = 2, 0
-        if not side:
-            m._side = None
         m.run(20)
         torch.cuda.synchronize()
         a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -90,3 +88,43 @@ def loopback_overhead(S=1 << 20, every=10, gens=200):
 
 if __name__ == "__main__" and os.environ.get("PGA_LOOPBACK"):
     loopback_overhead()
+
+
+def rccl_self_overhead(S=1 << 20, every=10, gens=500):
+    """us/gen of the headline island with and without migration, where the
+    migration runs the REAL RCCL path (backend nccl, world 1, grouped
+    ncclSend/ncclRecv to self) on one GPU: everything the driver's N>1 runs
+    pay per GPU except the xGMI wire time."""
+    import torch.distributed as dist
+    from libpga_amd.parallel import IslandModel
+
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ.setdefault("MASTER_PORT", "29517")
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    out = {}
+    for name, ev, side in (("none", 0, True), ("rccl_self", every, True), ("rccl_self_noside", every, False)):
+        ga = pga.GeneticAlgorithm(pga.models.OneMax(1024), S, seed=1, device="cuda:0", elitism=1)
+        m = IslandModel(ga, migrate_every=ev, migrate_pct=0.01, side_stream=side)
+        m.world, m.rank = 2, 0
+        m._peers = lambda: (0, 0)
+        m.connect() if ev else None
+        m.run(50)
+        torch.cuda.synchronize()
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        m.run(gens)
+        m.flush()
+        b.record()
+        b.synchronize()
+        out["us_per_gen_" + name] = a.elapsed_time(b) / gens * 1e3
+        out["migrations_" + name] = m.migrations
+    for v in ("rccl_self", "rccl_self_noside"):
+        out["overhead_pct_" + v] = 100.0 * (out["us_per_gen_" + v] / out["us_per_gen_none"] - 1.0)
+    out.update(pop=S, every=every)
+    print(json.dumps(out))
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__" and os.environ.get("PGA_RCCL_SELF"):
+    rccl_self_overhead()

@@ -334,14 +334,48 @@ __global__ __launch_bounds__(kBlock) void topk_digit_kernel(TopkState* st, uint3
 
 // ---- integer objectives: the u16 keys take at most R = L + 1 values, so one
 // LDS histogram of R bins replaces the radix passes ----
+// 16 consecutive u16 keys [c0, c0+16) clipped to `end`: two dwordx4 loads
+// issued together when the chunk is whole and aligned (c0 % 8 == 0), else
+// per-key loads; bit e of the result marks key e valid
+__device__ __forceinline__ uint32_t load_keys16(const uint16_t* k16, uint64_t c0, uint64_t end, uint32_t (&kv)[16]) {
+  if (c0 + 16 <= end && (c0 & 7) == 0) {
+    const uint4 a = *(const uint4*)(k16 + c0), b = *(const uint4*)(k16 + c0 + 8);
+    const uint32_t w[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      kv[2 * e] = w[e] & 0xFFFFu;
+      kv[2 * e + 1] = w[e] >> 16;
+    }
+    return 0xFFFFu;
+  }
+  uint32_t m = 0;
+#pragma unroll
+  for (int e = 0; e < 16; ++e) {
+    const bool ok = c0 + e < end;
+    kv[e] = ok ? k16[c0 + e] : 0u;
+    m |= ok ? (1u << e) : 0u;
+  }
+  return m;
+}
+
 __global__ __launch_bounds__(kBlock) void topk16_hist_kernel(const uint16_t* k16, uint64_t S, uint32_t R, bool largest,
-                                                             uint32_t* G) {
+                                                             uint32_t* G, uint64_t* status, uint32_t n_status) {
   extern __shared__ uint32_t hr[];
+  // aggregate words and ticket counters of the topk16_select_kernel that follows
+  for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < n_status; i += gridDim.x * kBlock) status[i] = 0;
+  if (status && blockIdx.x == 0 && threadIdx.x < 2) ((uint32_t*)(status + n_status))[threadIdx.x] = 0;
   for (uint32_t i = threadIdx.x; i < R; i += kBlock) hr[i] = 0;
   __syncthreads();
-  for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < S; i += (uint64_t)gridDim.x * kBlock) {
-    const uint32_t v = min((uint32_t)k16[i], R - 1);
-    atomicAdd(&hr[largest ? v : R - 1 - v], 1u);
+  // 16 keys per thread per pass (coalesced 32-byte chunks)
+  for (uint64_t c0 = ((uint64_t)blockIdx.x * kBlock + threadIdx.x) * 16; c0 < S;
+       c0 += (uint64_t)gridDim.x * kBlock * 16) {
+    uint32_t kv[16];
+    const uint32_t m = load_keys16(k16, c0, S, kv);
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const uint32_t v = min(kv[e], R - 1);
+      if ((m >> e) & 1u) atomicAdd(&hr[largest ? v : R - 1 - v], 1u);
+    }
   }
   __syncthreads();
   for (uint32_t i = threadIdx.x; i < R; i += kBlock)
@@ -486,6 +520,123 @@ __global__ __launch_bounds__(kBlock) void topk_offsets_kernel(uint32_t* cnt, uin
     oe += e[j];
   }
   if (threadIdx.x == 0) cnt[2 * n] = tg;  // total strictly greater
+}
+
+// ---- integer objectives, one launch after the histogram: threshold, count,
+// block offsets and the ordered write ----
+// Each block takes a ticket (its position in dispatch order) and owns the
+// ticket-th contiguous range; each thread owns a contiguous sub-range, so one
+// block scan of the per-thread counts orders the block.  The block publishes
+// its aggregate (flag | gt | eq) and then reads the aggregates of ALL its
+// predecessors in parallel (one word per thread, no look-back chain): a
+// predecessor by ticket is already dispatched and publishes without waiting
+// on anyone, so every wait ends.  The words carry all the data, so relaxed
+// agent-scope atomics suffice.  The last block to have read the histogram
+// re-zeroes it; topk16_hist_kernel zeroes the words and the tickets before
+// every selection.  Same result as count -> offsets -> write (population
+// order: the strictly-beyond-threshold keys, then the first ties).
+constexpr uint64_t kLbAgg = 1ull << 62, kLbMask31 = 0x7FFFFFFFull;
+
+__global__ __launch_bounds__(kBlock) void topk16_select_kernel(const uint16_t* k16, uint64_t S, uint64_t per_block,
+                                                               uint32_t R, bool largest, uint32_t k, uint32_t* G,
+                                                               uint64_t* status, uint32_t* ctr, uint32_t nblocks,
+                                                               uint32_t* idx_out) {
+  __shared__ uint32_t part[kBlock];
+  __shared__ uint32_t sh_T, sh_need, sh_b;
+  __shared__ bool sh_last;
+  __shared__ uint32_t lds[kBlock / 64];
+  if (threadIdx.x == 0) sh_b = atomicAdd(&ctr[0], 1u);
+  // threshold bin (as topk16_count_kernel)
+  const uint32_t per = (R + kBlock - 1) / kBlock;
+  uint32_t mine = 0;
+  for (uint32_t j = 0; j < per; ++j) {
+    const int64_t b = (int64_t)R - 1 - (int64_t)threadIdx.x * per - j;
+    if (b >= 0) mine += G[b];
+  }
+  part[threadIdx.x] = mine;
+  __syncthreads();
+  for (uint32_t o = 1; o < kBlock; o <<= 1) {
+    const uint32_t v = threadIdx.x >= o ? part[threadIdx.x - o] : 0u;
+    __syncthreads();
+    part[threadIdx.x] += v;
+    __syncthreads();
+  }
+  const uint32_t before = threadIdx.x ? part[threadIdx.x - 1] : 0u;
+  if (before < k && part[threadIdx.x] >= k) {
+    uint32_t acc = before;
+    for (uint32_t j = 0; j < per; ++j) {
+      const int64_t b = (int64_t)R - 1 - (int64_t)threadIdx.x * per - j;
+      if (b < 0) break;
+      const uint32_t c = G[b];
+      if (acc + c >= k) {
+        sh_T = (uint32_t)b;
+        sh_need = k - acc;
+        break;
+      }
+      acc += c;
+    }
+  }
+  __syncthreads();  // every read of G of this block is done
+  if (threadIdx.x == 0) sh_last = atomicAdd(&ctr[1], 1u) == nblocks - 1;
+  __syncthreads();
+  if (sh_last)  // every block has read the histogram: zero it for the next selection
+    for (uint32_t i = threadIdx.x; i < R; i += kBlock) G[i] = 0;
+  const uint32_t T = largest ? sh_T : sh_T + 0x10000u - R;
+  const uint32_t need_eq = sh_need, gt_total = k - sh_need;
+  const uint32_t b = sh_b;
+  const uint64_t pt = ((per_block + kBlock - 1) / kBlock + 15) / 16 * 16;  // keys per thread, whole 16-key chunks
+  const uint64_t blo = (uint64_t)b * per_block;
+  const uint64_t bhi = blo + per_block < S ? blo + per_block : S;
+  const uint64_t t0 = blo + threadIdx.x * pt;
+  const uint64_t t1 = t0 + pt < bhi ? t0 + pt : bhi;
+  const uint32_t flip = largest ? 0u : 0xFFFFu;  // keys(i) = v ^ flip = TopkKeys<16>
+  uint32_t gt = 0, eq = 0;
+  for (uint64_t c0 = t0; c0 < t1; c0 += 16) {
+    uint32_t kv[16];
+    const uint32_t m = load_keys16(k16, c0, t1, kv);
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const uint32_t key = kv[e] ^ flip;
+      gt += ((m >> e) & 1u) && key > T;
+      eq += ((m >> e) & 1u) && key == T;
+    }
+  }
+  uint32_t bg, be;
+  uint32_t og = block_excl_scan_u(gt, lds, bg);
+  __syncthreads();
+  uint32_t oe = block_excl_scan_u(eq, lds, be);
+  if (threadIdx.x == 0)
+    __hip_atomic_store(&status[b], kLbAgg | ((uint64_t)bg << 31) | (uint64_t)be, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+  // block prefix = sum of the predecessors' aggregates, read in parallel
+  uint32_t pg = 0, pe = 0;
+  for (uint32_t j = threadIdx.x; j < b; j += kBlock) {
+    uint64_t w = 0;
+    for (uint32_t spins = 0; spins < (1u << 26); ++spins) {  // bound: never hang the device
+      w = __hip_atomic_load(&status[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (w) break;
+    }
+    pg += (uint32_t)((w >> 31) & kLbMask31);
+    pe += (uint32_t)(w & kLbMask31);
+  }
+  auto add = [](uint32_t x, uint32_t y) { return x + y; };
+  pg = block_reduce(pg, lds, add);
+  pe = block_reduce(pe, lds, add);
+  uint32_t gpos = pg + og, epos = pe + oe;
+  for (uint64_t c0 = t0; c0 < t1; c0 += 16) {
+    uint32_t kv[16];
+    const uint32_t m = load_keys16(k16, c0, t1, kv);
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      if (!((m >> e) & 1u)) continue;
+      const uint32_t key = kv[e] ^ flip;
+      if (key > T) idx_out[gpos++] = (uint32_t)(c0 + e);
+      if (key == T) {
+        if (epos < need_eq) idx_out[gt_total + epos] = (uint32_t)(c0 + e);
+        ++epos;
+      }
+    }
+  }
 }
 
 template <int BITS>
@@ -677,7 +828,7 @@ size_t topk_workspace_bytes(uint64_t S, uint32_t k) {
                                                              (uint32_t*)nullptr, (int)k));
   (void)S;
   // layout: state | counts | 3 k-arrays | cub temp | value histogram (kept zeroed)
-  return align_up(sizeof(TopkState)) + align_up(sizeof(uint32_t) * (2 * 1024 + 1)) + 3 * align_up(4ull * k) +
+  return align_up(sizeof(TopkState)) + align_up(sizeof(uint32_t) * (2 * 1024 + 4)) + 3 * align_up(4ull * k) +
          align_up(cub_bytes) + align_up(4ull * kTopkMaxRange);
 }
 
@@ -688,7 +839,7 @@ void topk_run(TopkKeys<BITS> keys, uint64_t S, uint32_t k, bool sorted, uint32_t
   TopkState* st = (TopkState*)p;
   p += align_up(sizeof(TopkState));
   uint32_t* cnt = (uint32_t*)p;
-  p += align_up(sizeof(uint32_t) * (2 * 1024 + 1));
+  p += align_up(sizeof(uint32_t) * (2 * 1024 + 4));
   uint32_t* keys_buf = (uint32_t*)p;
   p += align_up(4ull * k);
   uint32_t* keys_sorted = (uint32_t*)p;
@@ -726,6 +877,15 @@ void topk_run(TopkKeys<BITS> keys, uint64_t S, uint32_t k, bool sorted, uint32_t
 }
 }  // namespace
 
+bool topk_fused_enabled() {  // PGA_TOPK_FUSED=0: the 4-kernel path (A/B)
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("PGA_TOPK_FUSED");
+    v = (e && e[0] == '0') ? 0 : 1;
+  }
+  return v == 1;
+}
+
 void topk_launch(const float* scores, const uint16_t* keys16, uint32_t key_range, uint64_t S, uint32_t k,
                  bool largest, bool sorted, uint32_t* idx_out, void* ws, hipStream_t s) {
   if (k == 0) return;
@@ -736,7 +896,7 @@ void topk_launch(const float* scores, const uint16_t* keys16, uint32_t key_range
     TopkState* st = (TopkState*)p;
     p += align_up(sizeof(TopkState));
     uint32_t* cnt = (uint32_t*)p;
-    p += align_up(sizeof(uint32_t) * (2 * 1024 + 1));
+    p += align_up(sizeof(uint32_t) * (2 * 1024 + 4));
     p += 3 * align_up(4ull * k);
     size_t cub_bytes = 0;
     PGA_HIP_CHECK(hipcub::DeviceRadixSort::SortPairsDescending(nullptr, cub_bytes, (uint32_t*)nullptr,
@@ -746,9 +906,18 @@ void topk_launch(const float* scores, const uint16_t* keys16, uint32_t key_range
     uint32_t* G = (uint32_t*)p;  // zero on allocation and after every use
     const uint32_t R = key_range;
     uint32_t grid = launch_grid(S, kBlock * 16);
-    hipLaunchKernelGGL(topk16_hist_kernel, grid, kBlock, 4 * R, s, keys16, S, R, largest, G);
     const uint32_t cgrid = grid > 1024 ? 1024 : grid;
     const uint64_t per_block = (S + cgrid - 1) / cgrid;
+    uint64_t* status = (uint64_t*)cnt;  // cgrid aggregate words, then 2 ticket counters
+    if (S < (1ull << 31) && topk_fused_enabled()) {
+      hipLaunchKernelGGL(topk16_hist_kernel, grid, kBlock, 4 * R, s, keys16, S, R, largest, G, status, cgrid);
+      const uint64_t pb16 = (per_block + 15) / 16 * 16;  // aligned 16-key chunks for every thread
+      hipLaunchKernelGGL(topk16_select_kernel, cgrid, kBlock, 0, s, keys16, S, pb16, R, largest, k, G, status,
+                         (uint32_t*)(status + cgrid), cgrid, idx_out);
+      PGA_HIP_CHECK(hipGetLastError());
+      return;
+    }
+    hipLaunchKernelGGL(topk16_hist_kernel, grid, kBlock, 4 * R, s, keys16, S, R, largest, G, (uint64_t*)nullptr, 0u);
     hipLaunchKernelGGL(topk16_count_kernel, cgrid, kBlock, 0, s, keys16, S, per_block, R, largest, k, G, st, cnt);
     hipLaunchKernelGGL(topk_offsets_kernel, 1, kBlock, 0, s, cnt, cgrid, G, R);
     hipLaunchKernelGGL(topk_write_kernel<16>, cgrid, kBlock, 0, s, TopkKeys<16>{scores, keys16, largest}, S,

@@ -84,6 +84,7 @@ class IslandModel:
         topology: str = "ring",
         group=None,
         overlap: bool = True,
+        side_stream: bool = False,
         seed: int = 0,
         validate: bool = True,
         timeout_s: Optional[float] = None,
@@ -119,10 +120,17 @@ class IslandModel:
         self.send = torch.empty(n, dtype=torch.int32, device=dev)
         self.recv = torch.empty(n, dtype=torch.int32, device=dev)
         self._pending = None
-        # emigrant selection + packing run on a side stream, concurrently with
-        # the next generation kernel (they only read the current generation)
-        # (not with elitism > 1: the elite top-k shares the island's selection workspace)
-        self._side = torch.cuda.Stream(dev) if dev.type == "cuda" and ga.operators.elitism <= 1 else None
+        # side_stream=True runs emigrant selection + packing on a side stream,
+        # concurrently with the next generation kernel (they only read the
+        # current generation; not with elitism > 1: the elite top-k shares the
+        # island's selection workspace).  Off by default: measured on MI355X
+        # (bench/migration_cost.py, PGA_RCCL_SELF=1, 1M x 1024-bit, every 10
+        # generations) the side stream shares the generation's hardware queue,
+        # so it overlaps nothing and adds two cross-stream waits per epoch:
+        # 11.5% vs 8.6% migration overhead.  The RCCL exchange itself still
+        # overlaps the next generation either way.
+        use_side = side_stream and dev.type == "cuda" and ga.operators.elitism <= 1
+        self._side = torch.cuda.Stream(dev) if use_side else None
         self._epoch = 0
         self.migrations = 0
         self.bytes_sent = 0

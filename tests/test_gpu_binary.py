@@ -169,3 +169,22 @@ def test_rank_selection_bitexact(sp):
     g.run(4)
     c.run(4)
     same(g, c)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("S", [1 << 20, (1 << 22) + 12345])
+def test_gpu_topk_selection_order_many_blocks(S):
+    """u16-key top-k in selection order (the migration path: histogram + one
+    fused look-back select launch) over up to 1024 blocks, repeated so the
+    histogram / ticket reset between calls is exercised: the indices with a
+    key beyond the threshold in population order, then the first ties."""
+    ga = pga.GeneticAlgorithm(pga.models.OneMax(64), S, seed=11, device=DEV)
+    sc = ga.scores.cpu()
+    for k in (10486, 1, S // 3, 10486):
+        for largest in (True, False):
+            got = ga.island.topk(k, largest, False).cpu().long()
+            key = sc if largest else -sc
+            T = key.sort(descending=True).values[k - 1]
+            gt = (key > T).nonzero().flatten()
+            eq = (key == T).nonzero().flatten()[: k - gt.numel()]
+            assert torch.equal(got, torch.cat([gt, eq])), (k, largest)

@@ -82,10 +82,8 @@ def _loopback_model(side: bool):
     from libpga_amd.parallel import IslandModel
 
     ga = pga.GeneticAlgorithm(pga.models.OneMax(512), 50_000, seed=3, device="cuda:0", elitism=1)
-    m = IslandModel(ga, migrate_every=3, migrate_pct=0.02)
+    m = IslandModel(ga, migrate_every=3, migrate_pct=0.02, side_stream=side)
     m.world, m.rank = 2, 0
-    if not side:
-        m._side = None
     return m
 
 
@@ -108,3 +106,14 @@ def test_overlapped_migration_stream_order_gpu(monkeypatch):
     torch.cuda.synchronize()
     assert a.migrations == b.migrations == 10
     assert torch.equal(a.ga.rows, b.ga.rows) and torch.equal(a.ga.scores, b.ga.scores)
+
+
+@pytest.mark.gpu
+def test_rccl_self_exchange_matches_loopback_gpu():
+    """The real RCCL migration path (backend nccl, world 1, ncclSend/ncclRecv
+    to self) gives the same island as a device-copy exchange, bit for bit."""
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    r = subprocess.run([sys.executable, os.path.join(HERE, "rccl_self_worker.py"), str(free_port())], env=env,
+                       capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    assert "rccl self-exchange ok" in r.stdout
