@@ -531,8 +531,9 @@ __global__ __launch_bounds__(kBlock) void topk_offsets_kernel(uint32_t* cnt, uin
 // predecessors in parallel (one word per thread, no look-back chain): a
 // predecessor by ticket is already dispatched and publishes without waiting
 // on anyone, so every wait ends.  The words carry all the data, so relaxed
-// agent-scope atomics suffice.  The last block to have read the histogram
-// re-zeroes it; topk16_hist_kernel zeroes the words and the tickets before
+// agent-scope atomics suffice.  The last ticket (which has seen every other
+// block's word, so every read of the histogram is done) re-zeroes the
+// histogram; topk16_hist_kernel zeroes the words and the tickets before
 // every selection.  Same result as count -> offsets -> write (population
 // order: the strictly-beyond-threshold keys, then the first ties).
 constexpr uint64_t kLbAgg = 1ull << 62, kLbMask31 = 0x7FFFFFFFull;
@@ -541,33 +542,29 @@ __global__ __launch_bounds__(kBlock) void topk16_select_kernel(const uint16_t* k
                                                                uint32_t R, bool largest, uint32_t k, uint32_t* G,
                                                                uint64_t* status, uint32_t* ctr, uint32_t nblocks,
                                                                uint32_t* idx_out) {
-  __shared__ uint32_t part[kBlock];
+  __shared__ uint32_t gl[kTopkMaxRange];  // this block's copy of the histogram
   __shared__ uint32_t sh_T, sh_need, sh_b;
-  __shared__ bool sh_last;
   __shared__ uint32_t lds[kBlock / 64];
   if (threadIdx.x == 0) sh_b = atomicAdd(&ctr[0], 1u);
-  // threshold bin (as topk16_count_kernel)
+  // threshold bin: thread t owns bins [R-1 - (t+1)*per + 1, R-1 - t*per], counted from the top
   const uint32_t per = (R + kBlock - 1) / kBlock;
   uint32_t mine = 0;
   for (uint32_t j = 0; j < per; ++j) {
     const int64_t b = (int64_t)R - 1 - (int64_t)threadIdx.x * per - j;
-    if (b >= 0) mine += G[b];
+    if (b >= 0) {
+      const uint32_t c = G[b];
+      gl[b] = c;  // re-read below by this same thread only
+      mine += c;
+    }
   }
-  part[threadIdx.x] = mine;
-  __syncthreads();
-  for (uint32_t o = 1; o < kBlock; o <<= 1) {
-    const uint32_t v = threadIdx.x >= o ? part[threadIdx.x - o] : 0u;
-    __syncthreads();
-    part[threadIdx.x] += v;
-    __syncthreads();
-  }
-  const uint32_t before = threadIdx.x ? part[threadIdx.x - 1] : 0u;
-  if (before < k && part[threadIdx.x] >= k) {
+  uint32_t tot;
+  const uint32_t before = block_excl_scan_u(mine, lds, tot);
+  if (before < k && before + mine >= k) {
     uint32_t acc = before;
     for (uint32_t j = 0; j < per; ++j) {
       const int64_t b = (int64_t)R - 1 - (int64_t)threadIdx.x * per - j;
       if (b < 0) break;
-      const uint32_t c = G[b];
+      const uint32_t c = gl[b];
       if (acc + c >= k) {
         sh_T = (uint32_t)b;
         sh_need = k - acc;
@@ -576,11 +573,7 @@ __global__ __launch_bounds__(kBlock) void topk16_select_kernel(const uint16_t* k
       acc += c;
     }
   }
-  __syncthreads();  // every read of G of this block is done
-  if (threadIdx.x == 0) sh_last = atomicAdd(&ctr[1], 1u) == nblocks - 1;
   __syncthreads();
-  if (sh_last)  // every block has read the histogram: zero it for the next selection
-    for (uint32_t i = threadIdx.x; i < R; i += kBlock) G[i] = 0;
   const uint32_t T = largest ? sh_T : sh_T + 0x10000u - R;
   const uint32_t need_eq = sh_need, gt_total = k - sh_need;
   const uint32_t b = sh_b;
@@ -622,6 +615,10 @@ __global__ __launch_bounds__(kBlock) void topk16_select_kernel(const uint16_t* k
   auto add = [](uint32_t x, uint32_t y) { return x + y; };
   pg = block_reduce(pg, lds, add);
   pe = block_reduce(pe, lds, add);
+  // every other block published its aggregate, hence had read the histogram:
+  // the last ticket zeroes it for the next selection
+  if (b == nblocks - 1)
+    for (uint32_t i = threadIdx.x; i < R; i += kBlock) G[i] = 0;
   uint32_t gpos = pg + og, epos = pe + oe;
   for (uint64_t c0 = t0; c0 < t1; c0 += 16) {
     uint32_t kv[16];
