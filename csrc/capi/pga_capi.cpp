@@ -959,6 +959,23 @@ int pga_comm_set_fault(pga_t* p, int every, int mode) {
   });
 }
 
+int pga_comm_exchange(pga_t** solvers, int count, float pct) {
+  if (!solvers || count < 1 || !solvers[0]) return -1;
+  pga_t* p0 = solvers[0];
+  return guard_r<int>(p0, -1, [&]() {
+    std::vector<pga_t*> v(solvers, solvers + count);
+    for (pga_t* p : v) {
+      if (!p || p->pops.empty()) throw std::invalid_argument("pga_comm_exchange: solver without populations");
+      if (p->comm != p0->comm) throw std::invalid_argument("pga_comm_exchange: solvers of different communicators");
+    }
+    if (p0->comm && p0->comm->size() > 1 && p0->comm->drives_all_ranks() && count != p0->comm->size())
+      throw std::invalid_argument("pga_comm_exchange: pass every rank of an InitAll / loopback group");
+    std::sort(v.begin(), v.end(), [](pga_t* a, pga_t* b) { return a->comm_rank < b->comm_rank; });
+    migrate_ranks(v, pct);
+    return 0;
+  });
+}
+
 int pga_comm_best(pga_t* p, float* score, int* rank) {
   if (!p || p->pops.empty()) return -1;
   return guard_r<int>(p, -1, [&]() {

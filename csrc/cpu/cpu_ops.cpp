@@ -99,6 +99,46 @@ void select_parents(const GenArgs& a, uint64_t child, uint32_t& pa, uint32_t& pb
 
 static inline uint32_t popc(uint32_t x) { return (uint32_t)__builtin_popcount(x); }
 
+// BINARY parent choice from the ST_SEL words (core.hpp "BINARY randomness layout")
+static void bin_select_parents(const GenArgs& a, uint64_t child, uint32_t& pa, uint32_t& pb) {
+  const uint32_t S = (uint32_t)a.S;
+  auto w = [&](uint32_t t) { return bin_sel_word(a.key, child, t); };
+  if (a.selection == SEL_TOURNAMENT) {
+    const uint32_t k = a.tour_k;
+    uint32_t best[2];
+    for (uint32_t p = 0; p < 2; ++p) {
+      uint32_t b = word_to_index(w(p * k), S);
+      float bs = a.score_cur[b];
+      for (uint32_t j = 1; j < k; ++j) {
+        uint32_t c = word_to_index(w(p * k + j), S);
+        float cs = a.score_cur[c];
+        if (bs < cs) { bs = cs; b = c; }
+      }
+      best[p] = b;
+    }
+    pa = best[0];
+    pb = best[1];
+  } else if (a.selection == SEL_ROULETTE) {
+    pa = roulette_pick(a.cumfit, S, w(0));
+    pb = roulette_pick(a.cumfit, S, w(1));
+  } else if (a.selection == SEL_RANK) {
+    pa = a.rank_order[rank_pick(w(0), w(1), w(2), S, a.rank_thresh)];
+    pb = a.rank_order[rank_pick(w(3), w(4), w(5), S, a.rank_thresh)];
+  } else {
+    pa = word_to_index(w(0), S);
+    pb = word_to_index(w(1), S);
+  }
+}
+
+// sparse bit-flip: the first K distinct positions of the mutation words
+static void sparse_positions(const GenArgs& a, uint64_t child, uint32_t K, std::vector<uint32_t>& out) {
+  out.clear();
+  for (uint32_t j = 0; out.size() < K; ++j) {
+    const uint32_t p = word_to_index(bin_mut_word(a.key, child, j), a.L);
+    if (std::find(out.begin(), out.end(), p) == out.end()) out.push_back(p);
+  }
+}
+
 uint32_t binary_run(int mode, const GenArgs& a, unsigned long long* best_parts) {
   const uint32_t GS = group_size(a.chunks);
   const uint64_t rw = a.row_words;
@@ -114,33 +154,36 @@ uint32_t binary_run(int mode, const GenArgs& a, unsigned long long* best_parts) 
   if (gen && a.n_elite > 0 && a.elite_idx == nullptr) elite0 = (uint32_t)best_index(reduce_best(a.best_cur, a.n_best_cur));
 
   unsigned long long best = 0;
-  std::vector<uint32_t> seg((size_t)GS * 4);
+  std::vector<uint32_t> seg((size_t)GS * 4), flips;
   for (uint64_t child = 0; child < a.S; ++child) {
     float score = 0.f;
-    if (gen && child < a.n_elite) {
-      const uint32_t src = a.elite_idx ? a.elite_idx[child] : elite0;
-      std::memcpy(nxt + child * rw, cur + (uint64_t)src * rw, sizeof(uint32_t) * 4 * nchunks);
-      score = a.score_cur[src];
-    } else {
+    {
+      // elitism: child = copy of the elite row, re-evaluated like every child
+      const bool elite = gen && child < a.n_elite;
       uint32_t pa = 0, pb = 0;
       bool xo = false;
       uint32_t blo = 0, bhi = 0;
-      if (gen || cross) {
-        select_parents(a, child, pa, pb);
-        xo = a.crossover != XO_NONE && do_crossover(a, pool_word(a.key, child, W_XOPROB));
+      const u32x4 misc = bin_misc(a.key, child);
+      if (elite) {
+        pa = pb = a.elite_idx ? a.elite_idx[child] : elite0;
+      } else if (gen || cross) {
+        bin_select_parents(a, child, pa, pb);
+        xo = a.crossover != XO_NONE && do_crossover(a, misc.x);
         if (a.crossover == XO_ONE_POINT) {
-          blo = word_to_index(pool_word(a.key, child, W_CUT1), L);
+          blo = word_to_index(misc.y, L);
           bhi = L;
         } else if (a.crossover == XO_TWO_POINT) {
-          uint32_t c1 = word_to_index(pool_word(a.key, child, W_CUT1), L);
-          uint32_t c2 = word_to_index(pool_word(a.key, child, W_CUT2), L);
+          uint32_t c1 = word_to_index(misc.y, L);
+          uint32_t c2 = word_to_index(misc.z, L);
           blo = std::min(c1, c2);
           bhi = std::max(c1, c2);
         }
       }
-      uint32_t rpos = 0xFFFFFFFFu;  // RESET_ONE: the one flipped bit
-      if (reset_one && pool_word(a.key, child, W_MUTIND) < a.mut_ind_thresh)
-        rpos = word_to_index(pool_word(a.key, child, W_MUTPOS), L);
+      // flipped positions: RESET_ONE (at most one) or the sparse bit-flip sampler
+      flips.clear();
+      if (reset_one && !elite && misc.w < a.mut_ind_thresh)
+        flips.push_back(word_to_index(bin_mut_word(a.key, child, 0), L));
+      if (bitflip && !elite && a.mut_sparse) sparse_positions(a, child, binom_count(misc.w, a.mut_thr), flips);
 
       // per-lane objective accumulators
       uint32_t acc_u[64] = {0};
@@ -183,12 +226,13 @@ uint32_t binary_run(int mode, const GenArgs& a, unsigned long long* best_parts) 
           const uint32_t c = c0 + q;
           if (c >= nchunks) continue;
           uint32_t* v = &seg[q * 4];
-          if (bitflip) {
+          if (bitflip && !elite && !a.mut_sparse) {
             const uint32_t clen = std::min(128u, L - c * 128u);
-            u32x4 m = chunk_flip_mask(a, child, c, clen, chunk_mut_word(a.key, child, c), a.mut_thr);
+            u32x4 m = chunk_flip_mask(a, child, c, clen, bin_chunk_mut_word(a.key, child, c), a.mut_thr);
             v[0] ^= m.x; v[1] ^= m.y; v[2] ^= m.z; v[3] ^= m.w;
-          } else if (reset_one && (rpos >> 7) == c) {
-            v[(rpos & 127u) >> 5] ^= 1u << (rpos & 31u);
+          } else {
+            for (uint32_t pos : flips)
+              if ((pos >> 7) == c) v[(pos & 127u) >> 5] ^= 1u << (pos & 31u);
           }
         }
         for (uint32_t q = 0; q < GS; ++q) {

@@ -42,12 +42,13 @@ Island::Island(const Config& cfg, int device) : cfg_(cfg), device_(device) {
   if (cfg_.island >= 65536) throw std::invalid_argument("island id must be < 65536");
   row_geometry(cfg_.encoding, cfg_.L, &row_words_, &chunks_);
   if (on_gpu()) PGA_HIP_CHECK(hipSetDevice(device_));
-  const size_t rb = 4ull * row_words_ * cfg_.S;
+  const uint64_t Sp = cfg_.S + kRowPad;  // padded (ops.hpp kRowPad)
+  const size_t rb = 4ull * row_words_ * Sp;
   for (int i = 0; i < 2; ++i) {
     rows_[i] = alloc(rb);
-    scores_[i] = alloc(4ull * cfg_.S);
+    scores_[i] = alloc(4ull * Sp);
     best_[i] = alloc(8ull * kMaxGrid);
-    keys_[i] = alloc(2ull * cfg_.S);
+    keys_[i] = alloc(2ull * Sp);
   }
   out_best_ = alloc(64);
   stats_ = alloc(4ull * (4 + 3 * 1024));
@@ -136,6 +137,8 @@ void Island::rebuild_mut_table() {
   if (mut_rate_eff_ > 1.f) mut_rate_eff_ = 1.f;
   std::vector<uint32_t> thr(kMutCap);
   build_mut_table(per_ind ? 0.f : mut_rate_eff_, kMutCap, thr.data(), &mut_inv_);
+  mut_sparse_ = cfg_.encoding == ENC_BINARY && cfg_.mutation == MUT_BIT_FLIP && bin_sparse_mutation(cfg_.L, mut_rate_eff_);
+  if (mut_sparse_) build_binom_table(mut_rate_eff_, cfg_.L, thr.data());
   if (!mut_thr_.ptr) mut_thr_ = alloc(4ull * kMutCap);
   if (on_gpu()) synchronize();
   copy_to_device(mut_thr_.ptr, thr.data(), 4ull * kMutCap);
@@ -245,6 +248,7 @@ GenArgs Island::make_args(int mode) {
   a.mut_ind_thresh = per_individual_mutation(cfg_.mutation) ? prob_thresh(mut_rate_eff_) : 0u;
   a.mut_thr = (const uint32_t*)mut_thr_.ptr;
   a.mut_inv_log2_1mp = mut_inv_;
+  a.mut_sparse = mut_sparse_ ? 1u : 0u;
   a.sigma = cfg_.sigma;
   a.lo = cfg_.lo;
   a.hi = cfg_.hi;

@@ -98,6 +98,8 @@ enum Stream : uint32_t {
   ST_MIGRATE = 5,  // migration pairing / victim choice
   ST_COMPAT = 6,   // reference-ABI rand slices handed to user callbacks
   ST_PERM = 7,     // permutation crossover helpers
+  ST_SEL = 8,      // BINARY: selection words, 4 per block
+  ST_BMUT = 9,     // BINARY: mutation words (positions, per-chunk geometric draws)
 };
 
 // Per-child randomness (stream ST_CHILD, one Philox block b per index):
@@ -128,7 +130,14 @@ PGA_HD void mulhilo32(uint32_t a, uint32_t b, uint32_t& hi, uint32_t& lo) {
   lo = (uint32_t)p;
 }
 
+// NH ("no hoist"): the key words pass through an empty asm, so the compiler
+// cannot precompute the 20 round keys of a loop-invariant key outside a
+// loop (20 SGPRs pinned for the whole loop); the hot BINARY kernel uses it.
+template <bool NH = false>
 PGA_HD u32x4 philox4x32_10(u32x4 c, uint32_t k0, uint32_t k1) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  if (NH) asm volatile("" : "+s"(k0), "+s"(k1));
+#endif
 #pragma unroll
   for (int r = 0; r < 10; ++r) {
     uint32_t hi0, lo0, hi1, lo1;
@@ -147,10 +156,11 @@ struct RngKey {
   uint32_t island;     // island id (< 65536)
 };
 
+template <bool NH = false>
 PGA_HD u32x4 draw(const RngKey& key, uint32_t stream, uint64_t ind, uint32_t block) {
   u32x4 c{(block & 0x00FFFFFFu) | (stream << 24), (uint32_t)ind,
           (uint32_t)(ind >> 32) | (key.island << 16), key.gen};
-  return philox4x32_10(c, key.k0, key.k1);
+  return philox4x32_10<NH>(c, key.k0, key.k1);
 }
 
 // by value + value selects: a select over field REFERENCES becomes a select of
@@ -310,6 +320,10 @@ struct GenArgs {
   // generations can be replayed without re-recording kernel arguments
   const uint32_t* gen_dev;
   uint32_t gen_off;
+
+  // BINARY bit-flip: 1 = sparse sampler (mut_thr is the Binomial CDF table),
+  // 0 = per-chunk geometric skips (mut_thr is the geometric table)
+  uint32_t mut_sparse;
 };
 
 PGA_HD uint32_t sel_words(const GenArgs& a) {
@@ -364,6 +378,55 @@ PGA_HD u32x4 chunk_flip_mask(const GenArgs& a, uint64_t child, uint32_t c, uint3
 }
 
 PGA_HD bool do_crossover(const GenArgs& a, uint32_t w0) { return a.xo_always || w0 < a.xo_thresh_hi; }
+
+// ------------------------------------------------- BINARY randomness layout ---
+// The BINARY encoding draws per child (REAL / PERMUTATION keep the ST_CHILD
+// word pool above):
+//   selection word t      = register t%4 of block t/4 of stream ST_SEL
+//   misc block            = block 0 of ST_CHILD: .x crossover test, .y/.z cut
+//                           points, .w mutation word (bit-flip count K in the
+//                           sparse regime, the per-individual test for RESET_ONE)
+//   mutation word j       = register j%4 of block j/4 of ST_BMUT
+//   dense chunk draw of c = register .x of block kDenseBlock + c of ST_BMUT
+//   crossover mask        = block c of ST_XO (128 bits per chunk)
+// so one Philox block yields all four contestants of a binary tournament and
+// the kernel can run the tournaments of 64 children with one lane each.
+//
+// Bit-flip mutation (rate p per bit) has two exact samplers, chosen by L and p:
+//   sparse (L <= kSparseMaxL, L*p <= kSparseMaxMean): K ~ Binomial(L, p) by
+//     inverse CDF of the misc word (mut_thr holds the CDF table), then the
+//     first K distinct values of word_to_index(mutation word j, L), j = 0,1,..
+//     (a uniform K-subset: together, independent Bernoulli(p) bits).
+//   dense: per 128-bit chunk, geometric skips from the dense chunk draw
+//     (chunk_flip_mask, mut_thr holds the geometric table).
+constexpr uint32_t kSparseMaxL = 8192;
+constexpr float kSparseMaxMean = 1.5f;
+constexpr uint32_t kDenseBlock = 0x400000u;  // well above any sparse word block
+constexpr uint32_t kRecPos = 8;              // positions a kernel carries per child record
+
+PGA_HD bool bin_sparse_mutation(uint32_t L, float p) {
+  return L <= kSparseMaxL && p > 0.f && (double)L * (double)p <= (double)kSparseMaxMean;
+}
+PGA_HD uint32_t bin_sel_word(const RngKey& key, uint64_t child, uint32_t t) {
+  return sel4(draw(key, ST_SEL, child, t >> 2), t & 3u);
+}
+template <bool NH = false>
+PGA_HD u32x4 bin_misc(const RngKey& key, uint64_t child) { return draw<NH>(key, ST_CHILD, child, 0); }
+template <bool NH = false>
+PGA_HD uint32_t bin_mut_word(const RngKey& key, uint64_t child, uint32_t j) {
+  return sel4(draw<NH>(key, ST_BMUT, child, j >> 2), j & 3u);
+}
+template <bool NH = false>
+PGA_HD uint32_t bin_chunk_mut_word(const RngKey& key, uint64_t child, uint32_t c) {
+  return draw<NH>(key, ST_BMUT, child, kDenseBlock + c).x;
+}
+// sparse regime: number of flips from the misc word (thr = CDF table;
+// entries of 0xFFFFFFFF end the table)
+PGA_HD uint32_t binom_count(uint32_t w, const uint32_t* thr) {
+  uint32_t k = 0;
+  while (k < kMutCap && thr[k] != 0xFFFFFFFFu && w >= thr[k]) ++k;
+  return k;
+}
 
 // bits of the 32-bit word starting at bit `base` that fall in [lo, hi)
 PGA_HD uint32_t range_mask32(uint32_t base, uint32_t lo, uint32_t hi) {

@@ -166,6 +166,7 @@ class Island {
   void prepare_objective();      // derived objective data (QUBO packing)
   size_t obj_len_[2] = {0, 0};
   float mut_inv_ = 0.f;
+  bool mut_sparse_ = false;  // BINARY bit-flip uses the sparse (Binomial) sampler
   float mut_rate_eff_ = 0.f;
   void* user_fn_ = nullptr;
   void* user_xo_fn_ = nullptr;

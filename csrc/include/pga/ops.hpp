@@ -27,6 +27,10 @@ namespace pga {
 // Max blocks of a persistent grid-stride launch; per-block best arrays must
 // hold at least this many entries.
 constexpr uint32_t kMaxGrid = 8192;
+// Population buffers (rows, scores, tournament keys) carry kRowPad spare
+// entries past S: the fast BINARY kernel's last wave writes its tail there
+// instead of predicating its stores.
+constexpr uint32_t kRowPad = 64;
 
 // grid for `S` work items processed `per_block` at a time: min(ceil, 8*CUs)
 uint32_t launch_grid(uint64_t S, uint32_t per_block);
@@ -112,5 +116,7 @@ void scatter_rows_launch(void* rows, float* scores, uint32_t row_words, const ui
 
 // mutation threshold table for geometric skips: thr[m-1] = floor((1-p)^m 2^32), m = 1..L
 void build_mut_table(float p, uint32_t L, uint32_t* host_out, float* inv_log2_1mp);
+// sparse BINARY bit-flip: kMutCap-entry Binomial(L, p) CDF table (binom_count)
+void build_binom_table(float p, uint32_t L, uint32_t* host_out);
 
 }  // namespace pga

@@ -10,23 +10,18 @@
 //     -> child store + score store + per-block best
 // replacing the reference's RNG-fill + 3 kernels x ceil(S/512) launches + 3
 // device syncs per generation (src/pga.cu:376-391, :250-347).  No random
-// buffer is materialised: every draw is an in-register Philox4x32-10.
-//
-// Grid: persistent grid-stride over individuals, sized from the kernel's
-// measured occupancy (no partial second wave); a block's children are
-// contiguous so its stores are contiguous.  Parents are random rows, so there
-// is no inter-block reuse to make XCD-aware (guide §5.5 T1 transfers only to
-// neighbour-tile reuse).
+// buffer is materialised: every draw is an in-register Philox4x32-10 (the
+// BINARY randomness layout is defined in core.hpp).
 //
 // Two kernels:
-//   binary_kernel<GS,OBJ,MODE>   every mode / operator; one child at a time
-//   binary_gen_pipe<GS,OBJ,XO>   the hot generation path, software-pipelined
-//                                three children deep (see below)
+//   binary_kernel<GS,OBJ,MODE>   every mode / operator / genome length; one
+//                                child per group at a time
+//   binary_gen_tp<GS,OBJ,XO,KEY> the hot generation path (L <= 8192 bits,
+//                                tournament-2 or random selection), see below
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
 #include <cstdio>
-#include <vector>
 
 #include "pga/device.hpp"
 #include "pga/ops.hpp"
@@ -35,16 +30,6 @@ namespace pga {
 namespace {
 
 using namespace dev;
-
-// PGA_PIPELINE=0 forces the generic GEN kernel (A/B testing)
-bool getenv_pipeline() {
-  static int v = -1;
-  if (v < 0) {
-    const char* e = getenv("PGA_PIPELINE");
-    v = (e && e[0] == '0') ? 0 : 1;
-  }
-  return v == 1;
-}
 
 // per-lane objective accumulator over the chunks a lane owns
 template <int OBJ>
@@ -132,6 +117,106 @@ __device__ __forceinline__ uint32_t chunk_len(uint32_t L, uint32_t c) {
   return L - b >= 128u ? 128u : L - b;
 }
 
+// Parents of `child` from the ST_SEL words; group-uniform (every lane of the
+// group computes the same).  Mirrors cpu_ops.cpp bin_select_parents.
+__device__ __forceinline__ void bin_select(const GenArgs& a, uint64_t child, uint32_t& pa, uint32_t& pb) {
+  const uint32_t S = (uint32_t)a.S;
+  u32x4 blk = draw(a.key, ST_SEL, child, 0);
+  if (a.selection == SEL_TOURNAMENT && a.tour_k == 2) {
+    const uint32_t i0 = word_to_index(blk.x, S), i1 = word_to_index(blk.y, S);
+    const uint32_t i2 = word_to_index(blk.z, S), i3 = word_to_index(blk.w, S);
+    const float s0 = a.score_cur[i0], s1 = a.score_cur[i1], s2 = a.score_cur[i2], s3 = a.score_cur[i3];
+    pa = (s0 < s1) ? i1 : i0;
+    pb = (s2 < s3) ? i3 : i2;
+  } else if (a.selection == SEL_TOURNAMENT) {
+    const uint32_t k = a.tour_k;
+    uint32_t cb = 0, best[2];
+    for (uint32_t p = 0; p < 2; ++p) {
+      uint32_t b = 0;
+      float bs = 0.f;
+      for (uint32_t j = 0; j < k; ++j) {
+        const uint32_t t = p * k + j;
+        if ((t >> 2) != cb) {
+          cb = t >> 2;
+          blk = draw(a.key, ST_SEL, child, cb);
+        }
+        const uint32_t c = word_to_index(sel4(blk, t & 3u), S);
+        const float cs = a.score_cur[c];
+        if (j == 0 || bs < cs) {
+          bs = cs;
+          b = c;
+        }
+      }
+      best[p] = b;
+    }
+    pa = best[0];
+    pb = best[1];
+  } else if (a.selection == SEL_ROULETTE) {
+    pa = roulette_pick(a.cumfit, S, blk.x);
+    pb = roulette_pick(a.cumfit, S, blk.y);
+  } else if (a.selection == SEL_RANK) {
+    const u32x4 b1 = draw(a.key, ST_SEL, child, 1);
+    pa = a.rank_order[rank_pick(blk.x, blk.y, blk.z, S, a.rank_thresh)];
+    pb = a.rank_order[rank_pick(blk.w, b1.x, b1.y, S, a.rank_thresh)];
+  } else {
+    pa = word_to_index(blk.x, S);
+    pb = word_to_index(blk.y, S);
+  }
+}
+
+// Sparse bit-flip sampler, group-cooperative form: continue the sequence of
+// mutation words at j with n distinct positions already flipped in fm (this
+// lane's chunk q), until K distinct positions are flipped.  A candidate is a
+// repeat iff its owner lane already has the bit: one ballot per candidate.
+template <int GS, bool NH = false>
+__device__ __forceinline__ uint4 sparse_continue(const GenArgs& a, uint64_t child, uint32_t K, uint32_t n, uint32_t j,
+                                              uint4 fm, uint32_t q, uint32_t gbase) {
+  u32x4 blk = draw<NH>(a.key, ST_BMUT, child, j >> 2);
+  while (n < K) {  // group-uniform
+    if ((j & 3u) == 0u) blk = draw<NH>(a.key, ST_BMUT, child, j >> 2);
+    const uint32_t p = word_to_index(sel4(blk, j & 3u), a.L);
+    ++j;
+    const uint32_t b = p & 127u;
+    const bool own = (p >> 7) == q;
+    const uint32_t wd = sel4(u32x4{fm.x, fm.y, fm.z, fm.w}, b >> 5);
+    unsigned long long bal = __ballot(own && ((wd >> (b & 31u)) & 1u));
+    if (GS < 64) bal = (bal >> gbase) & ((1ull << GS) - 1ull);
+    if (bal == 0ull) {
+      if (own) fm = xor4(fm, bit4(b));
+      ++n;
+    }
+  }
+  return fm;
+}
+
+// Sparse bit-flip sampler, sequential form (the definition, cpu_ops.cpp
+// sparse_positions): the first kk distinct word_to_index(mutation word j, L),
+// packed as 16-bit positions (0xFFFF = none; positions are < kSparseMaxL);
+// jn = the next unused word.
+template <bool NH>
+__device__ __forceinline__ uint4 sparse_seq(const RngKey& key, uint64_t child, uint32_t kk, uint32_t L, uint32_t& jn) {
+  uint32_t w0 = 0xFFFFFFFFu, w1 = 0xFFFFFFFFu, w2 = 0xFFFFFFFFu, w3 = 0xFFFFFFFFu;
+  uint32_t n = 0, j = 0;
+  u32x4 blk{0, 0, 0, 0};
+  while (n < kk) {
+    if ((j & 3u) == 0u) blk = draw<NH>(key, ST_BMUT, child, j >> 2);
+    const uint32_t p = word_to_index(sel4(blk, j & 3u), L);
+    ++j;
+    const bool seen = (w0 & 0xFFFFu) == p || (w0 >> 16) == p || (w1 & 0xFFFFu) == p || (w1 >> 16) == p ||
+                      (w2 & 0xFFFFu) == p || (w2 >> 16) == p || (w3 & 0xFFFFu) == p || (w3 >> 16) == p;
+    if (!seen) {
+      const uint32_t sh = (n & 1u) * 16u, keep = ~(0xFFFFu << sh), v = p << sh, wi = n >> 1;
+      w0 = wi == 0u ? (w0 & keep) | v : w0;
+      w1 = wi == 1u ? (w1 & keep) | v : w1;
+      w2 = wi == 2u ? (w2 & keep) | v : w2;
+      w3 = wi == 3u ? (w3 & keep) | v : w3;
+      ++n;
+    }
+  }
+  jn = j;
+  return make_uint4(w0, w1, w2, w3);
+}
+
 // ---------------------------------------------------------------------------
 // Generic kernel: every mode, every operator, any genome length.
 // ---------------------------------------------------------------------------
@@ -155,13 +240,14 @@ __global__ __launch_bounds__(kBlock) void binary_kernel(GenArgs a, unsigned long
   constexpr bool MUTATES = MODE == MODE_GEN || MODE == MODE_MUTATE;
   constexpr bool EVALS = OBJ != OBJ_NONE && (MODE == MODE_GEN || MODE == MODE_INIT || MODE == MODE_EVAL);
   const bool bitflip = MUTATES && a.mutation == MUT_BIT_FLIP && a.mut_rate > 0.f;
+  const bool sparse = bitflip && a.mut_sparse;
   const bool reset_one = MUTATES && a.mutation == MUT_RESET_ONE;
 
   if (MODE == MODE_GEN && a.n_elite > 0 && a.elite_idx == nullptr && blockIdx.x == 0) {
     unsigned long long b = block_reduce_parts(a.best_cur, a.n_best_cur, lds_red);
     if (threadIdx.x == 0) lds_elite = (uint32_t)best_index(b);
   }
-  if (MUTATES && bitflip)
+  if (bitflip)
     for (uint32_t i = threadIdx.x; i < kMutCap; i += kBlock) lds_thr[i] = a.mut_thr[i];
   __syncthreads();
 
@@ -169,35 +255,33 @@ __global__ __launch_bounds__(kBlock) void binary_kernel(GenArgs a, unsigned long
   const uint64_t stride = (uint64_t)gridDim.x * GPB;
   for (uint64_t child = (uint64_t)blockIdx.x * GPB + g_in_block; child < a.S; child += stride) {
     float score = 0.f;
-    if (MODE == MODE_GEN && child < a.n_elite) {
-      // elitism: copy elite rows unchanged into the front of the next generation
-      const uint32_t src = a.elite_idx ? a.elite_idx[child] : lds_elite;
-      for (uint32_t c = q; c < nchunks; c += GS) nxt[child * rs + c] = cur[(uint64_t)src * rs + c];
-      score = a.score_cur[src];
-    } else {
-      Pool<GS> pool;
-      pool.gbase = gbase;
-      pool.w = u32x4{0, 0, 0, 0};
+    {
+      // elitism: child = copy of the elite row, re-evaluated like every child
+      const bool elite = MODE == MODE_GEN && child < a.n_elite;
       uint32_t pa = 0, pb = 0;
       bool xo = false;
       uint32_t blo = 0, bhi = 0;  // ONE/TWO_POINT: bits [blo, bhi) come from parent B
-      if (MODE == MODE_GEN || MODE == MODE_CROSS || MODE == MODE_MUTATE) pool.w = draw(a.key, ST_CHILD, child, q);
-      if (MODE == MODE_GEN || MODE == MODE_CROSS) {
-        select_parents<GS>(a, pool, child, pa, pb);
-        xo = a.crossover != XO_NONE && do_crossover(a, pool.get(W_XOPROB, a.key, child));
+      u32x4 misc{0, 0, 0, 0};
+      if (MODE == MODE_GEN || MODE == MODE_CROSS || MODE == MODE_MUTATE) misc = bin_misc(a.key, child);
+      if (elite) {
+        pa = pb = a.elite_idx ? a.elite_idx[child] : lds_elite;
+      } else if (MODE == MODE_GEN || MODE == MODE_CROSS) {
+        bin_select(a, child, pa, pb);
+        xo = a.crossover != XO_NONE && do_crossover(a, misc.x);
         if (a.crossover == XO_ONE_POINT) {
-          blo = word_to_index(pool.get(W_CUT1, a.key, child), L);
+          blo = word_to_index(misc.y, L);
           bhi = L;
         } else if (a.crossover == XO_TWO_POINT) {
-          uint32_t c1 = word_to_index(pool.get(W_CUT1, a.key, child), L);
-          uint32_t c2 = word_to_index(pool.get(W_CUT2, a.key, child), L);
+          uint32_t c1 = word_to_index(misc.y, L);
+          uint32_t c2 = word_to_index(misc.z, L);
           blo = c1 < c2 ? c1 : c2;
           bhi = c1 < c2 ? c2 : c1;
         }
       }
       uint32_t rpos = 0xFFFFFFFFu;  // RESET_ONE: the one flipped bit
-      if (reset_one && pool.get(W_MUTIND, a.key, child) < a.mut_ind_thresh)
-        rpos = word_to_index(pool.get(W_MUTPOS, a.key, child), L);
+      if (reset_one && !elite && misc.w < a.mut_ind_thresh) rpos = word_to_index(bin_mut_word(a.key, child, 0), L);
+      uint4 fm = make_uint4(0, 0, 0, 0);  // sparse bit-flip: flips of chunk q (L <= 8192: one chunk per lane)
+      if (sparse && !elite) fm = sparse_continue<GS>(a, child, binom_count(misc.w, lds_thr), 0, 0, fm, q, gbase);
 
       BinObj<OBJ> acc;
       for (uint32_t c0 = 0; c0 < nchunks; c0 += GS) {  // group-uniform segment loop
@@ -219,9 +303,10 @@ __global__ __launch_bounds__(kBlock) void binary_kernel(GenArgs a, unsigned long
           }
         }
         if (c == nchunks - 1) v = and4(v, u4(a.last_mask));
-        if (bitflip) {
-          const uint32_t r0 = c == q ? pool.w.w : chunk_mut_word(a.key, child, c);
-          v = xor4(v, u4(chunk_flip_mask(a, child, c, chunk_len(L, c), r0, lds_thr)));
+        if (bitflip && !sparse && !elite) {
+          v = xor4(v, u4(chunk_flip_mask(a, child, c, chunk_len(L, c), bin_chunk_mut_word(a.key, child, c), lds_thr)));
+        } else if (sparse) {
+          v = xor4(v, fm);
         } else if (reset_one && (rpos >> 7) == c) {
           v = xor4(v, bit4(rpos & 127u));
         }
@@ -244,269 +329,279 @@ __global__ __launch_bounds__(kBlock) void binary_kernel(GenArgs a, unsigned long
 }
 
 // ---------------------------------------------------------------------------
-// Software-pipelined fused generation (the hot path).
+// The hot generation kernel: transposed tournaments.
 //
-// Every child is a chain of two DEPENDENT global round trips (tournament
-// score reads -> parent-row gathers) followed by a few hundred VALU
-// instructions.  Each group keeps three children in flight:
-//   body:  S2(c+1)  tournament compare + issue the parent-row loads
-//          S1(c+2)  Philox pool + issue 4 score loads
-//          S3(c)    crossover mask + mutation + fitness + stores
-// The body is unrolled x3 over statically rotated register sets (a register
-// COPY of an in-flight load forces s_waitcnt vmcnt(0)), the mutation table
-// lives in LDS (a global table lookup would wait on every older load: vmcnt
-// retires in order) and mutation flips go to a separate mask so no loop ever
-// touches an in-flight register.  Valid when every lane owns at most one
-// chunk (L <= 8192 bits) and selection is tournament-2 or random.
-// Bit-identical to binary_kernel.
+// A wave owns a contiguous range of children and breeds NG = 64/GS of them per
+// STEP (group g: child begin + t*NG + g).  Steps come in BATCHES of GS steps =
+// 64 children, and the per-child work that does not touch the genome runs
+// transposed, one lane per child of a whole batch:
+//   ISSUE    one Philox block = the 4 tournament contestants, 4 key loads
+//   RESOLVE  (next step) compare -> parents; the misc block (crossover test,
+//            cut points, mutation count K); the sparse bit-flip positions
+//            (one more block, first K distinct by a pairwise check); write a
+//            32-byte child RECORD to the wave's LDS ring (2 batches)
+// so a child costs 3/64 of a Philox per lane for its child-level words
+// instead of one, its tournament 4 load instructions per 64 children instead
+// of per 8, and mutation is a short loop over the record's positions instead
+// of a divergent geometric search in every chunk.  Breeding a step: XO mask
+// Philox (one block per chunk), mix, flips, popcount, group butterfly, stores.
+//
+// Pipeline (per step t): RESOLVE batch (t+1)/GS if (t+1)%GS==0; ISSUE batch
+// (t+2)/GS if (t+2)%GS==0; load the parent rows of step t+1; breed step t
+// from the rows loaded one step earlier.  Every load is issued on EVERY step
+// (the 4 key loads of a non-ISSUE step read one dummy line): s_waitcnt
+// vmcnt retires in order and hipcc assumes the fewest outstanding loads over
+// all paths, so a conditionally issued load would make the next wait drain it.
 // ---------------------------------------------------------------------------
-constexpr int XOK_UNIFORM = 0, XOK_RANGE = 1;  // crossover kind template values
 
-// Diagnostic ablation switches (bench/micro/ablate builds only, see
-// bench/micro/README.md; the shipped build defines none of them).
-// Waves per SIMD the pipelined kernel is register-limited to.  Measured: a
-// fourth register set (rows of c+1 AND c+2 in flight) at 5 or 4 waves/SIMD
-// ran 96.8 / 97.9 us/gen against 92.4 for three sets at 6 waves (headline).
-#ifndef PGA_PIPE_WAVES
-#define PGA_PIPE_WAVES 6
+constexpr uint32_t kTpMaxElite = 64;  // elites the fast kernel routes through its records
+
+#ifndef PGA_TP_WAVES
+#define PGA_TP_WAVES 6
 #endif
-#ifndef PGA_ABL
-#define PGA_ABL 0
-#endif
-constexpr int kAblXoRng = 1, kAblPoolRng = 2, kAblMut = 4, kAblGather = 8;
-#ifndef PGA_CACHE
-#define PGA_CACHE 0  // 1: non-temporal child stores, 2: non-temporal parent loads
-#endif
-typedef unsigned int v4u __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ void store_row(uint4* p, uint4 v) {
-  if (PGA_CACHE & 1) {
-    v4u x = {v.x, v.y, v.z, v.w};
-    __builtin_nontemporal_store(x, (v4u*)p);
-  } else {
-    *p = v;
-  }
-}
-__device__ __forceinline__ uint4 load_row(const uint4* p) {
-  if (PGA_CACHE & 2) {
-    v4u x = __builtin_nontemporal_load((const v4u*)p);
-    return make_uint4(x[0], x[1], x[2], x[3]);
-  }
-  return *p;
+
+__device__ __forceinline__ uint32_t pos16(uint4 r1, uint32_t k) {  // k-th packed 16-bit position
+  const uint32_t w = sel4(u32x4{r1.x, r1.y, r1.z, r1.w}, k >> 1);
+  return (k & 1u) ? (w >> 16) : (w & 0xFFFFu);
 }
 
-// PGA_STAMP builds (bench/micro only): per-wave start/end wall-clock stamps of
-// the pipelined kernel, dumped by pga_stamp_report() (ramp-up / tail study)
-#ifndef PGA_STAMP
-#define PGA_STAMP 0
-#endif
-#if PGA_STAMP
-__device__ unsigned long long g_stamps[2 * 65536];
-#endif
-
-// RESET: the per-individual reset mutation is possible (otherwise only
-// bit-flip / none, and the pool words are dead after stage 2: fewer VGPRs)
-template <int GS, int OBJ, int XOK, bool KEY, bool RESET>
-__global__ __launch_bounds__(kBlock, RESET ? PGA_PIPE_WAVES - 1 : PGA_PIPE_WAVES) void binary_gen_pipe(GenArgs a, unsigned long long* best_parts) {
+template <int GS, int OBJ, bool FULL, bool DENSE>
+__global__ __launch_bounds__(kBlock, PGA_TP_WAVES) void binary_gen_tp(GenArgs a, unsigned long long* best_parts) {
   resolve_gen(a);
-  __shared__ unsigned long long lds_red[kBlock / 64];
-  __shared__ uint32_t lds_elite;
+  constexpr uint32_t NW = kBlock / 64;
+  constexpr uint32_t NG = 64 / GS;  // children per wave per step
+  constexpr bool EVALS = OBJ != OBJ_NONE;
+  // integer objectives tournament on their exact u16 keys (L2-resident)
+  constexpr bool KEY = OBJ == OBJ_ONEMAX || OBJ == OBJ_LEADING_ONES || OBJ == OBJ_TRAP;
+  __shared__ uint4 lds_rec[NW][2][64][2];  // per wave: 2 batches x 64 records x 32 B
+  __shared__ uint4 lds_idx[NW][64];        // contestants of the tournament in flight
   __shared__ uint32_t lds_thr[kMutCap];
+  __shared__ uint32_t lds_el[kTpMaxElite];  // elite sources
+  __shared__ unsigned long long lds_red[NW];
 
-  const uint32_t lane = lane_id();
-  const uint32_t q = lane & (GS - 1);
-  const uint32_t gbase = lane & ~(uint32_t)(GS - 1);
-  constexpr uint32_t GPB = kBlock / GS;
-  const uint64_t rs = a.row_words >> 2;
+  const uint32_t lane = lane_id(), wid = threadIdx.x >> 6;
+  const uint32_t q = lane & (GS - 1), gbase = lane & ~(uint32_t)(GS - 1), g = lane / GS;
   const uint4* cur = (const uint4*)a.cur;
   uint4* nxt = (uint4*)a.next;
-  const uint32_t L = a.L;
-  const uint32_t S = (uint32_t)a.S;
-  const bool have = q < a.chunks;
-  const bool last = q == a.chunks - 1;
+  const uint32_t L = a.L, S = (uint32_t)a.S;
+  // FULL: chunks == GS, every lane owns a chunk
+  const bool have = FULL || q < a.chunks, last = q == a.chunks - 1;
+  const uint32_t qq = have ? q : 0u;
   const uint32_t clen = have ? chunk_len(L, q) : 0u;
-  const bool k2 = a.selection == SEL_TOURNAMENT;  // tour_k == 2 guaranteed by the launcher
+  const bool tourn = a.selection == SEL_TOURNAMENT;  // tour_k == 2 guaranteed by the launcher, else random
   const bool xo_on = a.crossover != XO_NONE;
+  const bool range = a.crossover != XO_UNIFORM;  // ONE/TWO_POINT, or NONE (empty range)
+  // DENSE: per-chunk geometric bit-flips; otherwise the record carries the
+  // flip positions (sparse bit-flip, RESET_ONE, or none)
   const bool bitflip = a.mutation == MUT_BIT_FLIP && a.mut_rate > 0.f;
-  const bool reset_one = RESET && a.mutation == MUT_RESET_ONE;
+  const bool sparse = !DENSE && bitflip;
+  const bool reset_one = !DENSE && a.mutation == MUT_RESET_ONE;
   const uint4 lmask = u4(a.last_mask);
+  // Every row / score byte offset fits 32 bits (the launcher checks (S + pad)
+  // rows < 4 GiB): uniform base + 32-bit lane offset, one VGPR per address
+  const uint32_t rb = a.row_words * 4u;
+#define ELEM(T, base, i) (*(T*)((char*)(base) + (uint32_t)(i) * (uint32_t)sizeof(T)))
+#define ROW(base, row, ch) (*(uint4*)((char*)(base) + ((uint32_t)(row) * rb + (uint32_t)(ch) * 16u)))
 
-  if (a.n_elite > 0 && a.elite_idx == nullptr && blockIdx.x == 0) {
-    unsigned long long b = block_reduce_parts(a.best_cur, a.n_best_cur, lds_red);
-    if (threadIdx.x == 0) lds_elite = (uint32_t)best_index(b);
+  // this wave's children [begin, end): contiguous, a multiple of NG long
+  const uint64_t W = (uint64_t)gridDim.x * NW, w = (uint64_t)blockIdx.x * NW + wid;
+  uint64_t per = (S + W - 1) / W;
+  per = (per + NG - 1) / NG * NG;
+  const uint32_t begin = (uint32_t)(w * per < S ? w * per : S);
+  const uint32_t end = (uint32_t)(begin + per < S ? begin + per : S);
+  const uint32_t nsteps = (end - begin + NG - 1) / NG;
+
+  // elite sources of children [0, n_elite) (n_elite <= kTpMaxElite), for the
+  // blocks that hold any of them
+  if (a.n_elite > 0 && (uint64_t)blockIdx.x * NW * per < a.n_elite) {
+    if (a.elite_idx) {
+      for (uint32_t i = threadIdx.x; i < a.n_elite; i += kBlock) lds_el[i] = a.elite_idx[i];
+    } else {
+      unsigned long long b = block_reduce_parts(a.best_cur, a.n_best_cur, lds_red);
+      if (threadIdx.x == 0) lds_el[0] = (uint32_t)best_index(b);
+    }
   }
   if (bitflip)
     for (uint32_t i = threadIdx.x; i < kMutCap; i += kBlock) lds_thr[i] = a.mut_thr[i];
   __syncthreads();
 
-#if PGA_STAMP
-  const uint32_t wid_ = blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
-  if (lane == 0 && wid_ < 65536) g_stamps[2 * wid_] = wall_clock64();
-#endif
   unsigned long long my_best = 0;
-  const uint64_t stride = (uint64_t)gridDim.x * GPB;
-  uint64_t c0 = (uint64_t)blockIdx.x * GPB + threadIdx.x / GS;
+  if (nsteps > 0) {  // wave-uniform
+    uint4(*rec)[64][2] = lds_rec[wid];
+    // keys of the tournament in flight (lane = child `lane` of the batch)
+    float t0 = 0.f, t1 = 0.f, t2 = 0.f, t3 = 0.f;
+    const uint32_t nbatch = (end - begin + 63) / 64;
 
-  // elites first (only the first few groups of the grid have any)
-  while (c0 < a.n_elite && c0 < a.S) {
-    const uint32_t src = a.elite_idx ? a.elite_idx[c0] : lds_elite;
-    if (have) nxt[c0 * rs + q] = cur[(uint64_t)src * rs + q];
-    const float sc = a.score_cur[src];
-    if (q == 0) {
-      a.score_next[c0] = sc;
-      if (KEY) a.key_next[c0] = (uint16_t)sc;
-      const unsigned long long pb = pack_best(sc, c0);
-      my_best = pb > my_best ? pb : my_best;
+    // ISSUE: contestants of batch B (lane = batch child) and their key loads.
+    // The 4 loads are issued on every step (line 0 when not a real issue).
+#define PGA_TP_ISSUE(B, real)                                                          \
+  {                                                                                    \
+    uint32_t j0 = 0, j1 = 0, j2 = 0, j3 = 0;                                           \
+    if (real) {                                                                        \
+      const uint32_t tc = begin + (B) * 64u + lane;                                    \
+      const uint32_t cc = tc < end ? tc : end - 1;                                     \
+      const u32x4 blk = draw<true>(a.key, ST_SEL, cc, 0);                              \
+      const uint4 ix = make_uint4(word_to_index(blk.x, S), word_to_index(blk.y, S),    \
+                                  word_to_index(blk.z, S), word_to_index(blk.w, S));   \
+      lds_idx[wid][lane] = ix;                                                         \
+      if (tourn) {                                                                     \
+        j0 = ix.x;                                                                     \
+        j1 = ix.y;                                                                     \
+        j2 = ix.z;                                                                     \
+        j3 = ix.w;                                                                     \
+      }                                                                                \
+    }                                                                                  \
+    if (KEY) {                                                                         \
+      t0 = (float)ELEM(const uint16_t, a.key_cur, j0);                                 \
+      t1 = (float)ELEM(const uint16_t, a.key_cur, j1);                                 \
+      t2 = (float)ELEM(const uint16_t, a.key_cur, j2);                                 \
+      t3 = (float)ELEM(const uint16_t, a.key_cur, j3);                                 \
+    } else {                                                                           \
+      t0 = ELEM(const float, a.score_cur, j0);                                         \
+      t1 = ELEM(const float, a.score_cur, j1);                                         \
+      t2 = ELEM(const float, a.score_cur, j2);                                         \
+      t3 = ELEM(const float, a.score_cur, j3);                                         \
+    }                                                                                  \
+  }
+
+    // RESOLVE: parents, crossover plan and flip positions of batch B -> records
+#define PGA_TP_RESOLVE(B)                                                                                       \
+  {                                                                                                             \
+    const uint32_t tc = begin + (B) * 64u + lane;                                                               \
+    const uint32_t cc = tc < end ? tc : end - 1;                                                                \
+    const uint4 ix = lds_idx[wid][lane];                                                                        \
+    uint32_t pa = ix.x, pb = ix.y;                                                                              \
+    if (tourn) {                                                                                                \
+      pa = t0 < t1 ? ix.y : ix.x;                                                                               \
+      pb = t2 < t3 ? ix.w : ix.z;                                                                               \
+    }                                                                                                           \
+    const u32x4 misc = bin_misc<true>(a.key, cc);                                                               \
+    const bool elite = tc < a.n_elite;                                                                          \
+    const bool xo = !elite && xo_on && do_crossover(a, misc.x);                                                 \
+    if (elite) pa = lds_el[tc];                                                                                 \
+    pb = xo ? pb : pa;                                                                                          \
+    uint32_t lo = 0, hi = 0;                                                                                    \
+    if (range && xo) {                                                                                          \
+      const uint32_t x1 = word_to_index(misc.y, L);                                                             \
+      if (a.crossover == XO_ONE_POINT) {                                                                        \
+        lo = x1;                                                                                                \
+        hi = L;                                                                                                 \
+      } else {                                                                                                  \
+        const uint32_t x2 = word_to_index(misc.z, L);                                                           \
+        lo = x1 < x2 ? x1 : x2;                                                                                 \
+        hi = x1 < x2 ? x2 : x1;                                                                                 \
+      }                                                                                                         \
+    }                                                                                                           \
+    uint32_t K = 0, jn = 0;                                                                                     \
+    uint4 P = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu);                                   \
+    if (reset_one && !elite && misc.w < a.mut_ind_thresh) {                                                     \
+      K = 1;                                                                                                    \
+      P.x = word_to_index(bin_mut_word<true>(a.key, cc, 0), L) | 0xFFFF0000u;                                   \
+    }                                                                                                           \
+    if (sparse && !elite) {                                                                                     \
+      K = binom_count(misc.w, lds_thr);                                                                         \
+      if (K > 0u) {                                                                                             \
+        const uint32_t kk = K < kRecPos ? K : kRecPos;                                                          \
+        const u32x4 m0 = draw<true>(a.key, ST_BMUT, cc, 0);                                                     \
+        const uint32_t c0 = word_to_index(m0.x, L), c1 = word_to_index(m0.y, L);                                \
+        const uint32_t c2 = word_to_index(m0.z, L), c3 = word_to_index(m0.w, L);                                \
+        /* common case: the first kk <= 4 candidates are distinct, hence the positions */                      \
+        const bool slow = kk > 4u || (kk > 1u && c0 == c1) || (kk > 2u && (c2 == c0 || c2 == c1)) ||            \
+                          (kk > 3u && (c3 == c0 || c3 == c1 || c3 == c2));                                      \
+        P = make_uint4(c0 | (c1 << 16), c2 | (c3 << 16), 0xFFFFFFFFu, 0xFFFFFFFFu);                             \
+        jn = kk;                                                                                                \
+        if (slow) P = sparse_seq<true>(a.key, cc, kk, L, jn);                                                   \
+      }                                                                                                         \
+    }                                                                                                           \
+    const uint32_t meta = (K > 255u ? 255u : K) | ((jn > 0xFFFFu ? 0xFFFFu : jn) << 8) | (elite ? 1u << 31 : 0u); \
+    uint4(*r)[2] = rec[(B) & 1u];                                                                               \
+    r[lane][0] = make_uint4(pa, pb, lo | (hi << 16), meta);                                                     \
+    r[lane][1] = P;                                                                                             \
+  }
+
+    // prologue: batch 0 resolved (and batch 1 issued when GS == 1), rows of step 0 in flight
+    PGA_TP_ISSUE(0u, true)
+    PGA_TP_RESOLVE(0u)
+    if (GS == 1) PGA_TP_ISSUE(1u, 1u < nbatch)
+    uint4 A0, B0, A1, B1;
+    {
+      const uint4 r = rec[0][g][0];
+      A0 = ROW(cur, r.x, qq);
+      B0 = ROW(cur, r.y, qq);
     }
-    c0 += stride;
+
+    // one STEP: every vector-memory operation is unconditional (the tail of
+    // the last wave writes the padding rows past S)
+#define PGA_TP_STEP(t, XA, XB, YA, YB)                                                                      \
+  {                                                                                                         \
+    const uint32_t b = (t) / GS, i = (t) & (GS - 1);                                                        \
+    if ((((t) + 1) & (GS - 1)) == 0u && b + 1 < nbatch) PGA_TP_RESOLVE(b + 1)                               \
+    {                                                                                                       \
+      const uint32_t bi = ((t) + 2) / GS;                                                                   \
+      PGA_TP_ISSUE(bi, (((t) + 2) & (GS - 1)) == 0u && bi < nbatch)                                         \
+    }                                                                                                       \
+    {                                                                                                       \
+      /* parent rows of step t+1 (the last step re-reads its own) */                                        \
+      const uint32_t tn = (t) + 1 < nsteps ? (t) + 1 : (t);                                                 \
+      const uint4 r = rec[(tn / GS) & 1u][(tn & (GS - 1)) * NG + g][0];                                     \
+      YA = ROW(cur, r.x, qq);                                                                               \
+      YB = ROW(cur, r.y, qq);                                                                               \
+    }                                                                                                       \
+    const uint32_t c = begin + (t) * NG + g;                                                                \
+    const uint4 r0 = rec[b & 1u][i * NG + g][0];                                                            \
+    const uint32_t meta = r0.w;                                                                             \
+    const uint4 m = range ? range_keep_a(q, r0.z & 0xFFFFu, r0.z >> 16) : u4(draw<true>(a.key, ST_XO, c, q)); \
+    uint4 v = mix4(XA, XB, m);                                                                              \
+    if (last) v = and4(v, lmask);                                                                           \
+    uint4 fm = make_uint4(0, 0, 0, 0);                                                                      \
+    if (DENSE) {                                                                                            \
+      if (bitflip && !(meta >> 31)) /* elites are not mutated */                                           \
+        fm = u4(chunk_flip_mask(a, c, q, clen, bin_chunk_mut_word<true>(a.key, c, q), lds_thr));            \
+    } else {                                                                                                \
+      const uint32_t K = meta & 0xFFu;                                                                      \
+      if (K > 0u) {                                                                                         \
+        const uint4 r1 = rec[b & 1u][i * NG + g][1];                                                        \
+        const uint32_t kk = K < kRecPos ? K : kRecPos;                                                      \
+        /* the first 4 unrolled (a loop here costs ~20 VGPRs of the whole kernel) */                       \
+        _Pragma("unroll") for (uint32_t k = 0; k < 4; ++k) {                                               \
+          const uint32_t p = pos16(r1, k);                                                                  \
+          if (k < kk && (p >> 7) == q) fm = xor4(fm, bit4(p & 127u));                                       \
+        }                                                                                                   \
+        if (kk > 4u)                                                                                        \
+          for (uint32_t k = 4; k < kk; ++k) {                                                               \
+            const uint32_t p = pos16(r1, k);                                                                \
+            if ((p >> 7) == q) fm = xor4(fm, bit4(p & 127u));                                              \
+          }                                                                                                 \
+        if (K > kRecPos) fm = sparse_continue<GS, true>(a, c, K, kRecPos, (meta >> 8) & 0xFFFFu, fm, q, gbase); \
+      }                                                                                                     \
+    }                                                                                                       \
+    v = xor4(v, fm);                                                                                        \
+    BinObj<OBJ> acc;                                                                                        \
+    if (have) acc.add(a, v, q);                                                                             \
+    const float sc = acc.template finish<GS>(a);                                                            \
+    if (have) ROW(nxt, c, q) = v;                                                                           \
+    if (EVALS) { /* every lane of the group stores the same score */                                        \
+      ELEM(float, a.score_next, c) = sc;                                                                    \
+      if (KEY) ELEM(uint16_t, a.key_next, c) = (uint16_t)sc;                                                \
+      const unsigned long long pk = c < S ? pack_best(sc, c) : 0ull;                                        \
+      my_best = pk > my_best ? pk : my_best;                                                                \
+    }                                                                                                       \
   }
 
-#define PGA_SET(P)                                                       \
-  u32x4 P##w{0, 0, 0, 0};                                                \
-  uint32_t P##i0 = 0, P##i1 = 0, P##i2 = 0, P##i3 = 0;                   \
-  float P##t0 = 0.f, P##t1 = 0.f, P##t2 = 0.f, P##t3 = 0.f;              \
-  uint4 P##A = make_uint4(0, 0, 0, 0), P##B = make_uint4(0, 0, 0, 0);    \
-  uint32_t P##lo = 0, P##hi = 0;                                         \
-  bool P##xo = false;
-  PGA_SET(X)
-  PGA_SET(Y)
-  PGA_SET(Z)
-#undef PGA_SET
-
-  // Stages 1 and 2 issue their loads UNCONDITIONALLY (indices clamped for
-  // tail children, lanes without a chunk re-read chunk 0, B re-reads A's line
-  // when there is no crossover): hipcc's waitcnt pass must assume the minimum
-  // number of vector-memory ops over all paths, so any conditionally issued
-  // load between a load and its use degrades the wait to vmcnt(0).
-  const uint32_t qq = have ? q : 0u;
-
-  // stage 1: Philox pool + tournament contestant score loads
-#define PGA_STAGE1(c, P)                                                   \
-  {                                                                        \
-    const uint64_t cc_ = (c) < a.S ? (c) : a.S - 1;                        \
-    if (PGA_ABL & kAblPoolRng) {                                           \
-      const uint32_t h_ = (uint32_t)cc_ * 0x9E3779B9u + q * 0x85EBCA6Bu;   \
-      P##w = u32x4{h_, h_ * 0xC2B2AE35u, h_ ^ 0x27D4EB2Fu, h_ * 3u};        \
-    } else {                                                               \
-      P##w = draw(a.key, ST_CHILD, cc_, q);                                \
-    }                                                                      \
-    Pool<GS> pool_{P##w, gbase};                                           \
-    P##i0 = word_to_index(pool_.get(W_SEL + 0, a.key, cc_), S);            \
-    P##i1 = word_to_index(pool_.get(W_SEL + 1, a.key, cc_), S);            \
-    P##i2 = word_to_index(pool_.get(W_SEL + 2, a.key, cc_), S);            \
-    P##i3 = word_to_index(pool_.get(W_SEL + 3, a.key, cc_), S);            \
-    if (KEY) { /* exact u16 keys: L2-resident, same comparisons */        \
-      P##t0 = (float)a.key_cur[P##i0];                                     \
-      P##t1 = (float)a.key_cur[P##i1];                                     \
-      P##t2 = (float)a.key_cur[P##i2];                                     \
-      P##t3 = (float)a.key_cur[P##i3];                                     \
-    } else {                                                               \
-      P##t0 = a.score_cur[P##i0];                                          \
-      P##t1 = a.score_cur[P##i1];                                          \
-      P##t2 = a.score_cur[P##i2];                                          \
-      P##t3 = a.score_cur[P##i3];                                          \
-    }                                                                      \
+    uint32_t t = 0;
+    for (; t + 1 < nsteps; t += 2) {  // static row-register rotation
+      PGA_TP_STEP(t, A0, B0, A1, B1)
+      PGA_TP_STEP(t + 1, A1, B1, A0, B0)
+    }
+    if (t < nsteps) PGA_TP_STEP(t, A0, B0, A1, B1)
+#undef PGA_TP_ISSUE
+#undef PGA_TP_RESOLVE
+#undef PGA_TP_STEP
   }
-
-  // stage 2: tournament winners (branch-free select), crossover plan, row loads
-#define PGA_STAGE2(c, P)                                                                    \
-  {                                                                                         \
-    const uint64_t cc_ = (c) < a.S ? (c) : a.S - 1;                                         \
-    uint32_t pa_, pb_;                                                                      \
-    if (k2) {                                                                               \
-      pa_ = P##i0 ^ ((P##i0 ^ P##i1) & (0u - (uint32_t)(P##t0 < P##t1)));                   \
-      pb_ = P##i2 ^ ((P##i2 ^ P##i3) & (0u - (uint32_t)(P##t2 < P##t3)));                   \
-    } else {                                                                                \
-      pa_ = P##i0;                                                                          \
-      pb_ = P##i1;                                                                          \
-    }                                                                                       \
-    Pool<GS> pool_{P##w, gbase};                                                            \
-    P##xo = xo_on && do_crossover(a, pool_.get(W_XOPROB, a.key, cc_));                      \
-    if (XOK == XOK_RANGE) {                                                                 \
-      const uint32_t x1_ = word_to_index(pool_.get(W_CUT1, a.key, cc_), L);                 \
-      if (a.crossover == XO_ONE_POINT) {                                                    \
-        P##lo = x1_;                                                                        \
-        P##hi = L;                                                                          \
-      } else {                                                                              \
-        const uint32_t x2_ = word_to_index(pool_.get(W_CUT2, a.key, cc_), L);               \
-        P##lo = x1_ < x2_ ? x1_ : x2_;                                                      \
-        P##hi = x1_ < x2_ ? x2_ : x1_;                                                      \
-      }                                                                                     \
-    }                                                                                       \
-    pb_ = P##xo ? pb_ : pa_;                                                                \
-    if (PGA_ABL & kAblGather) {                                                             \
-      pa_ = (uint32_t)cc_;                                                                  \
-      pb_ = (uint32_t)cc_;                                                                  \
-    }                                                                                       \
-    P##A = load_row(cur + (uint64_t)pa_ * rs + qq);                                         \
-    P##B = load_row(cur + (uint64_t)pb_ * rs + qq);                                         \
-  }
-
-  // stage 3: crossover, mutation (own-register first draw, LDS thresholds),
-  // fitness, stores
-#define PGA_STAGE3(c, P)                                                                     \
-  if ((c) < a.S) {                                                                           \
-    /* branch-free: a phi between the loaded row and the mixed row would be a   */          \
-    /* register copy of an in-flight load (= s_waitcnt vmcnt(0))                 */          \
-    const uint4 mx_ = (PGA_ABL & kAblXoRng) ? make_uint4(P##w.x, P##w.y, ~P##w.x, ~P##w.y)               \
-                      : (XOK == XOK_UNIFORM ? u4(draw(a.key, ST_XO, (c), q)) : range_keep_a(q, P##lo, P##hi)); \
-    const uint32_t keep_ = P##xo ? 0u : 0xFFFFFFFFu;                                         \
-    const uint4 m_ = make_uint4(mx_.x | keep_, mx_.y | keep_, mx_.z | keep_, mx_.w | keep_); \
-    uint4 v_ = mix4(P##A, P##B, m_);                                                         \
-    if (last) v_ = and4(v_, lmask);                                                          \
-    if (bitflip && !(PGA_ABL & kAblMut)) {                                                   \
-      v_ = xor4(v_, u4(chunk_flip_mask(a, (c), q, clen, P##w.w, lds_thr)));                  \
-    } else if (reset_one) {                                                                  \
-      Pool<GS> pool_{P##w, gbase};                                                           \
-      if (pool_.get(W_MUTIND, a.key, (c)) < a.mut_ind_thresh) {                              \
-        const uint32_t mpos_ = word_to_index(pool_.get(W_MUTPOS, a.key, (c)), L);            \
-        if ((mpos_ >> 7) == q) v_ = xor4(v_, bit4(mpos_ & 127u));                            \
-      }                                                                                      \
-    }                                                                                        \
-    BinObj<OBJ> acc_;                                                                        \
-    if (have) {                                                                              \
-      store_row(nxt + (c) * rs + q, v_);                                                     \
-      acc_.add(a, v_, q);                                                                    \
-    }                                                                                        \
-    const float sc_ = acc_.template finish<GS>(a);                                           \
-    if (q == 0) {                                                                            \
-      a.score_next[(c)] = sc_;                                                               \
-      if (KEY) a.key_next[(c)] = (uint16_t)sc_;                                              \
-      const unsigned long long pb_ = pack_best(sc_, (c));                                    \
-      my_best = pb_ > my_best ? pb_ : my_best;                                               \
-    }                                                                                        \
-  }
-
-  // prologue: X = c0 (after stage 2), Y = c1 (after stage 1).  Each body
-  // issues the score loads of c+2, then the row loads of c+1 (whose score
-  // loads went out one body earlier), then finishes c (rows one body old).
-  PGA_STAGE1(c0, X)
-  PGA_STAGE2(c0, X)
-  PGA_STAGE1(c0 + stride, Y)
-  while (c0 < a.S) {  // group-uniform
-    PGA_STAGE1(c0 + 2 * stride, Z)
-    PGA_STAGE2(c0 + stride, Y)
-    PGA_STAGE3(c0, X)
-    c0 += stride;
-    if (c0 >= a.S) break;
-    PGA_STAGE1(c0 + 2 * stride, X)
-    PGA_STAGE2(c0 + stride, Z)
-    PGA_STAGE3(c0, Y)
-    c0 += stride;
-    if (c0 >= a.S) break;
-    PGA_STAGE1(c0 + 2 * stride, Y)
-    PGA_STAGE2(c0 + stride, X)
-    PGA_STAGE3(c0, Z)
-    c0 += stride;
-  }
-#undef PGA_STAGE1
-#undef PGA_STAGE2
-#undef PGA_STAGE3
-#if PGA_STAMP
-  if (lane == 0 && wid_ < 65536) g_stamps[2 * wid_ + 1] = wall_clock64();
-#endif
-
-  unsigned long long b = block_max_u64(my_best, lds_red);
-  if (threadIdx.x == 0 && best_parts) best_parts[blockIdx.x] = b;
+#undef ROW
+#undef ELEM
+  unsigned long long bb = block_max_u64(my_best, lds_red);
+  if (threadIdx.x == 0 && best_parts && EVALS) best_parts[blockIdx.x] = bb;
 }
 
 template <typename K>
@@ -521,24 +616,22 @@ uint32_t launch_mode(int mode, const GenArgs& a, unsigned long long* parts, hipS
   constexpr uint32_t gpb = kBlock / GS;
   switch (mode) {
     case MODE_GEN: {
-      const bool pipe = a.chunks <= (uint32_t)GS &&
+      const bool fast = a.chunks <= (uint32_t)GS &&
                         ((a.selection == SEL_TOURNAMENT && a.tour_k == 2) || a.selection == SEL_RANDOM) &&
-                        !(a.n_elite > 1 && a.elite_idx == nullptr) && getenv_pipeline();
-      if (pipe) {
-        constexpr bool INT_OBJ = OBJ == OBJ_ONEMAX || OBJ == OBJ_LEADING_ONES || OBJ == OBJ_TRAP;
-        const bool key = INT_OBJ && a.key_cur != nullptr;
-        const bool range = a.crossover == XO_ONE_POINT || a.crossover == XO_TWO_POINT;
-        const bool reset = a.mutation == MUT_RESET_ONE;
-#define PGA_PIPE(XK, KY)                                                        \
-  return reset ? go(binary_gen_pipe<GS, OBJ, XK, KY, true>, a, parts, gpb, s)   \
-               : go(binary_gen_pipe<GS, OBJ, XK, KY, false>, a, parts, gpb, s);
-        if (key) {
-          if (range) { PGA_PIPE(XOK_RANGE, INT_OBJ) }
-          PGA_PIPE(XOK_UNIFORM, INT_OBJ)
+                        !(a.n_elite > 1 && a.elite_idx == nullptr);
+      constexpr bool INT_OBJ = OBJ == OBJ_ONEMAX || OBJ == OBJ_LEADING_ONES || OBJ == OBJ_TRAP;
+      // 32-bit offsets: the (S + kRowPad)-row buffers must stay below 4 GiB
+      const bool o32 = (a.S + kRowPad) * (uint64_t)a.row_words * 4u <= 0xFFFFFFFFull;
+      if (fast && o32 && a.n_elite <= kTpMaxElite && (!INT_OBJ || a.key_cur != nullptr)) {
+        const bool dense = a.mutation == MUT_BIT_FLIP && a.mut_rate > 0.f && !a.mut_sparse;
+        const bool full = a.chunks == (uint32_t)GS;
+        // one block = 4 waves x 64 children per batch
+        if (full) {
+          if (dense) return go(binary_gen_tp<GS, OBJ, true, true>, a, parts, kBlock, s);
+          return go(binary_gen_tp<GS, OBJ, true, false>, a, parts, kBlock, s);
         }
-        if (range) { PGA_PIPE(XOK_RANGE, false) }
-        PGA_PIPE(XOK_UNIFORM, false)
-#undef PGA_PIPE
+        if (dense) return go(binary_gen_tp<GS, OBJ, false, true>, a, parts, kBlock, s);
+        return go(binary_gen_tp<GS, OBJ, false, false>, a, parts, kBlock, s);
       }
       return go(binary_kernel<GS, OBJ, MODE_GEN>, a, parts, gpb, s);
     }
@@ -561,31 +654,6 @@ uint32_t launch_obj(int mode, const GenArgs& a, unsigned long long* parts, hipSt
 }
 
 }  // namespace
-
-#if PGA_STAMP
-// wave start/end distribution of the last pipelined launch (100 MHz wall clock)
-void pga_stamp_report(uint32_t nwaves) {
-  std::vector<unsigned long long> h(2ull * nwaves);
-  PGA_HIP_CHECK(hipDeviceSynchronize());
-  PGA_HIP_CHECK(hipMemcpyFromSymbol(h.data(), HIP_SYMBOL(g_stamps), 16ull * nwaves));
-  unsigned long long t0 = ~0ull;
-  for (uint32_t i = 0; i < nwaves; ++i) t0 = h[2 * i] < t0 ? h[2 * i] : t0;
-  std::vector<double> st, en, du;
-  for (uint32_t i = 0; i < nwaves; ++i) {
-    st.push_back((h[2 * i] - t0) * 0.01);
-    en.push_back((h[2 * i + 1] - t0) * 0.01);
-    du.push_back((h[2 * i + 1] - h[2 * i]) * 0.01);
-  }
-  auto pr = [](const char* n, std::vector<double> v) {
-    std::sort(v.begin(), v.end());
-    std::printf("%s us: min %.1f p10 %.1f p50 %.1f p90 %.1f max %.1f\n", n, v[0], v[v.size() / 10], v[v.size() / 2],
-                v[v.size() * 9 / 10], v.back());
-  };
-  pr("wave start", st);
-  pr("wave end  ", en);
-  pr("wave life ", du);
-}
-#endif
 
 uint32_t binary_launch(int mode, const GenArgs& a, unsigned long long* best_parts, hipStream_t s) {
   uint32_t grid = 0;

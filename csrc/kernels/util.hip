@@ -54,12 +54,7 @@ uint32_t occupancy_blocks(const void* kernel, int block) {
 
 uint32_t launch_grid_occ(uint64_t S, uint32_t per_block, const void* kernel) {
   uint64_t need = (S + per_block - 1) / per_block;
-  static int mult = -1;
-  if (mult < 0) {  // PGA_GRID_MULT: launch k x the resident grid (load-balance experiments)
-    const char* e = getenv("PGA_GRID_MULT");
-    mult = e && atoi(e) > 0 ? atoi(e) : 1;
-  }
-  uint64_t cap = (uint64_t)device_cu_count() * occupancy_blocks(kernel, dev::kBlock) * mult;
+  uint64_t cap = (uint64_t)device_cu_count() * occupancy_blocks(kernel, dev::kBlock);
   if (cap > kMaxGrid) cap = kMaxGrid;
   uint64_t g = need < cap ? need : cap;
   return (uint32_t)(g == 0 ? 1 : g);
@@ -76,6 +71,20 @@ void build_mut_table(float p, uint32_t L, uint32_t* out, float* inv_log2_1mp) {
   if (p <= 0.f) *inv_log2_1mp = 0.f;
   else if (p >= 1.f) *inv_log2_1mp = 0.f;
   else *inv_log2_1mp = (float)(1.0 / std::log2(q));
+}
+
+void build_binom_table(float p, uint32_t L, uint32_t* out) {
+  // out[k] = floor(P(K <= k) * 2^32), K ~ Binomial(L, p); 0xFFFFFFFF once the
+  // remaining tail is below 2^-32 (ends the table, see binom_count)
+  const long double pp = p, qq = 1.0L - pp;
+  long double pmf = expl((long double)L * log1pl(-pp)), cdf = 0.0L;
+  for (uint32_t k = 0; k < kMutCap; ++k) {
+    cdf += pmf;
+    const long double v = floorl(cdf * 4294967296.0L);
+    out[k] = v >= 4294967295.0L ? 0xFFFFFFFFu : (uint32_t)v;
+    pmf = k < L ? pmf * (long double)(L - k) / (long double)(k + 1) * pp / qq : 0.0L;
+  }
+  out[kMutCap - 1] = 0xFFFFFFFFu;
 }
 
 namespace {

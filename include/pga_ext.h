@@ -122,6 +122,10 @@ int pga_comm_info(const pga_t *p, struct pga_comm_stats *out);
  * arrives with forged scores (mode 2) */
 int pga_comm_set_fault(pga_t *p, int every, int mode);
 /* global best over ranks (score, owning rank) */
+/* one inter-rank migration epoch now (the step pga_run_islands takes every
+ * m generations), for callers driving their own generation loop; pass every
+ * rank of an InitAll / loopback group, or the one solver of an InitRank rank */
+int pga_comm_exchange(pga_t **solvers, int count, float pct);
 int pga_comm_best(pga_t *p, float *score, int *rank);
 /* pga_run_islands over every rank of an InitAll / loopback group at once */
 int pga_run_islands_multi(pga_t **solvers, int n, unsigned generations, unsigned m, float pct);

@@ -101,17 +101,18 @@ def test_staged_equals_fused():
     assert torch.equal(a.scores, b.scores)
 
 
-def test_mutation_rate_statistics():
+@pytest.mark.parametrize("p", [0.01, 1.0 / 512])  # dense (per-chunk geometric) and sparse (Binomial) samplers
+def test_mutation_rate_statistics(p):
     """Bit-flip at rate p: with crossover=none and random selection, a child
     differs from its parent in Binomial(L, p) bits."""
-    L, S, p = 512, 4096, 0.01
+    L, S = 512, 4096
     ga = make(pga.models.OneMax(L), S=S, selection="random", crossover="none", mutation_rate=p)
     parents = ga.genomes().clone()
     ga.run(1)
     kids = ga.genomes()
-    # parent A of child i is child word W_SEL=5: ST_CHILD block 1, register .z
+    # parent A of child i is selection word 0: ST_SEL (8) block 0, register .x
     seed = 3
-    idx = torch.tensor([(_C.philox(1 | (3 << 24), i, 0, 0, seed, 0)[2] * S) >> 32 for i in range(S)])
+    idx = torch.tensor([(_C.philox(0 | (8 << 24), i, 0, 0, seed, 0)[0] * S) >> 32 for i in range(S)])
     nflip = (kids != parents[idx]).sum(-1).float()
     mean = nflip.mean().item()
     assert abs(mean - L * p) < 4 * math.sqrt(L * p * (1 - p) / S)

@@ -62,6 +62,7 @@ def lib():
     L.pga_comm_degraded.argtypes = [vp]
     L.pga_comm_info.argtypes = [vp, C.POINTER(Stats)]
     L.pga_comm_best.argtypes = [vp, C.POINTER(C.c_float), C.POINTER(C.c_int)]
+    L.pga_comm_exchange.argtypes = [C.POINTER(vp), C.c_int, C.c_float]
     L.pga_comm_rank.argtypes = [vp]
     L.pga_comm_size.argtypes = [vp]
     return L
@@ -175,11 +176,16 @@ def test_forged_scores_are_rescored(lib, validate):
     for p in solvers:
         lib.pga_comm_set_validation(p, validate)
     lib.pga_run_islands_multi(arr, 2, 3, 1, 0.05)
+    assert lib.pga_comm_exchange(arr, 2, 0.05) == 0  # one more epoch, observed on arrival
     best = max(lib.pga_best_score(p, q) for p, q in zip(solvers, pops))
     if validate:
         assert best <= LEN  # a forged fitness never enters
     else:
-        assert best > 1e37  # without re-scoring it would
+        assert best > 1e37  # without re-scoring it does
+    # the next generation re-evaluates every child from its genome (elites
+    # included), so an unvalidated forged fitness does not outlive it
+    lib.pga_run_islands_multi(arr, 2, 1, 0, 0.05)
+    assert max(lib.pga_best_score(p, q) for p, q in zip(solvers, pops)) <= LEN
     for p in solvers:
         lib.pga_deinit(p)
 

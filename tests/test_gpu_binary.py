@@ -71,6 +71,18 @@ def test_mutation_modes_bitexact(mut):
     same(g, c)
 
 
+@pytest.mark.parametrize("L,S,rate", [(1000, 100000, 0.0015), (64, 20000, 1.5 / 64), (8192, 3000, None), (200, 5000, None)])
+def test_sparse_mutation_bitexact(L, S, rate):
+    """Sparse bit-flip sampler (L*p <= 1.5): the transposed kernel's record
+    positions, its sequential fallback and the K > 8 group continuation (about
+    3 children per generation at S=100000, L*p=1.5) against the CPU."""
+    kw = {} if rate is None else {"mutation_rate": rate}
+    g, c = pair(pga.models.OneMax(L), S, elitism=1, **kw)
+    g.run(2)
+    c.run(2)
+    same(g, c)
+
+
 def test_staged_equals_fused_gpu():
     a = pga.GeneticAlgorithm(pga.models.OneMax(1024), 2048, seed=4, device=DEV)
     b = pga.GeneticAlgorithm(pga.models.OneMax(1024), 2048, seed=4, device=DEV)
