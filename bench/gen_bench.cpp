@@ -14,11 +14,6 @@
 #include "pga/island.hpp"
 #include "pga/ops.hpp"
 
-#ifdef PGA_STAMP
-namespace pga {
-void pga_stamp_report(uint32_t nwaves);
-}
-#endif
 
 int main(int argc, char** argv) {
   pga::Config c;
@@ -57,9 +52,6 @@ int main(int argc, char** argv) {
   float ms = 0.f;
   PGA_HIP_CHECK(hipEventElapsedTime(&ms, e0, e1));
   const double us = 1000.0 * ms / gens;
-#ifdef PGA_STAMP
-  pga::pga_stamp_report(PGA_STAMP);
-#endif
   std::printf("{\"pop\": %llu, \"length\": %u, \"gens\": %d, \"us_per_gen\": %.2f, \"gens_per_sec\": %.1f, "
               "\"evals_per_sec\": %.4e, \"best\": %.1f}\n",
               (unsigned long long)c.S, c.L, gens, us, 1e6 / us, 1e6 / us * (double)c.S, isl.best_score());

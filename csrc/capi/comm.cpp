@@ -14,7 +14,8 @@
 namespace pga {
 
 uint32_t plan_migrants(int topology, int nranks, uint32_t k) {
-  if (nranks <= 1 || k == 0) return 0;
+  if (nranks < 1 || k == 0) return 0;
+  if (nranks == 1) return k;  // self-exchange (fault-injection test mode)
   if (topology == TOPO_ALL_TO_ALL) {
     const uint32_t peers = (uint32_t)nranks - 1;
     return std::max<uint32_t>(1, k / peers) * peers;
@@ -24,7 +25,8 @@ uint32_t plan_migrants(int topology, int nranks, uint32_t k) {
 
 std::vector<Xfer> migration_plan(int topology, int nranks, uint32_t k, uint64_t seed, uint32_t epoch) {
   std::vector<Xfer> plan;
-  if (nranks <= 1 || k == 0) return plan;
+  if (nranks < 1 || k == 0) return plan;
+  if (nranks == 1) return {{0, 0, 0, 0, k}};  // a 1-rank ring: to itself
   const int n = nranks;
   if (topology == TOPO_ALL_TO_ALL) {
     // rank r's j-th peer (peers in rank order, r skipped) gets slice j of r's
@@ -111,9 +113,11 @@ class LoopbackComm final : public Comm {
     return all;
   }
 
-  void set_fault(int every, int mode) {
+  void set_fault(int every, int mode) override {
+    if (mode < 0 || mode > 2) throw std::invalid_argument("loopback fault mode must be 0 (none), 1 (drop) or 2 (corrupt)");
     every_ = every;
     mode_ = mode;
+    self_exchange = true;
   }
 
  private:
@@ -130,10 +134,5 @@ std::shared_ptr<Comm> loopback_comm(int nranks) {
   return std::make_shared<LoopbackComm>(nranks);
 }
 
-void loopback_set_fault(Comm* c, int every, int mode) {
-  auto* l = dynamic_cast<LoopbackComm*>(c);
-  if (!l) throw std::invalid_argument("fault injection needs the loopback transport");
-  l->set_fault(every, mode);
-}
 
 }  // namespace pga

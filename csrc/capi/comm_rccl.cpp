@@ -44,83 +44,111 @@ class RcclComm final : public Comm {
   // in InitRank mode, one per GPU in InitAll mode)
   RcclComm(std::vector<ncclComm_t> comms, std::vector<int> ranks, int nranks, bool all)
       : comms_(std::move(comms)), ranks_(std::move(ranks)), n_(nranks), all_(all) {
-    events_.resize(comms_.size(), nullptr);
+    ready_.resize(comms_.size(), nullptr);
+    done_.resize(comms_.size(), nullptr);
+    streams_.resize(comms_.size(), nullptr);
   }
   ~RcclComm() override {
-    for (hipEvent_t e : events_)
-      if (e) (void)hipEventDestroy(e);
-    for (ncclComm_t c : comms_)
-      if (c) (aborted_ ? ncclCommAbort(c) : ncclCommDestroy(c));
+    for (auto* v : {&ready_, &done_})
+      for (hipEvent_t e : *v)
+        if (e) (void)hipEventDestroy(e);
+    if (!aborted_)
+      for (ncclComm_t c : comms_)
+        if (c) (void)ncclCommDestroy(c);
+    // after an abort the communication streams may still hold the aborted
+    // kernels' completions; they are released with the device context
+    if (!aborted_)
+      for (hipStream_t st : streams_)
+        if (st) (void)hipStreamDestroy(st);
   }
   int size() const override { return n_; }
   const char* name() const override { return all_ ? "rccl-all" : "rccl"; }
   bool drives_all_ranks() const override { return all_; }
 
+  void set_fault(int every, int mode) override {
+    if (mode != 0 && mode != 3) throw std::invalid_argument("RCCL fault mode must be 0 (none) or 3 (withhold sends)");
+    every_ = every;
+    mode_ = mode;
+    self_exchange = true;
+  }
+
+  // The emigrants are packed on each rank's compute stream; the transfers
+  // run on the rank's own communication stream, which waits for them.  The
+  // compute stream is NOT ordered after the transfer here: wait() decides.
   void exchange(const std::vector<Xfer>& plan, std::vector<LocalRank>& local) override {
     if (aborted_) throw std::runtime_error("RCCL communicator was aborted");
+    ++count_;
+    const bool withhold = mode_ == 3 && every_ > 0 && count_ % (uint64_t)every_ == 0;
+    for (LocalRank& l : local) {
+      const size_t j = slot_of(l.rank);
+      PGA_COMM_HIP(hipSetDevice(l.device));
+      if (!streams_[j]) {
+        PGA_COMM_HIP(hipStreamCreateWithFlags(&streams_[j], hipStreamNonBlocking));
+        PGA_COMM_HIP(hipEventCreateWithFlags(&ready_[j], hipEventDisableTiming));
+        PGA_COMM_HIP(hipEventCreateWithFlags(&done_[j], hipEventDisableTiming));
+      }
+      PGA_COMM_HIP(hipEventRecord(ready_[j], l.stream));
+      PGA_COMM_HIP(hipStreamWaitEvent(streams_[j], ready_[j], 0));
+    }
     {
       Group g;
       for (LocalRank& l : local) {
         ncclComm_t c = comm_of(l.rank);
+        hipStream_t cs = streams_[slot_of(l.rank)];
         const size_t rb = l.row_bytes;
         for (const Xfer& x : plan) {
-          if (x.src == l.rank) {
-            nccl_check(ncclSend((const char*)l.send_rows + rb * x.src_off, rb * x.n, ncclUint8, x.dst, c, l.stream),
+          if (x.src == l.rank && !withhold) {
+            nccl_check(ncclSend((const char*)l.send_rows + rb * x.src_off, rb * x.n, ncclUint8, x.dst, c, cs),
                        "ncclSend");
-            nccl_check(ncclSend(l.send_scores + x.src_off, x.n, ncclFloat32, x.dst, c, l.stream), "ncclSend");
+            nccl_check(ncclSend(l.send_scores + x.src_off, x.n, ncclFloat32, x.dst, c, cs), "ncclSend");
             bytes_sent += (rb + 4) * x.n;
           }
           if (x.dst == l.rank) {
-            nccl_check(ncclRecv((char*)l.recv_rows + rb * x.dst_off, rb * x.n, ncclUint8, x.src, c, l.stream),
-                       "ncclRecv");
-            nccl_check(ncclRecv(l.recv_scores + x.dst_off, x.n, ncclFloat32, x.src, c, l.stream), "ncclRecv");
+            nccl_check(ncclRecv((char*)l.recv_rows + rb * x.dst_off, rb * x.n, ncclUint8, x.src, c, cs), "ncclRecv");
+            nccl_check(ncclRecv(l.recv_scores + x.dst_off, x.n, ncclFloat32, x.src, c, cs), "ncclRecv");
           }
         }
       }
     }
-    for (size_t i = 0; i < local.size(); ++i) {
-      const size_t j = slot_of(local[i].rank);
-      if (!events_[j]) {
-        PGA_COMM_HIP(hipSetDevice(local[i].device));
-        PGA_COMM_HIP(hipEventCreateWithFlags(&events_[j], hipEventDisableTiming));
-      }
-      PGA_COMM_HIP(hipEventRecord(events_[j], local[i].stream));
+    for (LocalRank& l : local) {
+      const size_t j = slot_of(l.rank);
+      PGA_COMM_HIP(hipSetDevice(l.device));
+      PGA_COMM_HIP(hipEventRecord(done_[j], streams_[j]));
     }
   }
 
-  // Poll the exchange's completion events and RCCL's asynchronous error
-  // state; on an error or after timeout_s, abort the communicators so no
-  // rank stays blocked in a transfer whose peer is gone.
+  // timeout_s > 0: poll the transfers' completion events and RCCL's
+  // asynchronous error state on the host until the deadline.  Success: the
+  // compute streams wait for the transfers (the received rows are consumed
+  // there).  Failure or expiry: ncclCommAbort now — it releases RCCL kernels
+  // blocked on a dead peer — and the compute streams are left alone.
+  // timeout_s <= 0: no host wait at all; only errors RCCL already reported
+  // are seen, and the compute streams are ordered after the transfers.
   bool wait(std::vector<LocalRank>& local, double timeout_s) override {
     if (aborted_) return false;
-    if (timeout_s <= 0) {  // asynchronous mode: only surface errors RCCL already saw
-      for (ncclComm_t c : comms_) {
-        ncclResult_t st = ncclSuccess;
-        if (ncclCommGetAsyncError(c, &st) != ncclSuccess || (st != ncclSuccess && st != ncclInProgress))
-          return abort_all();
+    if (timeout_s > 0) {
+      const auto t0 = std::chrono::steady_clock::now();
+      for (;;) {
+        bool done = true;
+        for (const LocalRank& l : local) {
+          const hipError_t q = hipEventQuery(done_[slot_of(l.rank)]);
+          if (q == hipErrorNotReady) done = false;
+          else if (q != hipSuccess) return abort_all();
+        }
+        if (async_error()) return abort_all();
+        if (done) break;
+        const double dt = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        if (dt > timeout_s) return abort_all();
+        std::this_thread::sleep_for(std::chrono::microseconds(50));
       }
-      return true;
+    } else if (async_error()) {
+      return abort_all();
     }
-    const auto t0 = std::chrono::steady_clock::now();
-    for (;;) {
-      bool done = true;
-      for (const LocalRank& l : local) {
-        hipEvent_t e = events_[slot_of(l.rank)];
-        if (!e) continue;
-        const hipError_t q = hipEventQuery(e);
-        if (q == hipErrorNotReady) done = false;
-        else if (q != hipSuccess) return abort_all();
-      }
-      for (ncclComm_t c : comms_) {
-        ncclResult_t st = ncclSuccess;
-        if (ncclCommGetAsyncError(c, &st) != ncclSuccess || (st != ncclSuccess && st != ncclInProgress))
-          return abort_all();
-      }
-      if (done) return true;
-      const double dt = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-      if (dt > timeout_s) return abort_all();
-      std::this_thread::sleep_for(std::chrono::microseconds(50));
+    for (LocalRank& l : local) {
+      PGA_COMM_HIP(hipSetDevice(l.device));
+      PGA_COMM_HIP(hipStreamWaitEvent(l.stream, done_[slot_of(l.rank)], 0));
     }
+    return true;
   }
 
   std::vector<float> allgather(const std::vector<LocalRank>& local, const std::vector<float>& mine) override {
@@ -153,17 +181,30 @@ class RcclComm final : public Comm {
     throw std::runtime_error("rank " + std::to_string(rank) + " is not local to this communicator");
   }
   ncclComm_t comm_of(int rank) const { return comms_[slot_of(rank)]; }
+  bool async_error() const {
+    for (ncclComm_t c : comms_) {
+      ncclResult_t st = ncclSuccess;
+      if (ncclCommGetAsyncError(c, &st) != ncclSuccess || (st != ncclSuccess && st != ncclInProgress)) return true;
+    }
+    return false;
+  }
   bool abort_all() {
+    if (!aborted_)
+      for (ncclComm_t c : comms_)
+        if (c) (void)ncclCommAbort(c);
     aborted_ = true;
     return false;
   }
 
   std::vector<ncclComm_t> comms_;
   std::vector<int> ranks_;
-  std::vector<hipEvent_t> events_;
+  std::vector<hipEvent_t> ready_, done_;
+  std::vector<hipStream_t> streams_;  // one communication stream per local rank
   int n_;
   bool all_;
   bool aborted_ = false;
+  uint64_t count_ = 0;
+  int every_ = 0, mode_ = 0;
 };
 
 }  // namespace

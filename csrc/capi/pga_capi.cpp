@@ -40,7 +40,21 @@ struct pga_population {
   pga_t* owner = nullptr;
   hipStream_t stream = nullptr;  // own stream: islands of pga_run_islands evolve concurrently
   hipEvent_t done = nullptr;
+  // persistent emigrant staging of intra-solver migration (grown, never freed
+  // per call: hipFree would synchronise the whole device)
+  void* emi_rows = nullptr;
+  float* emi_scores = nullptr;
+  uint32_t emi_cap = 0;
   ~pga_population() {
+    if (emi_rows && isl) {
+      if (isl->on_gpu()) {
+        (void)hipFree(emi_rows);
+        (void)hipFree(emi_scores);
+      } else {
+        std::free(emi_rows);
+        std::free(emi_scores);
+      }
+    }
     if (done) (void)hipEventDestroy(done);
     if (stream) (void)hipStreamDestroy(stream);
   }
@@ -167,37 +181,37 @@ void dev_free(pga::Island& isl, void* ptr) {
   else std::free(ptr);
 }
 
-struct Emigrants {
-  uint32_t k = 0;
-  void* rows = nullptr;
-  float* scores = nullptr;
-};
+// Intra-solver migration, fully stream-ordered on the solver stream: the
+// top-k emigrants of a population go to its own persistent staging, the
+// destination's bottom-k are replaced from there.  No allocation, free or host
+// synchronisation per call, so concurrent island streams are not serialised.
+void ensure_emigrant_staging(population_t* pop, uint32_t k) {
+  if (pop->emi_cap >= k) return;
+  pga::Island& isl = *pop->isl;
+  if (pop->emi_rows) {
+    isl.synchronize();  // a previous epoch may still read the old staging
+    dev_free(isl, pop->emi_rows);
+    dev_free(isl, pop->emi_scores);
+  }
+  pop->emi_rows = pop->emi_scores = nullptr;
+  pop->emi_cap = 0;
+  pop->emi_rows = dev_alloc(isl, isl.row_bytes() * k);
+  pop->emi_scores = (float*)dev_alloc(isl, 4ull * k);
+  pop->emi_cap = k;
+}
 
-Emigrants take_best(pga::Island& isl, uint32_t k) {
-  Emigrants e;
-  e.k = k;
-  uint32_t* idx = (uint32_t*)dev_alloc(isl, 4ull * k);
-  e.rows = dev_alloc(isl, isl.row_bytes() * k);
-  e.scores = (float*)dev_alloc(isl, 4ull * k);
+void take_best(population_t* pop, uint32_t k) {
+  ensure_emigrant_staging(pop, k);
+  pga::Island& isl = *pop->isl;
+  uint32_t* idx = (uint32_t*)isl.scratch(4ull * k);
   isl.topk(k, true, idx, false);
-  isl.gather(idx, k, e.rows, e.scores);
-  isl.synchronize();
-  dev_free(isl, idx);
-  return e;
+  isl.gather(idx, k, pop->emi_rows, pop->emi_scores);
 }
 
-void replace_worst(pga::Island& isl, Emigrants& e) {
-  uint32_t* idx = (uint32_t*)dev_alloc(isl, 4ull * e.k);
-  isl.topk(e.k, false, idx, false);
-  isl.scatter(idx, e.k, e.rows, e.scores);
-  isl.synchronize();
-  dev_free(isl, idx);
-}
-
-void free_emigrants(pga::Island& isl, Emigrants& e) {
-  dev_free(isl, e.rows);
-  dev_free(isl, e.scores);
-  e = Emigrants();
+void replace_worst(pga::Island& isl, const population_t* from, uint32_t k) {
+  uint32_t* idx = (uint32_t*)isl.scratch(4ull * k);
+  isl.topk(k, false, idx, false);
+  isl.scatter(idx, k, from->emi_rows, from->emi_scores);
 }
 
 int default_device() {
@@ -554,9 +568,8 @@ void pga_migrate_between(pga_t* p, population_t* from, population_t* to, float p
     a.stream = b.stream = p->stream;
     const uint32_t k = migrants(a.config().S, b.config().S, pct);
     if (!k) return;
-    Emigrants e = take_best(a, k);
-    replace_worst(b, e);
-    free_emigrants(a, e);
+    take_best(from, k);
+    replace_worst(b, from, k);
   });
 }
 
@@ -573,21 +586,20 @@ void pga_migrate(pga_t* p, float pct) {
       const uint32_t j = pga::word_to_index(pga::draw(key, pga::ST_MIGRATE, 0, i).x, i + 1);
       std::swap(perm[i], perm[j]);
     }
-    std::vector<Emigrants> out(n);
+    std::vector<uint32_t> ks(n, 0);
     for (size_t i = 0; i < n; ++i) {
       population_t* src = p->pops[perm[i]];
       population_t* dst = p->pops[perm[(i + 1) % n]];
       src->isl->stream = p->stream;
-      const uint32_t k = migrants(src->isl->config().S, dst->isl->config().S, pct);
-      if (k) out[i] = take_best(*src->isl, k);
+      ks[i] = migrants(src->isl->config().S, dst->isl->config().S, pct);
+      if (ks[i]) take_best(src, ks[i]);
     }
     for (size_t i = 0; i < n; ++i) {
       population_t* dst = p->pops[perm[(i + 1) % n]];
-      if (out[i].k) {
+      if (ks[i]) {
         dst->isl->stream = p->stream;
-        replace_worst(*dst->isl, out[i]);
+        replace_worst(*dst->isl, p->pops[perm[i]], ks[i]);
       }
-      free_emigrants(*p->pops[perm[i]]->isl, out[i]);
     }
   });
 }
@@ -621,7 +633,8 @@ void ensure_staging(pga_t* p, pga::Island& isl, uint32_t k) {
 // so the exchange overlaps whatever the GPUs run next.
 void migrate_ranks(const std::vector<pga_t*>& solvers, float pct) {
   pga_t* p0 = solvers.front();
-  if (!p0->comm || p0->comm->size() == 1 || p0->degraded) return;
+  // a 1-rank communicator exchanges only in fault-injection (test) mode
+  if (!p0->comm || (p0->comm->size() == 1 && !p0->comm->self_exchange) || p0->degraded) return;
   pga::Comm& comm = *p0->comm;
   const uint64_t S = p0->pops[0]->isl->config().S;
   const uint32_t k0 = migrants(S, S, pct);
@@ -954,7 +967,7 @@ int pga_comm_info(const pga_t* p, struct pga_comm_stats* out) {
 int pga_comm_set_fault(pga_t* p, int every, int mode) {
   if (!p || !p->comm) return -1;
   return guard_r<int>(p, -1, [&]() {
-    pga::loopback_set_fault(p->comm.get(), every, mode);
+    p->comm->set_fault(every, mode);
     return 0;
   });
 }

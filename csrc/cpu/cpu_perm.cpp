@@ -15,6 +15,35 @@
 namespace pga {
 namespace cpu {
 
+// PMX / OX1 child of parents A and B with A's segment [lo, hi) (the kernels'
+// LDS versions compute the same child; tests/test_perm.py pins both against
+// the textbook examples)
+void perm_crossover(int op, const uint16_t* A, const uint16_t* B, uint32_t L, uint32_t lo, uint32_t hi, uint16_t* C) {
+  std::vector<int32_t> M(L, -1);  // city -> its position in A's segment
+  for (uint32_t k = lo; k < hi; ++k) M[A[k]] = (int32_t)k;
+  std::fill(C, C + L, 0);
+  if (op == XO_PMX) {
+    for (uint32_t p = 0; p < L; ++p) {
+      if (p >= lo && p < hi) {
+        C[p] = A[p];
+      } else {
+        uint32_t v = B[p];
+        for (uint32_t guard = 0; M[v] >= 0 && guard < L; ++guard) v = B[M[v]];
+        C[p] = (uint16_t)v;
+      }
+    }
+  } else {  // OX1: fill from the segment end, B in order from the segment end
+    for (uint32_t k = lo; k < hi; ++k) C[k] = A[k];
+    uint32_t pos = hi % L;
+    for (uint32_t t = 0; t < L; ++t) {
+      const uint32_t p = (hi + t) % L;
+      if (M[B[p]] >= 0) continue;
+      C[pos] = B[p];  // free positions: hi .. L-1, then 0 .. lo-1 (exactly L - (hi - lo) of them)
+      pos = (pos + 1) % L;
+    }
+  }
+}
+
 uint32_t perm_run(int mode, const GenArgs& a, unsigned long long* best_parts) {
   if (a.L > kPermMaxL) throw std::invalid_argument("PERMUTATION encoding supports at most 4096 genes");
   const uint32_t L = a.L, nch = a.chunks, lp = 8 * nch, GS = group_size(nch);
@@ -29,7 +58,6 @@ uint32_t perm_run(int mode, const GenArgs& a, unsigned long long* best_parts) {
   if (gen && a.n_elite > 0 && a.elite_idx == nullptr) elite0 = (uint32_t)best_index(reduce_best(a.best_cur, a.n_best_cur));
 
   std::vector<uint16_t> A(lp), B(lp), C(lp);
-  std::vector<int32_t> M(lp);
   unsigned long long best = 0;
   for (uint64_t child = 0; child < a.S; ++child) {
     bool elite = false;
@@ -60,29 +88,7 @@ uint32_t perm_run(int mode, const GenArgs& a, unsigned long long* best_parts) {
         C = A;
       } else {
         std::memcpy(B.data(), cur + (uint64_t)pb * rh, 2ull * lp);
-        std::fill(M.begin(), M.end(), -1);
-        for (uint32_t k = lo; k < hi; ++k) M[A[k]] = (int32_t)k;
-        std::fill(C.begin(), C.end(), 0);
-        if (a.crossover == XO_PMX) {
-          for (uint32_t p = 0; p < L; ++p) {
-            if (p >= lo && p < hi) {
-              C[p] = A[p];
-            } else {
-              uint32_t v = B[p];
-              for (uint32_t guard = 0; M[v] >= 0 && guard < L; ++guard) v = B[M[v]];
-              C[p] = (uint16_t)v;
-            }
-          }
-        } else {  // OX1: fill from the segment end, B in order from the segment end
-          for (uint32_t k = lo; k < hi; ++k) C[k] = A[k];
-          uint32_t pos = hi % L;
-          for (uint32_t t = 0; t < L; ++t) {
-            const uint32_t p = (hi + t) % L;
-            if (M[B[p]] >= 0) continue;
-            C[pos] = B[p];  // free positions: hi .. L-1, then 0 .. lo-1 (exactly K of them)
-            pos = (pos + 1) % L;
-          }
-        }
+        perm_crossover(a.crossover, A.data(), B.data(), L, lo, hi, C.data());
       }
     }
     if (!elite && mut_on && pool_word(a.key, child, W_MUTIND) < a.mut_ind_thresh) {

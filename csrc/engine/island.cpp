@@ -409,7 +409,7 @@ void Island::topk(uint32_t k, bool largest, uint32_t* idx_out, bool sorted) {
       synchronize();
       release(topk_ws_);
       topk_ws_ = alloc(need);
-      PGA_HIP_CHECK(hipMemset(topk_ws_.ptr, 0, need));  // the value histogram must start zeroed
+      PGA_HIP_CHECK(hipMemsetAsync(topk_ws_.ptr, 0, need, stream));  // the value histogram must start zeroed
     }
     const uint16_t* k16 = integer_objective(cfg_.objective, cfg_.L) ? (const uint16_t*)keys_[cur_].ptr : nullptr;
     topk_launch(sc, k16, cfg_.L + 1, cfg_.S, k, largest, sorted, idx_out, topk_ws_.ptr, stream);

@@ -16,9 +16,12 @@
 //
 // Plans are computed identically on every rank from (topology, epoch, seed),
 // so no rank ever has to tell another whom it talks to.  Transfers are
-// stream-ordered and asynchronous; Comm::wait() is the optional host-side
-// completion check with a timeout (RCCL: event polling +
-// ncclCommGetAsyncError, ncclCommAbort on expiry).
+// asynchronous.  RCCL posts them on a dedicated communication stream per
+// rank that first waits for the emigrants packed on the compute stream;
+// Comm::wait() then either makes the compute stream wait for the transfer
+// (success) or, on a timeout / asynchronous error, calls ncclCommAbort at
+// once and leaves the compute stream untouched, so a dead peer can never
+// stall the generations that follow (the islands continue degraded).
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -78,6 +81,12 @@ class Comm {
   virtual bool wait(std::vector<LocalRank>& local, double timeout_s) = 0;
   // one float per rank; `local[i]` contributes mine[i]; returns all ranks' values
   virtual std::vector<float> allgather(const std::vector<LocalRank>& local, const std::vector<float>& mine) = 0;
+  // test-only fault injection (pga_comm_set_fault): loopback drops (1) or
+  // corrupts (2) every `every`-th exchange; RCCL withholds this process's
+  // sends (3) of every `every`-th exchange, so its receives can never
+  // complete.  Arming it also lets a 1-rank communicator exchange with itself.
+  virtual void set_fault(int every, int mode) = 0;
+  bool self_exchange = false;
   uint64_t bytes_sent = 0;
 };
 
@@ -92,6 +101,5 @@ std::shared_ptr<Comm> rccl_comm_all(const std::vector<int>& devices);
 // (mode 2: the received scores are overwritten with +3e38, which re-scoring
 // must undo)
 std::shared_ptr<Comm> loopback_comm(int nranks);
-void loopback_set_fault(Comm* c, int every, int mode);
 
 }  // namespace pga

@@ -19,6 +19,8 @@ uint32_t encoding_run(int mode, const GenArgs& a, unsigned long long* best_parts
 uint32_t binary_run(int mode, const GenArgs& a, unsigned long long* best_parts);
 uint32_t real_run(int mode, const GenArgs& a, unsigned long long* best_parts);
 uint32_t perm_run(int mode, const GenArgs& a, unsigned long long* best_parts);
+// PMX (op = XO_PMX) or OX1 child of A and B keeping A's segment [lo, hi)
+void perm_crossover(int op, const uint16_t* A, const uint16_t* B, uint32_t L, uint32_t lo, uint32_t hi, uint16_t* C);
 
 unsigned long long reduce_best(const unsigned long long* parts, uint32_t n);
 unsigned long long best_of_scores(const float* scores, uint64_t S);

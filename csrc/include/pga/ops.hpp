@@ -39,6 +39,9 @@ uint32_t launch_grid(uint64_t S, uint32_t per_block);
 uint32_t launch_grid_occ(uint64_t S, uint32_t per_block, const void* kernel);
 uint32_t occupancy_blocks(const void* kernel, int block);
 int device_cu_count();
+// PGA_FORCE_GENERIC=1: every encoding runs its generic (non-pipelined) GEN
+// kernel.  Verification / debugging only: the fast kernels are bit-identical.
+bool force_generic_kernels();
 
 // ---- encodings: one launch per call, returns the grid used (= number of
 // valid entries written to best_parts, when the mode evaluates) ----

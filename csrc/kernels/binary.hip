@@ -618,7 +618,7 @@ uint32_t launch_mode(int mode, const GenArgs& a, unsigned long long* parts, hipS
     case MODE_GEN: {
       const bool fast = a.chunks <= (uint32_t)GS &&
                         ((a.selection == SEL_TOURNAMENT && a.tour_k == 2) || a.selection == SEL_RANDOM) &&
-                        !(a.n_elite > 1 && a.elite_idx == nullptr);
+                        !(a.n_elite > 1 && a.elite_idx == nullptr) && !force_generic_kernels();
       constexpr bool INT_OBJ = OBJ == OBJ_ONEMAX || OBJ == OBJ_LEADING_ONES || OBJ == OBJ_TRAP;
       // 32-bit offsets: the (S + kRowPad)-row buffers must stay below 4 GiB
       const bool o32 = (a.S + kRowPad) * (uint64_t)a.row_words * 4u <= 0xFFFFFFFFull;

@@ -482,15 +482,6 @@ __global__ __launch_bounds__(kBlock) void perm_gen_fast(GenArgs a, unsigned long
   }
 }
 
-bool perm_fast_enabled() {
-  static int v = -1;
-  if (v < 0) {
-    const char* e = getenv("PGA_PERM_FAST");
-    v = (e && e[0] == '0') ? 0 : 1;
-  }
-  return v == 1;
-}
-
 template <int GS, int MODE, int OBJ>
 uint32_t go(const GenArgs& a, unsigned long long* parts, hipStream_t s) {
   const size_t lds = perm_lds_bytes(GS, a.chunks, OBJ == OBJ_TSP_EUC);
@@ -537,7 +528,7 @@ template <int GS, int OBJ>
 uint32_t launch_mode(int mode, const GenArgs& a, unsigned long long* parts, hipStream_t s) {
   switch (mode) {
     case MODE_GEN:
-      if (OBJ != OBJ_NONE && a.chunks <= (uint32_t)GS && perm_fast_enabled()) return go_fast<GS, OBJ>(a, parts, s);
+      if (OBJ != OBJ_NONE && a.chunks <= (uint32_t)GS && !force_generic_kernels()) return go_fast<GS, OBJ>(a, parts, s);
       return go<GS, MODE_GEN, OBJ>(a, parts, s);
     case MODE_INIT: return go<GS, MODE_INIT, OBJ>(a, parts, s);
     case MODE_EVAL: return go<GS, MODE_EVAL, OBJ>(a, parts, s);

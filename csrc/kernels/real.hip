@@ -834,20 +834,8 @@ uint32_t go_fast(const GenArgs& a, unsigned long long* parts, hipStream_t s) {
   return launch_occ(real_gen_fast<GS, U, ROT>, ROWS, lds, a, parts, s, c);
 }
 
-// PGA_REAL_FAST=0 forces the generic kernel; PGA_REAL_U = 1|2|4 children per group
-int real_fast_u() {
-  static int v = -2;
-  if (v == -2) {
-    const char* e = getenv("PGA_REAL_FAST");
-    const char* u = getenv("PGA_REAL_U");
-    v = (e && e[0] == '0') ? 0 : (u ? atoi(u) : 1);
-    if (v != 0 && v != 1 && v != 2 && v != 4) v = 1;
-  }
-  return v;
-}
-
 bool real_fast_eligible(int mode, const GenArgs& a, bool rot) {
-  if (mode != MODE_GEN || real_fast_u() == 0) return false;
+  if (mode != MODE_GEN || force_generic_kernels()) return false;
   if (a.objective == OBJ_USER_FNPTR || a.objective == OBJ_TSP_RANDOM_KEY) return false;
   if (a.objective == OBJ_ROSENBROCK && !rot) return false;
   if (!(a.selection == SEL_RANDOM || (a.selection == SEL_TOURNAMENT && a.tour_k == 2))) return false;
@@ -855,19 +843,10 @@ bool real_fast_eligible(int mode, const GenArgs& a, bool rot) {
   return true;
 }
 
-bool real_pipe_enabled() {
-  static int v = -1;
-  if (v < 0) {
-    const char* e = getenv("PGA_REAL_PIPE");
-    v = (e && e[0] == '0') ? 0 : 1;
-  }
-  return v == 1;
-}
-
 template <int GS, bool ROT>
 uint32_t launch_fast(const GenArgs& a, unsigned long long* parts, hipStream_t s) {
   if constexpr (ROT && (GS == 4 || GS == 8)) {
-    if (real_pipe_enabled()) {
+    {
       static bool c[6] = {false, false, false, false, false, false};
       switch (a.objective) {
         case OBJ_SPHERE: return launch_occ(real_gen_pipe<GS, OBJ_SPHERE, true>, kBlock / GS, 0, a, parts, s, c[0]);
@@ -884,7 +863,7 @@ uint32_t launch_fast(const GenArgs& a, unsigned long long* parts, hipStream_t s)
       }
     }
   }
-  if (!ROT && real_pipe_enabled()) {
+  if (!ROT) {
     static bool c[8] = {false, false, false, false, false, false, false, false};
     switch (a.objective) {
       case OBJ_SPHERE: return launch_occ(real_gen_pipe<GS, OBJ_SPHERE>, kBlock / GS, 0, a, parts, s, c[0]);
@@ -899,12 +878,7 @@ uint32_t launch_fast(const GenArgs& a, unsigned long long* parts, hipStream_t s)
       default: break;  // Rosenbrock needs the neighbouring dimension: fast path below
     }
   }
-  switch (real_fast_u()) {
-    case 1: return go_fast<GS, 1, ROT>(a, parts, s);
-    case 4: return go_fast<GS, 4, ROT>(a, parts, s);
-    case 2: return go_fast<GS, 2, ROT>(a, parts, s);
-    default: return go_fast<GS, 1, ROT>(a, parts, s);
-  }
+  return go_fast<GS, 1, ROT>(a, parts, s);
 }
 
 template <int GS, bool ROT>

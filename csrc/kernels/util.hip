@@ -52,6 +52,14 @@ uint32_t occupancy_blocks(const void* kernel, int block) {
   return (uint32_t)n;
 }
 
+bool force_generic_kernels() {
+  static const bool v = [] {
+    const char* e = getenv("PGA_FORCE_GENERIC");
+    return e && e[0] == '1';
+  }();
+  return v;
+}
+
 uint32_t launch_grid_occ(uint64_t S, uint32_t per_block, const void* kernel) {
   uint64_t need = (S + per_block - 1) / per_block;
   uint64_t cap = (uint64_t)device_cu_count() * occupancy_blocks(kernel, dev::kBlock);
@@ -107,7 +115,7 @@ __global__ __launch_bounds__(kBlock) void best_of_scores_kernel(const float* sco
     const float v = scores[i];
     unsigned long long p = pack_best(v, i);
     b = p > b ? p : b;
-    if (keys) keys[i] = (uint16_t)(v <= 0.f ? 0.f : (v >= 65535.f ? 65535.f : v));
+    if (keys) keys[i] = (uint16_t)(!(v > 0.f) ? 0.f : (v >= 65535.f ? 65535.f : v));
   }
   b = block_max_u64(b, lds);
   if (threadIdx.x == 0) parts[blockIdx.x] = b;
@@ -250,14 +258,19 @@ __device__ __forceinline__ uint32_t topk_key(float s, bool largest) {
 
 // Keys of the selection: 32-bit orderable f32 keys, or (integer objectives)
 // the population's u16 tournament keys — two radix passes instead of four.
+// u16 keys are clamped to vmax (= R - 1 of a value-histogram selection) in
+// every pass, exactly as the histogram bins them: a key above the objective's
+// range (a checkpoint's or an unvalidated migrant's score) can then neither
+// make the passes disagree nor write past k indices.
 template <int BITS>
 struct TopkKeys {
   const float* s;
   const uint16_t* k16;
   bool largest;
+  uint32_t vmax = 0xFFFFu;
   __device__ __forceinline__ uint32_t operator()(uint64_t i) const {
     if (BITS == 16) {
-      const uint32_t v = k16[i];
+      const uint32_t v = min((uint32_t)k16[i], vmax);
       return largest ? v : 0xFFFFu - v;
     }
     return topk_key(s[i], largest);
@@ -437,7 +450,7 @@ __global__ __launch_bounds__(kBlock) void topk16_count_kernel(const uint16_t* k1
     st->prefix = T;
     st->remaining = sh_need;
   }
-  const TopkKeys<16> keys{nullptr, k16, largest};
+  const TopkKeys<16> keys{nullptr, k16, largest, R - 1};
   const uint64_t b0 = (uint64_t)blockIdx.x * per_block;
   const uint64_t b1 = b0 + per_block < S ? b0 + per_block : S;
   uint32_t gt = 0, eq = 0;
@@ -598,7 +611,7 @@ __global__ __launch_bounds__(kBlock) void topk16_select_kernel(const uint16_t* k
     const uint32_t m = load_keys16(k16, c0, t1, kv);
 #pragma unroll
     for (int e = 0; e < 16; ++e) {
-      const uint32_t key = kv[e] ^ flip;
+      const uint32_t key = min(kv[e], R - 1) ^ flip;  // as the histogram bins it
       gt += ((m >> e) & 1u) && key > T;
       eq += ((m >> e) & 1u) && key == T;
     }
@@ -635,8 +648,8 @@ __global__ __launch_bounds__(kBlock) void topk16_select_kernel(const uint16_t* k
 #pragma unroll
     for (int e = 0; e < 16; ++e) {
       if (!((m >> e) & 1u)) continue;
-      const uint32_t key = kv[e] ^ flip;
-      if (key > T) idx_out[gpos++] = (uint32_t)(c0 + e);
+      const uint32_t key = min(kv[e], R - 1) ^ flip;
+      if (key > T && gpos < gt_total) idx_out[gpos++] = (uint32_t)(c0 + e);
       if (key == T) {
         if (epos < need_eq) idx_out[gt_total + epos] = (uint32_t)(c0 + e);
         ++epos;
@@ -665,7 +678,7 @@ __global__ __launch_bounds__(kBlock) void topk_write_kernel(TopkKeys<BITS> keys,
     uint32_t rg = block_excl_scan_u(isg, lds, tg);
     __syncthreads();
     uint32_t re = block_excl_scan_u(ise, lds, te);
-    if (isg) {
+    if (isg && gpos + rg < gt_total) {
       if (keys_out) keys_out[gpos + rg] = key;
       idx_out[gpos + rg] = (uint32_t)i;
     }
@@ -706,7 +719,7 @@ __global__ __launch_bounds__(kBlock) void scatter_rows_kernel(uint4* rows, float
 __global__ __launch_bounds__(kBlock) void scores_to_keys_kernel(const float* s, uint64_t S, uint16_t* k) {
   for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < S; i += (uint64_t)gridDim.x * kBlock) {
     const float v = s[i];
-    k[i] = (uint16_t)(v <= 0.f ? 0.f : (v >= 65535.f ? 65535.f : v));
+    k[i] = (uint16_t)(!(v > 0.f) ? 0.f : (v >= 65535.f ? 65535.f : v));
   }
 }
 
@@ -883,15 +896,6 @@ void topk_run(TopkKeys<BITS> keys, uint64_t S, uint32_t k, bool sorted, uint32_t
 }
 }  // namespace
 
-bool topk_fused_enabled() {  // PGA_TOPK_FUSED=0: the 4-kernel path (A/B)
-  static int v = -1;
-  if (v < 0) {
-    const char* e = getenv("PGA_TOPK_FUSED");
-    v = (e && e[0] == '0') ? 0 : 1;
-  }
-  return v == 1;
-}
-
 void topk_launch(const float* scores, const uint16_t* keys16, uint32_t key_range, uint64_t S, uint32_t k,
                  bool largest, bool sorted, uint32_t* idx_out, void* ws, hipStream_t s) {
   if (k == 0) return;
@@ -915,7 +919,7 @@ void topk_launch(const float* scores, const uint16_t* keys16, uint32_t key_range
     const uint32_t cgrid = grid > 1024 ? 1024 : grid;
     const uint64_t per_block = (S + cgrid - 1) / cgrid;
     uint64_t* status = (uint64_t*)cnt;  // cgrid aggregate words, then 2 ticket counters
-    if (S < (1ull << 31) && topk_fused_enabled()) {
+    if (S < (1ull << 31)) {  // fused histogram + ticketed select; 4-kernel path beyond
       hipLaunchKernelGGL(topk16_hist_kernel, grid, kBlock, 4 * R, s, keys16, S, R, largest, G, status, cgrid);
       const uint64_t pb16 = (per_block + 15) / 16 * 16;  // aligned 16-key chunks for every thread
       hipLaunchKernelGGL(topk16_select_kernel, cgrid, kBlock, 0, s, keys16, S, pb16, R, largest, k, G, status,
@@ -926,7 +930,7 @@ void topk_launch(const float* scores, const uint16_t* keys16, uint32_t key_range
     hipLaunchKernelGGL(topk16_hist_kernel, grid, kBlock, 4 * R, s, keys16, S, R, largest, G, (uint64_t*)nullptr, 0u);
     hipLaunchKernelGGL(topk16_count_kernel, cgrid, kBlock, 0, s, keys16, S, per_block, R, largest, k, G, st, cnt);
     hipLaunchKernelGGL(topk_offsets_kernel, 1, kBlock, 0, s, cnt, cgrid, G, R);
-    hipLaunchKernelGGL(topk_write_kernel<16>, cgrid, kBlock, 0, s, TopkKeys<16>{scores, keys16, largest}, S,
+    hipLaunchKernelGGL(topk_write_kernel<16>, cgrid, kBlock, 0, s, TopkKeys<16>{scores, keys16, largest, R - 1}, S,
                        per_block, st, cnt, cgrid, (uint32_t*)nullptr, idx_out);
     PGA_HIP_CHECK(hipGetLastError());
     return;

@@ -11,6 +11,7 @@
 
 #include <memory>
 
+#include "pga/cpu.hpp"
 #include "pga/island.hpp"
 #include "pga/trace.hpp"
 #include "pga/ops.hpp"
@@ -104,6 +105,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("philox", [](uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t k0, uint32_t k1) {
     pga::u32x4 r = pga::philox4x32_10(pga::u32x4{c0, c1, c2, c3}, k0, k1);
     return py::make_tuple(r.x, r.y, r.z, r.w);
+  });
+  m.def("perm_crossover", [](int op, const std::vector<uint16_t>& A, const std::vector<uint16_t>& B, uint32_t lo,
+                             uint32_t hi) {
+    if (A.size() != B.size() || hi > A.size() || lo > hi) throw std::invalid_argument("perm_crossover: bad arguments");
+    std::vector<uint16_t> C(A.size());
+    pga::cpu::perm_crossover(op, A.data(), B.data(), (uint32_t)A.size(), lo, hi, C.data());
+    return C;
   });
   m.def("mut_table", [](float p, uint32_t L) {
     auto t = torch::empty({(int64_t)L}, torch::dtype(torch::kInt64));

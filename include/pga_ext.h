@@ -118,8 +118,10 @@ int pga_comm_set_timeout(pga_t *p, double seconds);
 int pga_comm_set_validation(pga_t *p, int on);             /* re-score received migrants (default 1) */
 int pga_comm_degraded(const pga_t *p);
 int pga_comm_info(const pga_t *p, struct pga_comm_stats *out);
-/* loopback only (tests): every `every`-th exchange is dropped (mode 1) or
- * arrives with forged scores (mode 2) */
+/* tests: every `every`-th exchange is dropped (mode 1, loopback), arrives
+ * with forged scores (mode 2, loopback) or has this rank's sends withheld so
+ * its receives never complete (mode 3, RCCL: exercises the timeout + abort
+ * path).  Also lets a 1-rank communicator exchange with itself. */
 int pga_comm_set_fault(pga_t *p, int every, int mode);
 /* global best over ranks (score, owning rank) */
 /* one inter-rank migration epoch now (the step pga_run_islands takes every

@@ -26,7 +26,12 @@ Failure handling (the reference aborts on any error):
     can never inject a fake fitness;
   * a migration that fails or exceeds ``timeout_s`` puts the model in
     DEGRADED mode: islands are loosely coupled, so each keeps evolving alone
-    and ``degraded`` / ``failures`` report it;
+    and ``degraded`` / ``failures`` report it.  The deadline is enforced on
+    the host by polling the exchange's completion (``is_completed``, never a
+    blocking wait); on expiry the process group is aborted at once and the
+    compute stream is never made to wait for the dead transfer, so the
+    generations that follow run on (RCCL's ``work.wait(timeout)`` would only
+    order the stream, not bound the host);
   * ``fault_hook(recv, epoch) -> bool`` is a test-only injection point that
     may corrupt the received buffer in place or drop it (return False).
 
@@ -39,6 +44,7 @@ from __future__ import annotations
 import datetime
 import math
 import os
+import time
 from typing import Callable, Optional, Tuple
 
 import torch
@@ -131,6 +137,12 @@ class IslandModel:
         # overlaps the next generation either way.
         use_side = side_stream and dev.type == "cuda" and ga.operators.elitism <= 1
         self._side = torch.cuda.Stream(dev) if use_side else None
+        # test-only fault: post the receive but withhold the matching send, so
+        # the exchange can never complete (exercises the deadline + abort path)
+        self._withhold_send = False
+        if topology == "all_to_all" and self.world > 1:
+            others = [p for p in range(self.world) if p != self.rank]
+            self._peer_idx = torch.tensor(others, dtype=torch.long, device=dev)
         self._epoch = 0
         self.migrations = 0
         self.bytes_sent = 0
@@ -175,8 +187,9 @@ class IslandModel:
             self._pending = self._a2a()
             return True
         dst, src = self._peers()
-        ops = [dist.P2POp(dist.isend, self.send, dst, group=self.group),
-               dist.P2POp(dist.irecv, self.recv, src, group=self.group)]
+        ops = [dist.P2POp(dist.irecv, self.recv, src, group=self.group)]
+        if not self._withhold_send:
+            ops.insert(0, dist.P2POp(dist.isend, self.send, dst, group=self.group))
         try:
             self._pending = dist.batch_isend_irecv(ops)
         except Exception as e:  # noqa: BLE001 — any comm failure degrades
@@ -185,24 +198,44 @@ class IslandModel:
         return True
 
     def _a2a(self):
-        # every peer gets an equal slice of the emigrants; self slice is empty
+        # every peer gets an equal slice of the emigrants, packed as
+        # [peer][per rows | per scores] (one indexed copy per part, no
+        # per-peer loop); the self slice is empty
         w, per = self.world, self.k // (self.world - 1)
         srows, sscores = self._views(self.send)
-        # repack as [peer][per rows | per scores] so each peer's chunk is contiguous
-        packed = torch.empty(w * per * (self.rw + 1), dtype=torch.int32, device=self.send.device)
+        packed = torch.zeros(w * per * (self.rw + 1), dtype=torch.int32, device=self.send.device)
         pv = packed.view(w, per * (self.rw + 1))
-        rr = srows.view(self.k, self.rw)
-        ss = sscores.view(torch.int32)
-        j = 0
-        for p in range(w):
-            if p == self.rank:
-                pv[p].zero_()
-                continue
-            pv[p, : per * self.rw] = rr[j * per:(j + 1) * per].reshape(-1)
-            pv[p, per * self.rw:] = ss[j * per:(j + 1) * per]
-            j += 1
+        pv[self._peer_idx, : per * self.rw] = srows.view(w - 1, per * self.rw)
+        pv[self._peer_idx, per * self.rw:] = sscores.view(torch.int32).view(w - 1, per)
         self._a2a_recv = torch.empty_like(packed)
         return [dist.all_to_all_single(self._a2a_recv, packed, group=self.group, async_op=True)]
+
+    def _await(self, works) -> None:
+        """Complete the exchange.  Without a timeout: stream-ordered waits
+        only.  With one: poll completion on the host until the deadline, then
+        abort the group (raising TimeoutError) without ever ordering the
+        compute stream after the unfinished transfer."""
+        if self.timeout is None:
+            for wk in works:
+                wk.wait()
+            return
+        deadline = time.monotonic() + self.timeout.total_seconds()
+        pending = list(works)
+        while pending:
+            pending = [wk for wk in pending if not wk.is_completed()]
+            if pending and time.monotonic() > deadline:
+                self._abort()
+                raise TimeoutError(f"migration epoch {self._epoch} exceeded {self.timeout.total_seconds()} s")
+            if pending:
+                time.sleep(50e-6)
+        for wk in works:
+            wk.wait()  # completed: raises a transport error, else just orders the stream
+
+    def _abort(self) -> None:
+        try:
+            dist.distributed_c10d._abort_process_group(self.group)
+        except Exception as e:  # noqa: BLE001 — best effort; the model is degraded either way
+            log.warning("process-group abort failed: %s", e)
 
     def finish_migration(self) -> None:
         """Wait for the exchange and replace the worst individuals."""
@@ -212,10 +245,7 @@ class IslandModel:
             # the next generation must not overwrite rows the side stream still packs
             torch.cuda.current_stream(self._side.device).wait_stream(self._side)
         try:
-            for wk in self._pending:
-                ok = wk.wait(self.timeout) if self.timeout is not None else wk.wait()
-                if ok is False:
-                    raise TimeoutError(f"migration epoch {self._epoch} timed out")
+            self._await(self._pending)
         except Exception as e:  # noqa: BLE001
             self._pending = None
             self._fail(e)
@@ -229,9 +259,9 @@ class IslandModel:
                 return
         if self.topology == "all_to_all":
             w, per = self.world, self.k // (self.world - 1)
-            pv = self._a2a_recv.view(w, per * (self.rw + 1))
-            rows = torch.cat([pv[p, : per * self.rw] for p in range(w) if p != self.rank])
-            scores = torch.cat([pv[p, per * self.rw:] for p in range(w) if p != self.rank]).view(torch.float32)
+            pv = self._a2a_recv.view(w, per * (self.rw + 1))[self._peer_idx]
+            rows = pv[:, : per * self.rw].reshape(-1)
+            scores = pv[:, per * self.rw:].reshape(-1).view(torch.float32)
         else:
             rows, scores = self._views(self.recv)
         rows, scores = rows.contiguous(), scores.contiguous()
@@ -303,8 +333,8 @@ class IslandModel:
     def global_best(self) -> Tuple[float, int, torch.Tensor]:
         """(score, owning rank, decoded genome) of the best individual of all islands."""
         score, genome = self.ga.best()
-        if self.world == 1:
-            return score, 0, genome
+        if self.world == 1 or self.degraded:
+            return score, self.rank, genome
         dev = self.send.device
         t = torch.tensor([score, float(self.rank)], dtype=torch.float64, device=dev)
         allt = [torch.empty_like(t) for _ in range(self.world)]
@@ -317,7 +347,7 @@ class IslandModel:
 
     def global_reduce_best(self) -> float:
         s = self.ga.best_score()
-        if self.world == 1:
+        if self.world == 1 or self.degraded:  # an aborted group cannot reduce: the local best
             return s
         t = torch.tensor([s], dtype=torch.float32, device=self.send.device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)

@@ -1,4 +1,5 @@
-"""Worker for test_parallel.py::test_rccl_self_exchange_matches_loopback_gpu.
+"""Worker for test_parallel.py::test_rccl_self_exchange_matches_loopback_gpu
+(mode "match") and ::test_rccl_withheld_send_degrades_gpu (mode "withhold").
 
 One process, torch.distributed backend "nccl" (= RCCL) with world size 1 on
 the box's one GPU.  The island model is told it has a peer, but both peers
@@ -23,9 +24,9 @@ class _Done:
         return True
 
 
-def model(pga, IslandModel):
+def model(pga, IslandModel, **kw):
     ga = pga.GeneticAlgorithm(pga.models.OneMax(512), 50_000, seed=3, device="cuda:0", elitism=1)
-    m = IslandModel(ga, migrate_every=3, migrate_pct=0.02)
+    m = IslandModel(ga, migrate_every=3, migrate_pct=0.02, **kw)
     m.world, m.rank = 2, 0
     m._peers = lambda: (0, 0)
     return m
@@ -67,5 +68,37 @@ def main(port: int) -> None:
     print("rccl self-exchange ok", a.migrations, a.bytes_sent)
 
 
+def withhold(port: int) -> None:
+    """Migration epochs over real RCCL, then one whose send is withheld: the
+    receive can never complete, the 2 s host deadline expires, the group is
+    aborted, and the island keeps evolving (degraded) without ever ordering
+    its compute stream after the dead transfer."""
+    import time
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK="0", WORLD_SIZE="1", LOCAL_RANK="0")
+    import libpga_amd as pga
+    from libpga_amd.parallel import IslandModel
+
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    m = model(pga, IslandModel, timeout_s=2.0)
+    m.run(7)  # epochs at generations 3 and 6 complete
+    assert m.migrations == 2 and not m.degraded
+    m._withhold_send = True
+    t0 = time.monotonic()
+    m.run(10)  # epoch at generation 9 times out; generations 9..16 still run
+    best = m.ga.best_score()
+    dt = time.monotonic() - t0
+    assert m.degraded and m.failures == 1 and m.migrations == 2, (m.degraded, m.failures, m.migrations)
+    assert m.ga.generation == 17 and best > 0
+    assert dt < 30, dt
+    print("rccl withheld send ok", round(dt, 2))
+    sys.stdout.flush()
+    os._exit(0)  # the aborted group is not torn down again
+
+
 if __name__ == "__main__":
-    main(int(sys.argv[1]))
+    if len(sys.argv) > 2 and sys.argv[2] == "withhold":
+        withhold(int(sys.argv[1]))
+    else:
+        main(int(sys.argv[1]))

@@ -12,6 +12,8 @@ Reference: the migration entry points are empty stubs
 checks are semantic (parity unpinned)."""
 import ctypes as C
 import os
+import subprocess
+import time
 
 import pytest
 import torch  # noqa: F401  (loads the HIP runtime the library links against)
@@ -63,6 +65,10 @@ def lib():
     L.pga_comm_info.argtypes = [vp, C.POINTER(Stats)]
     L.pga_comm_best.argtypes = [vp, C.POINTER(C.c_float), C.POINTER(C.c_int)]
     L.pga_comm_exchange.argtypes = [C.POINTER(vp), C.c_int, C.c_float]
+    L.pga_comm_unique_id.argtypes = [C.c_char_p]
+    L.pga_comm_init.argtypes = [vp, C.c_int, C.c_int, C.c_char_p]
+    L.pga_generation.restype = C.c_uint
+    L.pga_generation.argtypes = [vp]
     L.pga_comm_rank.argtypes = [vp]
     L.pga_comm_size.argtypes = [vp]
     return L
@@ -249,3 +255,63 @@ def test_example_islands_multi_gpu():
     r = subprocess.run([exe, "65536", "30", "all_to_all"], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "GPU islands" in r.stdout
+
+
+def rccl_rank0(lib, n=1):
+    """A GPU solver joined to a fresh n-rank communicator through the
+    one-process-per-GPU path (pga_comm_unique_id + pga_comm_init =
+    ncclCommInitRank), as rank 0."""
+    uid = C.create_string_buffer(128)
+    assert lib.pga_comm_unique_id(uid) == 0, lib.pga_last_error()
+    solvers, pops, arr = make_group(lib, 1, device=0)
+    assert lib.pga_comm_init(solvers[0], n, 0, uid.raw) == 0, lib.pga_last_error()
+    return solvers[0], pops[0]
+
+
+@pytest.mark.gpu
+def test_rccl_initrank_self_exchange_gpu(lib):
+    """InitRank with one rank; the fault hook (no fault, mode 0) arms the
+    self-exchange, so every epoch runs grouped ncclSend/ncclRecv on the
+    communication stream and the compute stream waits for it."""
+    p, pop = rccl_rank0(lib)
+    assert lib.pga_comm_size(p) == 1 and lib.pga_comm_rank(p) == 0
+    assert lib.pga_comm_set_fault(p, 0, 0) == 0
+    lib.pga_run_islands(p, 30, 5, 0.05)
+    st = info(lib, p)
+    k = round(0.05 * S)
+    assert st.epochs == 5 and st.failures == 0 and not st.degraded
+    assert st.migrants_received == 5 * k and st.bytes_sent == 5 * k * (16 + 4)
+    assert lib.pga_generation(pop) == 30 and lib.pga_best_score(p, pop) >= 50
+    lib.pga_deinit(p)
+
+
+@pytest.mark.gpu
+def test_rccl_withheld_send_degrades_gpu(lib):
+    """The 2nd exchange posts its receive but withholds the matching send:
+    the host deadline (2 s) expires, ncclCommAbort runs at once, the pending
+    scatter is dropped and the generations continue on the compute stream,
+    which never waited for the dead transfer."""
+    p, pop = rccl_rank0(lib)
+    assert lib.pga_comm_set_timeout(p, 2.0) == 0
+    assert lib.pga_comm_set_fault(p, 2, 3) == 0
+    t0 = time.monotonic()
+    lib.pga_run_islands(p, 40, 5, 0.05)
+    best = lib.pga_best_score(p, pop)  # synchronises the solver stream
+    dt = time.monotonic() - t0
+    st = info(lib, p)
+    assert st.degraded == 1 and st.failures == 1 and lib.pga_comm_degraded(p) == 1
+    assert st.epochs == 2 and st.migrants_received == round(0.05 * S)
+    assert lib.pga_generation(pop) == 40 and best >= 50
+    assert dt < 30, dt  # one 2 s timeout, not a hang
+    lib.pga_deinit(p)
+
+
+@pytest.mark.gpu
+def test_islands_multiproc_example_gpu(tmp_path):
+    exe = os.path.join(ROOT, "build", "examples", "islands_multiproc")
+    if not os.path.exists(exe):
+        pytest.skip("examples not built")
+    r = subprocess.run([exe, "0", "1", str(tmp_path / "id"), "65536", "30"], capture_output=True, text=True,
+                       timeout=120)
+    assert r.returncode == 0, r.stderr
+    assert "rank 0/1 generations 30" in r.stdout

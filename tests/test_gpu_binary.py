@@ -200,3 +200,26 @@ def test_gpu_topk_selection_order_many_blocks(S):
             gt = (key > T).nonzero().flatten()
             eq = (key == T).nonzero().flatten()[: k - gt.numel()]
             assert torch.equal(got, torch.cat([gt, eq])), (k, largest)
+
+
+@pytest.mark.parametrize("S", [5000, 300000])
+def test_topk_keys_above_range(S):
+    """Scores outside the objective's range (a checkpoint's or an unvalidated
+    migrant's) reach the u16-key top-k: every pass clamps the key to the
+    histogram's top bin, so the selection stays exactly k distinct indices."""
+    L = 64
+    ga = pga.GeneticAlgorithm(pga.models.OneMax(L), S, seed=5, device=DEV)
+    isl = ga.island
+    forged = torch.tensor([3, 17, S // 2, S - 1], dtype=torch.int32, device=DEV)
+    rows = torch.empty((forged.numel(), isl.row_words), dtype=torch.int32, device=DEV)
+    sc = torch.empty(forged.numel(), dtype=torch.float32, device=DEV)
+    isl.gather(forged, rows, sc)
+    isl.scatter(forged, rows, torch.tensor([5000.0, 70.0, 1e9, float("nan")], device=DEV))
+    torch.cuda.synchronize()
+    for k in (1, 3, 10, 257):
+        top = isl.topk(k, True).cpu().tolist()
+        assert len(top) == k and len(set(top)) == k and all(0 <= i < S for i in top)
+        if k >= 3:  # the three finite forged scores clamp to the top bin (no true score reaches L here)
+            assert {3, 17, S // 2} <= set(top)
+        low = isl.topk(k, False).cpu().tolist()
+        assert len(low) == k and len(set(low)) == k and all(0 <= i < S for i in low)

@@ -117,3 +117,15 @@ def test_rccl_self_exchange_matches_loopback_gpu():
                        capture_output=True, text=True, timeout=110)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
     assert "rccl self-exchange ok" in r.stdout
+
+
+@pytest.mark.gpu
+def test_rccl_withheld_send_degrades_gpu():
+    """RCCL failure path of the python island model: a receive whose send is
+    withheld trips the 2 s host deadline, the group is aborted, and the
+    island finishes its generations degraded (exit 0, no hang)."""
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    r = subprocess.run([sys.executable, os.path.join(HERE, "rccl_self_worker.py"), str(free_port()), "withhold"],
+                       env=env, capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    assert "rccl withheld send ok" in r.stdout

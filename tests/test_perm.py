@@ -27,21 +27,22 @@ def test_cpu_valid_and_scores(xo, mut, n):
     assert torch.allclose(p.reference_fitness(g), ga.scores, rtol=1e-5, atol=1e-2)
 
 
-def test_ox_reference_example():
-    """OX1 on the textbook example: A = 1..9 segment [3,7), B = 9 3 7 8 2 6 5 1 4."""
-    from libpga_amd import _C  # noqa: F401
-    A = torch.tensor([0, 1, 2, 3, 4, 5, 6, 7, 8])
-    B = torch.tensor([8, 2, 6, 7, 1, 5, 4, 0, 3])
-    lo, hi = 3, 7
-    seg = set(A[lo:hi].tolist())
-    child = [None] * 9
-    child[lo:hi] = A[lo:hi].tolist()
-    order = [B[(hi + t) % 9].item() for t in range(9) if B[(hi + t) % 9].item() not in seg]
-    pos = [(hi + t) % 9 for t in range(9 - (hi - lo))]
-    for c, q in zip(order, pos):
-        child[q] = c
-    assert sorted(child) == list(range(9))
-
+def test_crossover_known_answers():
+    """The library's OX1 and PMX (the CPU backend's operator, which the GPU
+    kernels match bit for bit in test_gpu_bitexact) on the textbook parents
+    A = 1..9, B = 9 3 7 8 2 6 5 1 4 with A's segment 4 5 6 7 (cuts [3, 7)),
+    written 0-based.  OX1 (Davis): 3 8 2 4 5 6 7 1 9.  PMX (Goldberg and
+    Lingle): 9 3 2 4 5 6 7 1 8."""
+    from libpga_amd import _C
+    A = [0, 1, 2, 3, 4, 5, 6, 7, 8]
+    B = [8, 2, 6, 7, 1, 5, 4, 0, 3]
+    XO_PMX, XO_OX = 5, 6
+    assert _C.perm_crossover(XO_OX, A, B, 3, 7) == [2, 7, 1, 3, 4, 5, 6, 0, 8]
+    assert _C.perm_crossover(XO_PMX, A, B, 3, 7) == [8, 2, 1, 3, 4, 5, 6, 0, 7]
+    # degenerate segments: an empty one gives B, the full one A
+    for op in (XO_OX, XO_PMX):
+        assert _C.perm_crossover(op, A, B, 4, 4) == B
+        assert _C.perm_crossover(op, A, B, 0, 9) == A
 
 def test_tsp_circle_converges():
     p = M.TSPEuclidean.circle(24)

@@ -144,7 +144,7 @@ def write_ninja(opt: str, with_torch: bool) -> str:
         lines.append(f"  extra = -fgpu-rdc --hip-link")
         lines.append("  ldflags = -lpthread -L/opt/rocm/lib -lrccl")
         ex.append(exe)
-    for name in ("onemax_bits", "islands_multi_gpu"):
+    for name in ("onemax_bits", "islands_multi_gpu", "islands_multiproc"):
         src = f"examples/{name}.c"
         if not os.path.exists(os.path.join(ROOT, src)):
             continue
