@@ -1,11 +1,21 @@
 #!/usr/bin/env python3
 """Per-epoch cost of the island-migration device work on one GPU (everything
 IslandModel does except the RCCL transfer itself): top-k emigrants, pack,
-bottom-k victims, scatter, best/key refresh.  Prints one JSON line."""
+bottom-k victims, scatter, best/key refresh (Island.emigrate / immigrate).  Prints one JSON line."""
 import json
 import types
 import os
 import sys
+
+
+def emit(res):
+    """One JSON line on stdout, and to $PGA_OUT when set (RCCL may print its
+    version banner on stdout, so the file is the clean record)."""
+    line = json.dumps(res)
+    print(line, flush=True)
+    if os.environ.get("PGA_OUT"):
+        with open(os.environ["PGA_OUT"], "w") as f:
+            f.write(line + "\n")
 
 import torch
 
@@ -24,12 +34,10 @@ def main():
     rows = torch.empty(k * rw, dtype=torch.int32, device="cuda:0")
     sc = torch.empty(k, dtype=torch.float32, device="cuda:0")
 
-    def epoch():  # exactly IslandModel's device work (selection-order top-k)
-        idx = isl.topk(k, True, False)
-        isl.gather(idx, rows, sc)
+    def epoch():  # exactly IslandModel's device work (fused selections)
+        isl.emigrate(k, rows, sc)
         isl.evaluate_rows(rows, sc)
-        vic = isl.topk(k, False, False)
-        isl.scatter(vic, rows, sc)
+        isl.immigrate(k, rows, sc)
 
     for _ in range(5):
         epoch()
@@ -46,7 +54,7 @@ def main():
         b.synchronize()
         res[name + "_us"] = a.elapsed_time(b) / n * 1e3
     res.update(pop=S, k=k)
-    print(json.dumps(res))
+    emit(res)
 
 
 if __name__ == "__main__" and not os.environ.get("PGA_LOOPBACK") and not os.environ.get("PGA_RCCL_SELF"):
@@ -83,7 +91,7 @@ def loopback_overhead(S=1 << 20, every=10, gens=200):
         b.record()
         b.synchronize()
         out["us_per_gen_" + ("overlap" if side else "serial")] = a.elapsed_time(b) / gens * 1e3
-    print(json.dumps(out))
+    emit(out)
 
 
 if __name__ == "__main__" and os.environ.get("PGA_LOOPBACK"):
@@ -122,7 +130,7 @@ def rccl_self_overhead(S=1 << 20, every=10, gens=500):
     for v in ("rccl_self", "rccl_self_noside"):
         out["overhead_pct_" + v] = 100.0 * (out["us_per_gen_" + v] / out["us_per_gen_none"] - 1.0)
     out.update(pop=S, every=every)
-    print(json.dumps(out))
+    emit(out)
     dist.destroy_process_group()
 
 

@@ -202,16 +202,11 @@ void ensure_emigrant_staging(population_t* pop, uint32_t k) {
 
 void take_best(population_t* pop, uint32_t k) {
   ensure_emigrant_staging(pop, k);
-  pga::Island& isl = *pop->isl;
-  uint32_t* idx = (uint32_t*)isl.scratch(4ull * k);
-  isl.topk(k, true, idx, false);
-  isl.gather(idx, k, pop->emi_rows, pop->emi_scores);
+  pop->isl->emigrate(k, pop->emi_rows, pop->emi_scores);
 }
 
 void replace_worst(pga::Island& isl, const population_t* from, uint32_t k) {
-  uint32_t* idx = (uint32_t*)isl.scratch(4ull * k);
-  isl.topk(k, false, idx, false);
-  isl.scatter(idx, k, from->emi_rows, from->emi_scores);
+  isl.immigrate(k, from->emi_rows, from->emi_scores);
 }
 
 int default_device() {
@@ -650,9 +645,7 @@ void migrate_ranks(const std::vector<pga_t*>& solvers, float pct) {
       throw std::invalid_argument("migration: ranks need populations of the same size and genome length");
     isl.stream = p->stream;
     ensure_staging(p, isl, k);
-    uint32_t* idx = (uint32_t*)isl.scratch(4ull * k);
-    isl.topk(k, true, idx, false);
-    isl.gather(idx, k, p->mig_send_rows, p->mig_send_scores);
+    isl.emigrate(k, p->mig_send_rows, p->mig_send_scores);
     pga::LocalRank l;
     l.rank = p->comm_rank;
     l.device = p->device;
@@ -687,9 +680,7 @@ void migrate_ranks(const std::vector<pga_t*>& solvers, float pct) {
     use_device(p);
     pga::Island& isl = *p->pops[0]->isl;
     if (p->validate_migrants) isl.evaluate_rows(p->mig_recv_rows, p->mig_recv_scores, k);
-    uint32_t* idx = (uint32_t*)isl.scratch(4ull * k);
-    isl.topk(k, false, idx, false);
-    isl.scatter(idx, k, p->mig_recv_rows, p->mig_recv_scores);
+    isl.immigrate(k, p->mig_recv_rows, p->mig_recv_scores);
     p->migrants_received += k;
   }
 }

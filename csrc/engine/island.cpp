@@ -399,18 +399,21 @@ void Island::stats(float out[4]) {
   }
 }
 
+void Island::ensure_topk_ws(uint32_t k) {
+  const size_t need = topk_workspace_bytes(cfg_.S, k);
+  if (topk_ws_.bytes >= need) return;
+  synchronize();
+  release(topk_ws_);
+  topk_ws_ = alloc(need);
+  PGA_HIP_CHECK(hipMemsetAsync(topk_ws_.ptr, 0, need, stream));  // the value histogram must start zeroed
+}
+
 void Island::topk(uint32_t k, bool largest, uint32_t* idx_out, bool sorted) {
   TraceRange tr(largest ? "pga.topk" : "pga.bottomk");
   if (k > cfg_.S) throw std::invalid_argument("k exceeds population size");
   const float* sc = (const float*)scores_[cur_].ptr;
   if (on_gpu()) {
-    size_t need = topk_workspace_bytes(cfg_.S, k);
-    if (topk_ws_.bytes < need) {
-      synchronize();
-      release(topk_ws_);
-      topk_ws_ = alloc(need);
-      PGA_HIP_CHECK(hipMemsetAsync(topk_ws_.ptr, 0, need, stream));  // the value histogram must start zeroed
-    }
+    ensure_topk_ws(k);
     const uint16_t* k16 = integer_objective(cfg_.objective, cfg_.L) ? (const uint16_t*)keys_[cur_].ptr : nullptr;
     topk_launch(sc, k16, cfg_.L + 1, cfg_.S, k, largest, sorted, idx_out, topk_ws_.ptr, stream);
   } else {
@@ -454,6 +457,56 @@ void Island::scatter(const uint32_t* idx, uint32_t n, const void* in_rows, const
   else
     cpu::scatter_rows(rows_[cur_].ptr, (float*)scores_[cur_].ptr, row_words_, idx, n, in_rows, in_scores);
   rebest();  // best partials and tournament keys follow the new scores
+}
+
+void Island::emigrate(uint32_t k, void* out_rows, float* out_scores) {
+  TraceRange tr("pga.migrate.emigrate");
+  if (k == 0) return;
+  if (k > cfg_.S) throw std::invalid_argument("k exceeds population size");
+  const uint16_t* k16 = integer_objective(cfg_.objective, cfg_.L) ? (const uint16_t*)keys_[cur_].ptr : nullptr;
+  if (on_gpu() && topk_move_supported(k16, cfg_.L + 1, cfg_.S)) {
+    ensure_topk_ws(k);
+    TopkMove mv;
+    mv.mode = TopkMove::GATHER;
+    mv.rw16 = row_words_ / 4;
+    mv.src_rows = (const uint4*)rows_[cur_].ptr;
+    mv.src_scores = (const float*)scores_[cur_].ptr;
+    mv.dst_rows = (uint4*)out_rows;
+    mv.dst_scores = out_scores;
+    topk_launch((const float*)scores_[cur_].ptr, k16, cfg_.L + 1, cfg_.S, k, true, false, nullptr, topk_ws_.ptr, stream,
+                &mv);
+    return;
+  }
+  uint32_t* idx = (uint32_t*)scratch(4ull * k);
+  topk(k, true, idx, false);
+  gather(idx, k, out_rows, out_scores);
+}
+
+void Island::immigrate(uint32_t k, const void* in_rows, const float* in_scores) {
+  TraceRange tr("pga.migrate.immigrate");
+  if (k == 0) return;
+  if (k > cfg_.S) throw std::invalid_argument("k exceeds population size");
+  uint16_t* k16 = integer_objective(cfg_.objective, cfg_.L) ? (uint16_t*)keys_[cur_].ptr : nullptr;
+  if (on_gpu() && topk_move_supported(k16, cfg_.L + 1, cfg_.S)) {
+    ensure_topk_ws(k);
+    TopkMove mv;
+    mv.mode = TopkMove::SCATTER;
+    mv.rw16 = row_words_ / 4;
+    mv.src_rows = (const uint4*)in_rows;
+    mv.src_scores = in_scores;
+    mv.dst_rows = (uint4*)rows_[cur_].ptr;
+    mv.dst_scores = (float*)scores_[cur_].ptr;
+    mv.dst_keys = k16;
+    topk_launch((const float*)scores_[cur_].ptr, k16, cfg_.L + 1, cfg_.S, k, false, false, nullptr, topk_ws_.ptr,
+                stream, &mv);
+    // the victims' keys were written with their rows: only the best partials follow
+    n_best_[cur_] = best_of_scores_launch((const float*)scores_[cur_].ptr, cfg_.S,
+                                          (unsigned long long*)best_[cur_].ptr, stream, nullptr);
+    return;
+  }
+  uint32_t* idx = (uint32_t*)scratch(4ull * k);
+  topk(k, false, idx, false);
+  scatter(idx, k, in_rows, in_scores);
 }
 
 bool Island::evaluate_rows(void* rows, float* scores, uint32_t n) {
@@ -516,13 +569,7 @@ bool Island::capture_graph() {
   if (!cap_stream_) PGA_HIP_CHECK(hipStreamCreateWithFlags(&cap_stream_, hipStreamNonBlocking));
   // workspaces that a stage would otherwise (re)allocate synchronously
   if (cfg_.n_elite > 1) {
-    const size_t need = topk_workspace_bytes(cfg_.S, cfg_.n_elite);
-    if (topk_ws_.bytes < need) {
-      synchronize();
-      release(topk_ws_);
-      topk_ws_ = alloc(need);
-      PGA_HIP_CHECK(hipMemset(topk_ws_.ptr, 0, need));
-    }
+    ensure_topk_ws(cfg_.n_elite);
   }
   const int cur0 = cur_;
   const uint32_t gen0 = gen_, nb0 = n_best_[cur_];

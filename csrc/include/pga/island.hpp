@@ -110,6 +110,13 @@ class Island {
   void topk(uint32_t k, bool largest, uint32_t* idx_out, bool sorted = true);
   void gather(const uint32_t* idx, uint32_t n, void* out_rows, float* out_scores);
   void scatter(const uint32_t* idx, uint32_t n, const void* in_rows, const float* in_scores);
+  // Island migration, stream-ordered: emigrate = the top-k rows + scores
+  // (selection order) into out buffers; immigrate = the k given rows replace
+  // the bottom-k (then best partials follow).  On the GPU, integer objectives
+  // do each in ONE selection kernel with the row moves fused in; otherwise
+  // topk + gather / scatter.  `idx_scratch` (k words, device) may be null.
+  void emigrate(uint32_t k, void* out_rows, float* out_scores);
+  void immigrate(uint32_t k, const void* in_rows, const float* in_scores);
   // score n external rows (e.g. received migrants) with this island's
   // objective, in place; false when the objective is not native (OBJ_NONE)
   bool evaluate_rows(void* rows, float* scores, uint32_t n);
@@ -151,6 +158,7 @@ class Island {
   Buffer alloc(size_t bytes);
   void release(Buffer& b);
   void rebuild_mut_table();
+  void ensure_topk_ws(uint32_t k);
 
   Config cfg_;
   int device_;

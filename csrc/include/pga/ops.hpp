@@ -108,8 +108,22 @@ size_t topk_workspace_bytes(uint64_t S, uint32_t k);
 // key_range: keys16 take values in [0, key_range) (L + 1 for the integer
 // objectives); <= kTopkMaxRange enables the one-pass value histogram
 constexpr uint32_t kTopkMaxRange = 8192;
+// Optional fused row move of the selection (u16-key selection-order path
+// only, see topk_move_supported): emigrants gathered into a send buffer, or
+// immigrants scattered over the selected victims (rows, scores, keys).
+struct TopkMove {
+  enum Mode : int32_t { NONE = 0, GATHER = 1, SCATTER = 2 };
+  int32_t mode = NONE;
+  uint32_t rw16 = 0;  // row stride in 16-byte units
+  const uint4* src_rows = nullptr;
+  const float* src_scores = nullptr;
+  uint4* dst_rows = nullptr;
+  float* dst_scores = nullptr;
+  uint16_t* dst_keys = nullptr;
+};
+bool topk_move_supported(const uint16_t* keys16, uint32_t key_range, uint64_t S);
 void topk_launch(const float* scores, const uint16_t* keys16, uint32_t key_range, uint64_t S, uint32_t k, bool largest,
-                 bool sorted, uint32_t* idx_out, void* workspace, hipStream_t s);
+                 bool sorted, uint32_t* idx_out, void* workspace, hipStream_t s, const TopkMove* mv = nullptr);
 // rows: out[i] = rows[idx[i]] (row_words 32-bit words per row), optional scores
 void gather_rows_launch(const void* rows, const float* scores, uint32_t row_words, const uint32_t* idx, uint32_t n,
                         void* out_rows, float* out_scores, hipStream_t s);

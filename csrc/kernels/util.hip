@@ -380,6 +380,27 @@ __device__ __forceinline__ uint32_t load_keys16(const uint16_t* k16, uint64_t c0
   return m;
 }
 
+constexpr uint32_t kTopkMoveSlots = 4096;  // selections per block listed in LDS for the cooperative row move
+
+// What the fused selection does with the i-th selected individual at output
+// position pos (besides idx_out[pos] = i when idx_out is set):
+//   GATHER   out rows[pos] = population row i, out scores[pos] = score i (emigrants)
+//   SCATTER  population row i = in rows[pos], score i and its u16 key =
+//            in scores[pos] (immigrants replace the selected victims)
+// so an island-migration epoch needs no separate gather / scatter kernels.
+__device__ __forceinline__ void topk_emit(const TopkMove& mv, uint32_t* idx_out, uint32_t pos, uint64_t i) {
+  if (idx_out) idx_out[pos] = (uint32_t)i;
+  if (mv.mode == TopkMove::GATHER) {
+    for (uint32_t c = 0; c < mv.rw16; ++c) mv.dst_rows[(uint64_t)pos * mv.rw16 + c] = mv.src_rows[i * mv.rw16 + c];
+    mv.dst_scores[pos] = mv.src_scores[i];
+  } else if (mv.mode == TopkMove::SCATTER) {
+    for (uint32_t c = 0; c < mv.rw16; ++c) mv.dst_rows[i * mv.rw16 + c] = mv.src_rows[(uint64_t)pos * mv.rw16 + c];
+    const float v = mv.src_scores[pos];
+    mv.dst_scores[i] = v;
+    if (mv.dst_keys) mv.dst_keys[i] = (uint16_t)(!(v > 0.f) ? 0.f : (v >= 65535.f ? 65535.f : v));
+  }
+}
+
 __global__ __launch_bounds__(kBlock) void topk16_hist_kernel(const uint16_t* k16, uint64_t S, uint32_t R, bool largest,
                                                              uint32_t* G, uint64_t* status, uint32_t n_status) {
   extern __shared__ uint32_t hr[];
@@ -563,8 +584,9 @@ constexpr uint64_t kLbAgg = 1ull << 62, kLbMask31 = 0x7FFFFFFFull;
 __global__ __launch_bounds__(kBlock) void topk16_select_kernel(const uint16_t* k16, uint64_t S, uint64_t per_block,
                                                                uint32_t R, bool largest, uint32_t k, uint32_t* G,
                                                                uint64_t* status, uint32_t* ctr, uint32_t nblocks,
-                                                               uint32_t* idx_out) {
+                                                               uint32_t* idx_out, TopkMove mv) {
   __shared__ uint32_t gl[kTopkMaxRange];  // this block's copy of the histogram
+  __shared__ uint32_t sel_pos[kTopkMoveSlots], sel_src[kTopkMoveSlots];  // row moves: output position, source
   __shared__ uint32_t sh_T, sh_need, sh_b;
   __shared__ uint32_t lds[kBlock / 64];
   if (threadIdx.x == 0) sh_b = atomicAdd(&ctr[0], 1u);
@@ -642,6 +664,12 @@ __global__ __launch_bounds__(kBlock) void topk16_select_kernel(const uint16_t* k
   if (b == nblocks - 1)
     for (uint32_t i = threadIdx.x; i < R; i += kBlock) G[i] = 0;
   uint32_t gpos = pg + og, epos = pe + oe;
+  // with a row move, the block's selections are listed in LDS first (slot:
+  // gt ones in scan order, then the taken ties) and copied by the whole block
+  // afterwards, 16 bytes per lane, rows contiguous: one thread per row was
+  // 3x slower than the separate gather / scatter kernels
+  const bool move = mv.mode != TopkMove::NONE;
+  uint32_t lg = og, le = bg + oe;
   for (uint64_t c0 = t0; c0 < t1; c0 += 16) {
     uint32_t kv[16];
     const uint32_t m = load_keys16(k16, c0, t1, kv);
@@ -649,10 +677,51 @@ __global__ __launch_bounds__(kBlock) void topk16_select_kernel(const uint16_t* k
     for (int e = 0; e < 16; ++e) {
       if (!((m >> e) & 1u)) continue;
       const uint32_t key = min(kv[e], R - 1) ^ flip;
-      if (key > T && gpos < gt_total) idx_out[gpos++] = (uint32_t)(c0 + e);
+      uint32_t pos = 0xFFFFFFFFu, slot = 0;
+      if (key > T && gpos < gt_total) {
+        pos = gpos++;
+        slot = lg++;
+      }
       if (key == T) {
-        if (epos < need_eq) idx_out[gt_total + epos] = (uint32_t)(c0 + e);
+        if (epos < need_eq) {
+          pos = gt_total + epos;
+          slot = le;
+        }
         ++epos;
+        ++le;
+      }
+      if (pos == 0xFFFFFFFFu) continue;
+      if (idx_out) idx_out[pos] = (uint32_t)(c0 + e);
+      if (move && slot < kTopkMoveSlots) {
+        sel_pos[slot] = pos;
+        sel_src[slot] = (uint32_t)(c0 + e - blo);
+      } else if (move) {
+        topk_emit(mv, nullptr, pos, c0 + e);  // beyond the LDS list (huge blocks): per thread
+      }
+    }
+  }
+  if (!move) return;
+  // slots [0, bg) are gt selections (all taken up to gt_total), [bg, bg+be)
+  // ties, of which only those with a global tie rank < need_eq were filled
+  __syncthreads();
+  const uint32_t taken_eq = pe >= need_eq ? 0u : min(be, need_eq - pe);
+  const uint32_t n_gt = pg >= gt_total ? 0u : min(bg, gt_total - pg);
+  const uint32_t nsel = min(bg + taken_eq, kTopkMoveSlots);
+  const uint32_t rw16 = mv.rw16;
+  for (uint32_t t = threadIdx.x; t < nsel * rw16; t += kBlock) {
+    const uint32_t r = t / rw16, c = t % rw16;
+    if (r >= n_gt && r < bg) continue;  // gt slots beyond gt_total were never filled
+    const uint64_t i = blo + sel_src[r];
+    const uint64_t pos = sel_pos[r];
+    if (mv.mode == TopkMove::GATHER) {
+      mv.dst_rows[pos * rw16 + c] = mv.src_rows[i * rw16 + c];
+      if (c == 0) mv.dst_scores[pos] = mv.src_scores[i];
+    } else {
+      mv.dst_rows[i * rw16 + c] = mv.src_rows[pos * rw16 + c];
+      if (c == 0) {
+        const float v = mv.src_scores[pos];
+        mv.dst_scores[i] = v;
+        if (mv.dst_keys) mv.dst_keys[i] = (uint16_t)(!(v > 0.f) ? 0.f : (v >= 65535.f ? 65535.f : v));
       }
     }
   }
@@ -896,10 +965,16 @@ void topk_run(TopkKeys<BITS> keys, uint64_t S, uint32_t k, bool sorted, uint32_t
 }
 }  // namespace
 
+bool topk_move_supported(const uint16_t* keys16, uint32_t key_range, uint64_t S) {
+  return keys16 && key_range >= 2 && key_range <= kTopkMaxRange && S < (1ull << 31);
+}
+
 void topk_launch(const float* scores, const uint16_t* keys16, uint32_t key_range, uint64_t S, uint32_t k,
-                 bool largest, bool sorted, uint32_t* idx_out, void* ws, hipStream_t s) {
+                 bool largest, bool sorted, uint32_t* idx_out, void* ws, hipStream_t s, const TopkMove* mv) {
   if (k == 0) return;
   if (k > S) throw std::runtime_error("topk: k > S");
+  if (mv && (sorted || !topk_move_supported(keys16, key_range, S)))
+    throw std::invalid_argument("topk: fused row moves need the u16-key selection-order path");
   if (keys16 && !sorted && key_range >= 2 && key_range <= kTopkMaxRange) {
     // integer objective, selection order: histogram over the R key values
     char* p = (char*)ws;
@@ -923,7 +998,7 @@ void topk_launch(const float* scores, const uint16_t* keys16, uint32_t key_range
       hipLaunchKernelGGL(topk16_hist_kernel, grid, kBlock, 4 * R, s, keys16, S, R, largest, G, status, cgrid);
       const uint64_t pb16 = (per_block + 15) / 16 * 16;  // aligned 16-key chunks for every thread
       hipLaunchKernelGGL(topk16_select_kernel, cgrid, kBlock, 0, s, keys16, S, pb16, R, largest, k, G, status,
-                         (uint32_t*)(status + cgrid), cgrid, idx_out);
+                         (uint32_t*)(status + cgrid), cgrid, idx_out, mv ? *mv : TopkMove{});
       PGA_HIP_CHECK(hipGetLastError());
       return;
     }

@@ -212,6 +212,22 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
              i->scatter((const uint32_t*)idx.data_ptr<int32_t>(), (uint32_t)n, in_rows.data_ptr(),
                         in_scores.data_ptr<float>());
            })
+      .def("emigrate",
+           [](const IslandPtr& i, uint32_t k, torch::Tensor out_rows, torch::Tensor out_scores) {
+             bind_stream(*i);
+             check_tensor(out_rows, *i, torch::kInt32, "out_rows");
+             check_tensor(out_scores, *i, torch::kFloat32, "out_scores");
+             TORCH_CHECK(out_rows.numel() >= (int64_t)k * i->row_words() && out_scores.numel() >= k, "output too small");
+             i->emigrate(k, out_rows.data_ptr(), out_scores.data_ptr<float>());
+           })
+      .def("immigrate",
+           [](const IslandPtr& i, uint32_t k, torch::Tensor in_rows, torch::Tensor in_scores) {
+             bind_stream(*i);
+             check_tensor(in_rows, *i, torch::kInt32, "in_rows");
+             check_tensor(in_scores, *i, torch::kFloat32, "in_scores");
+             TORCH_CHECK(in_rows.numel() >= (int64_t)k * i->row_words() && in_scores.numel() >= k, "input too small");
+             i->immigrate(k, in_rows.data_ptr(), in_scores.data_ptr<float>());
+           })
       .def("evaluate_rows",
            [](const IslandPtr& i, torch::Tensor rows, torch::Tensor scores) {
              bind_stream(*i);

@@ -6,10 +6,12 @@ exports its top ``migrate_pct`` individuals and imports the same number from
 its peer(s), replacing its worst individuals.
 
 Data path per migration (all on-device, no host synchronisation):
-  top-k (radix select, util.hip) -> gather rows+scores into ONE packed send
-  buffer (gather_rows_kernel) -> RCCL send/recv on torch's NCCL stream ->
-  [next generation kernel runs concurrently on the compute stream]
-  -> stream wait on the NCCL work -> bottom-k victims -> scatter migrants.
+  top-k selection with the row gather fused in (Island.emigrate: u16-key
+  histogram + one ticketed select kernel writing rows+scores into ONE packed
+  send buffer) -> RCCL send/recv on torch's NCCL stream -> [next generation
+  kernel runs concurrently on the compute stream] -> stream wait on the NCCL
+  work -> re-score -> bottom-k selection with the scatter fused in
+  (Island.immigrate).
 
 Why this shape on MI355X: the 8 GPUs of a node are fully connected by xGMI,
 7 point-to-point links of ~153 GB/s each.  A ring migration uses one link per
@@ -180,9 +182,8 @@ class IslandModel:
 
     def _post(self) -> bool:
         isl = self.ga.island
-        idx = isl.topk(self.k, True, False)
         srows, sscores = self._views(self.send)
-        isl.gather(idx, srows, sscores)
+        isl.emigrate(self.k, srows, sscores)  # top-k selection with the gather fused in
         if self.topology == "all_to_all":
             self._pending = self._a2a()
             return True
@@ -269,8 +270,7 @@ class IslandModel:
             isl.evaluate_rows(rows, scores)  # trust nothing from the wire
             if self.ga.problem.encoding == "permutation":
                 self._sanitize_perm(rows, scores)
-        victims = isl.topk(self.k, False, False)
-        isl.scatter(victims, rows, scores)  # also refreshes best + keys
+        isl.immigrate(self.k, rows, scores)  # bottom-k replaced (fused scatter), best + keys follow
         self.migrations += 1
 
     def _sanitize_perm(self, rows: torch.Tensor, scores: torch.Tensor) -> None:

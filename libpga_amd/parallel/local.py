@@ -46,6 +46,7 @@ class LocalIslands:
                         if self.device.type == "cuda" else None)
         self.migrations = 0
         self._epoch = 0
+        self._staging = {}
 
     @property
     def generation(self) -> int:
@@ -79,16 +80,17 @@ class LocalIslands:
         out = []
         for i in order:  # take every island's emigrants before any is replaced
             isl = self.islands[i].island
-            idx = isl.topk(self.k, True, False)
-            rows = torch.empty(self.k * int(isl.row_words), dtype=torch.int32, device=self.device)
-            sc = torch.empty(self.k, dtype=torch.float32, device=self.device)
-            isl.gather(idx, rows, sc)
+            if i not in self._staging:  # persistent per-island emigrant buffers
+                self._staging[i] = (torch.empty(self.k * int(isl.row_words), dtype=torch.int32, device=self.device),
+                                    torch.empty(self.k, dtype=torch.float32, device=self.device))
+            rows, sc = self._staging[i]
+            isl.emigrate(self.k, rows, sc)  # top-k selection, gather fused in
             out.append((rows, sc))
         n = len(order)
         for j, i in enumerate(order):
             dst = self.islands[order[(j + 1) % n]].island
             rows, sc = out[j]
-            dst.scatter(dst.topk(self.k, False, False), rows, sc)
+            dst.immigrate(self.k, rows, sc)  # bottom-k selection, scatter fused in
         self._epoch += 1
         self.migrations += 1
 

@@ -223,3 +223,37 @@ def test_topk_keys_above_range(S):
             assert {3, 17, S // 2} <= set(top)
         low = isl.topk(k, False).cpu().tolist()
         assert len(low) == k and len(set(low)) == k and all(0 <= i < S for i in low)
+
+
+@pytest.mark.parametrize("S,k", [(5000, 50), (1 << 20, 10486)])
+def test_fused_migration_matches_unfused(S, k):
+    """Island.emigrate / immigrate (selection kernel with the row gather /
+    scatter fused in) == topk + gather / topk + scatter, bit for bit, and the
+    victims' tournament keys follow their new scores."""
+    kw = dict(seed=9, device=DEV, elitism=1)
+    a = pga.GeneticAlgorithm(pga.models.OneMax(1024), S, **kw)
+    b = pga.GeneticAlgorithm(pga.models.OneMax(1024), S, **kw)
+    a.run(3)
+    b.run(3)
+    ia, ib = a.island, b.island
+    rw = int(ia.row_words)
+    ra, sa = torch.empty(k * rw, dtype=torch.int32, device=DEV), torch.empty(k, device=DEV)
+    rb, sb = torch.empty_like(ra), torch.empty_like(sa)
+    ia.emigrate(k, ra, sa)
+    ib.gather(ib.topk(k, True, False), rb, sb)
+    torch.cuda.synchronize()
+    assert torch.equal(ra, rb) and torch.equal(sa, sb)
+    # immigrants: another island's best rows replace the worst
+    c = pga.GeneticAlgorithm(pga.models.OneMax(1024), S, seed=10, device=DEV, elitism=1)
+    c.run(5)
+    rc, sc = torch.empty_like(ra), torch.empty_like(sa)
+    c.island.emigrate(k, rc, sc)
+    ia.immigrate(k, rc, sc)
+    ib.scatter(ib.topk(k, False, False), rc, sc)
+    torch.cuda.synchronize()
+    assert torch.equal(a.rows, b.rows) and torch.equal(a.scores, b.scores)
+    assert a.best_score() == b.best_score()
+    a.run(2)
+    b.run(2)  # identical keys => identical tournaments
+    torch.cuda.synchronize()
+    assert torch.equal(a.rows, b.rows) and torch.equal(a.scores, b.scores)
