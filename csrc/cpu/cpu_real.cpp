@@ -26,8 +26,7 @@ static float butterfly_prod(float* v, uint32_t GS) {
 }
 
 uint32_t real_run(int mode, const GenArgs& a, unsigned long long* best_parts) {
-  if (a.chunks > 64) throw std::invalid_argument("REAL encoding supports at most 256 genes");
-  const uint32_t GS = group_size(a.chunks);
+  const uint32_t GS = group_size(a.chunks);  // 64 lanes own chunks c, c+64, ... of long genomes
   const uint64_t rw = a.row_words;
   const float* cur = (const float*)a.cur;
   float* nxt = (float*)a.next;
@@ -42,12 +41,15 @@ uint32_t real_run(int mode, const GenArgs& a, unsigned long long* best_parts) {
   const uint32_t dp = ((4 * nchunks + 15) / 16) * 16;
   if (evals && a.objective == OBJ_USER_FNPTR)
     throw std::invalid_argument("device function-pointer objectives need the GPU backend");
+  if (nchunks > 64 && evals && a.objective == OBJ_TSP_RANDOM_KEY)
+    throw std::invalid_argument("the random-key TSP and function-pointer objectives support at most 256 genes");
 
   uint32_t elite0 = 0;
   if (gen && a.n_elite > 0 && a.elite_idx == nullptr) elite0 = (uint32_t)best_index(reduce_best(a.best_cur, a.n_best_cur));
 
   unsigned long long best = 0;
-  std::vector<float> v(4 * GS), x(std::max<uint32_t>(4 * GS, dp) + 4), z(std::max<uint32_t>(4 * GS, dp) + 4);
+  const uint32_t nv = 4 * std::max<uint32_t>(GS, nchunks);
+  std::vector<float> v(nv), x(std::max<uint32_t>(nv, dp) + 4), z(std::max<uint32_t>(nv, dp) + 4);
   for (uint64_t child = 0; child < a.S; ++child) {
     std::fill(v.begin(), v.end(), 0.f);
     bool elite = false;
@@ -124,11 +126,12 @@ uint32_t real_run(int mode, const GenArgs& a, unsigned long long* best_parts) {
         float s0[64] = {0}, s1[64] = {0}, s2[64];
         for (uint32_t q = 0; q < GS; ++q) s2[q] = 1.f;
         for (uint32_t d = 0; d < L; ++d) {
-          RealAcc acc{s0[d / 4], s1[d / 4], s2[d / 4]};
+          const uint32_t ln = (d / 4) % GS;  // the lane owning gene d's chunk
+          RealAcc acc{s0[ln], s1[ln], s2[ln]};
           real_obj_term(a, d, z[d], z[d + 1], v[d], acc);
-          s0[d / 4] = acc.s0;
-          s1[d / 4] = acc.s1;
-          s2[d / 4] = acc.s2;
+          s0[ln] = acc.s0;
+          s1[ln] = acc.s1;
+          s2[ln] = acc.s2;
         }
         RealAcc t{butterfly_sum(s0, GS), butterfly_sum(s1, GS), butterfly_prod(s2, GS)};
         score = real_obj_finish(a, t);

@@ -3,8 +3,9 @@
 //
 // Geometry: one individual = `chunks` 16-byte chunks of 4 genes; a group of
 // GS = group_size(chunks) lanes owns one individual (lane q holds genes
-// 4q..4q+3), GPB = 256/GS individuals per block iteration.  Genomes up to 256
-// genes (GS <= 64).  Per iteration every child's genes are also staged in an
+// 4q..4q+3), GPB = 256/GS individuals per block iteration, for genomes up to
+// 256 genes (GS <= 64); longer genomes use real_long_kernel (a chunk-segment
+// loop, one wave per individual).  Per iteration every child's genes are also staged in an
 // LDS tile X[GPB][TW] (TW = max(4 GS, 16) + 1: the +1 breaks the 16-way bank
 // conflict of the MFMA A-operand column reads).
 //
@@ -266,6 +267,156 @@ __global__ __launch_bounds__(kBlock) void real_kernel(GenArgs a, unsigned long l
         my_best = pb > my_best ? pb : my_best;
       }
       if (tile_needed) __syncthreads();  // tiles are rewritten next iteration
+    }
+  }
+  if (evals && best_parts) {
+    unsigned long long b = block_max_u64(my_best, lds_red);
+    if (threadIdx.x == 0) best_parts[blockIdx.x] = b;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Long genomes (L > 256 genes, more than 64 chunks): one wave per individual,
+// lane q owns chunks q, q+64, q+128, ... (a segment loop, the BINARY generic
+// kernel's layout), per-lane partial sums in gene order, one 64-lane
+// butterfly.  Element-wise objectives and Rosenbrock: the neighbour of a
+// segment's last gene is the next segment's first, so lane 63 defers that
+// term to the next segment (added before that segment's own terms: the CPU's
+// gene-order accumulation per lane).  Rotation (M is L x L), the reference-E3
+// random-key TSP (O(L^2)) and device function pointers stay <= 256 genes.
+// ---------------------------------------------------------------------------
+template <int MODE>
+__global__ __launch_bounds__(kBlock) void real_long_kernel(GenArgs a, unsigned long long* best_parts) {
+  resolve_gen(a);
+  __shared__ uint32_t lds_thr[kMutCap];
+  __shared__ unsigned long long lds_red[kBlock / 64];
+  __shared__ uint32_t lds_elite;
+  constexpr uint32_t GS = 64, GPB = kBlock / 64;
+  const uint32_t q = lane_id(), g = threadIdx.x >> 6;
+  const uint64_t rs = a.row_words >> 2;
+  const float4* cur = (const float4*)a.cur;
+  float4* nxt = (float4*)a.next;
+  const uint32_t L = a.L, nchunks = a.chunks;
+  constexpr bool MUTATES = MODE == MODE_GEN || MODE == MODE_MUTATE;
+  constexpr bool EVALS = MODE == MODE_GEN || MODE == MODE_INIT || MODE == MODE_EVAL;
+  const bool evals = EVALS && a.objective != OBJ_NONE;
+  const bool per_gene_mut = MUTATES && (a.mutation == MUT_GAUSSIAN || a.mutation == MUT_UNIFORM) && a.mut_rate > 0.f;
+  const bool reset_one = MUTATES && a.mutation == MUT_RESET_ONE;
+  const bool shift = (a.obj_i & 1) && a.obj_data2 && real_obj_rotatable(a.objective);
+  const bool rosen = a.objective == OBJ_ROSENBROCK;
+
+  if (MODE == MODE_GEN && a.n_elite > 0 && a.elite_idx == nullptr && blockIdx.x == 0) {
+    unsigned long long b = block_reduce_parts(a.best_cur, a.n_best_cur, lds_red);
+    if (threadIdx.x == 0) lds_elite = (uint32_t)best_index(b);
+  }
+  if (per_gene_mut)
+    for (uint32_t i = threadIdx.x; i < kMutCap; i += kBlock) lds_thr[i] = a.mut_thr[i];
+  __syncthreads();
+
+  unsigned long long my_best = 0;
+  for (uint64_t child = (uint64_t)blockIdx.x * GPB + g; child < a.S; child += (uint64_t)gridDim.x * GPB) {
+    const bool elite = MODE == MODE_GEN && child < a.n_elite;  // wave-uniform
+    const uint32_t src = elite ? (a.elite_idx ? a.elite_idx[child] : lds_elite) : 0u;
+    const bool breeds = !elite && (MODE == MODE_GEN || MODE == MODE_CROSS || MODE == MODE_MUTATE);
+    Pool<GS> pool{u32x4{0, 0, 0, 0}, 0u};
+    uint32_t pa = 0, pb = 0, blo = 0, bhi = 0, rpos = 0xFFFFFFFFu;
+    bool xo = false;
+    float ua = 0.f, rval = 0.f;
+    if (breeds) {
+      pool.w = draw(a.key, ST_CHILD, child, q);
+      if (MODE == MODE_GEN || MODE == MODE_CROSS) {
+        select_parents<GS>(a, pool, child, pa, pb);
+        xo = a.crossover != XO_NONE && do_crossover(a, pool.get(W_XOPROB, a.key, child));
+        if (a.crossover == XO_ONE_POINT) {
+          blo = word_to_index(pool.get(W_CUT1, a.key, child), L);
+          bhi = L;
+        } else if (a.crossover == XO_TWO_POINT) {
+          const uint32_t c1 = word_to_index(pool.get(W_CUT1, a.key, child), L);
+          const uint32_t c2 = word_to_index(pool.get(W_CUT2, a.key, child), L);
+          blo = c1 < c2 ? c1 : c2;
+          bhi = c1 < c2 ? c2 : c1;
+        } else if (a.crossover == XO_ARITHMETIC) {
+          ua = word_to_unit(pool.get(W_CUT1, a.key, child));
+        }
+      }
+      if (reset_one && pool.get(W_MUTIND, a.key, child) < a.mut_ind_thresh) {
+        rpos = word_to_index(pool.get(W_MUTPOS, a.key, child), L);
+        rval = real_reset_value(a, pool.get(W_SEL + sel_words(a), a.key, child));
+      }
+    }
+    RealAcc acc{0.f, 0.f, 1.f};
+    float dz = 0.f, dx = 0.f;  // lane 63: the deferred Rosenbrock term of its last gene
+    uint32_t dd = 0xFFFFFFFFu;
+    for (uint32_t c0 = 0; c0 < nchunks; c0 += GS) {  // wave-uniform
+      const uint32_t c = c0 + q;
+      const bool have = c < nchunks;
+      const uint32_t clen = have ? (L - 4 * c >= 4 ? 4u : L - 4 * c) : 0u;
+      float v[4] = {0.f, 0.f, 0.f, 0.f};
+      if (have) {
+        if (elite) {
+          const float4 e = cur[(uint64_t)src * rs + c];
+          v[0] = e.x; v[1] = e.y; v[2] = e.z; v[3] = e.w;
+        } else if (MODE == MODE_INIT) {
+          real_init_chunk(a, child, c, v);
+        } else if (MODE == MODE_EVAL || MODE == MODE_MUTATE) {
+          const float4 e = cur[child * rs + c];
+          v[0] = e.x; v[1] = e.y; v[2] = e.z; v[3] = e.w;
+        }
+        if (breeds && (MODE == MODE_GEN || MODE == MODE_CROSS)) {
+          const float4 A4 = cur[(uint64_t)pa * rs + c], B4 = cur[(uint64_t)pb * rs + c];
+          const float A[4] = {A4.x, A4.y, A4.z, A4.w}, B[4] = {B4.x, B4.y, B4.z, B4.w};
+          real_cross_chunk(a, child, c, A, B, xo, blo, bhi, ua, v);
+        }
+        if (breeds && per_gene_mut) {
+          real_mutate_chunk(a, child, c, clen, c == q ? pool.w.w : chunk_mut_word(a.key, child, c), lds_thr, v);
+        } else if (breeds && (rpos >> 2) == c) {
+          const uint32_t j = rpos & 3u;
+          v[0] = j == 0 ? rval : v[0];
+          v[1] = j == 1 ? rval : v[1];
+          v[2] = j == 2 ? rval : v[2];
+          v[3] = j == 3 ? rval : v[3];
+        }
+        for (uint32_t j = 0; j < 4; ++j) v[j] = j < clen ? v[j] : 0.f;
+        if (MODE != MODE_EVAL) nxt[child * rs + c] = make_float4(v[0], v[1], v[2], v[3]);
+      }
+      if (evals && !elite) {
+        float x[4];
+        for (uint32_t j = 0; j < 4; ++j) {
+          const uint32_t d = 4 * c + j;
+          x[j] = (shift && d < L) ? v[j] - a.obj_data2[d] : v[j];
+          if (d >= L) x[j] = 0.f;
+        }
+        const float nx0 = __shfl_down(x[0], 1, 64);  // first gene of chunk c + 1 (lanes < 63)
+        if (rosen) {
+          const float first = __shfl(x[0], 0, 64);  // this segment's chunk c0 = previous lane 63's c + 1
+          if (q == 63 && dd != 0xFFFFFFFFu) real_obj_term(a, dd, dz, first, dx, acc);
+          dd = 0xFFFFFFFFu;
+        }
+        for (uint32_t j = 0; j < 4; ++j) {
+          const uint32_t d = 4 * c + j;
+          if (d >= L) continue;
+          if (rosen && j == 3 && q == 63) {  // neighbour in the next segment
+            dd = d;
+            dz = x[3];
+            dx = v[3];
+            continue;
+          }
+          const float zn = j < 3 ? x[j + 1] : nx0;
+          real_obj_term(a, d, x[j], zn, v[j], acc);
+        }
+      }
+    }
+    float score = 0.f;
+    if (evals) {
+      acc.s0 = group_sum<GS>(acc.s0);
+      acc.s1 = group_sum<GS>(acc.s1);
+      acc.s2 = group_prod<GS>(acc.s2);
+      score = elite ? a.score_cur[src] : real_obj_finish(a, acc);
+    }
+    if (evals && q == 0) {
+      a.score_next[child] = score;
+      const unsigned long long pk = pack_best(score, child);
+      my_best = pk > my_best ? pk : my_best;
     }
   }
   if (evals && best_parts) {
@@ -903,9 +1054,24 @@ uint32_t launch_rot(int mode, const GenArgs& a, unsigned long long* parts, hipSt
 }  // namespace
 
 uint32_t real_launch(int mode, const GenArgs& a, unsigned long long* best_parts, hipStream_t s) {
-  if (a.chunks > 64) throw std::invalid_argument("REAL encoding supports at most 256 genes");
   const bool rot = (a.obj_i & 2) && real_obj_rotatable(a.objective);
   if (rot && a.L > 128) throw std::invalid_argument("rotated objectives support at most 128 dimensions");
+  if (a.chunks > 64) {
+    if (a.objective == OBJ_TSP_RANDOM_KEY || a.objective == OBJ_USER_FNPTR)
+      throw std::invalid_argument("the random-key TSP and function-pointer objectives support at most 256 genes");
+    static bool c[5] = {false, false, false, false, false};
+    constexpr uint32_t per_block = kBlock / 64;
+    uint32_t grid = 0;
+    switch (mode) {
+      case MODE_GEN: grid = launch_occ(real_long_kernel<MODE_GEN>, per_block, 0, a, best_parts, s, c[0]); break;
+      case MODE_INIT: grid = launch_occ(real_long_kernel<MODE_INIT>, per_block, 0, a, best_parts, s, c[1]); break;
+      case MODE_EVAL: grid = launch_occ(real_long_kernel<MODE_EVAL>, per_block, 0, a, best_parts, s, c[2]); break;
+      case MODE_CROSS: grid = launch_occ(real_long_kernel<MODE_CROSS>, per_block, 0, a, best_parts, s, c[3]); break;
+      default: grid = launch_occ(real_long_kernel<MODE_MUTATE>, per_block, 0, a, best_parts, s, c[4]); break;
+    }
+    PGA_HIP_CHECK(hipGetLastError());
+    return grid;
+  }
   uint32_t grid = 0;
   switch (group_size(a.chunks)) {
     case 1: grid = launch_rot<1>(mode, a, best_parts, s); break;

@@ -27,6 +27,12 @@ PROBLEMS = {
     "ackley_rot20": lambda: M.Ackley(20, rotate=True, shift=True, seed=7),
     "rosenbrock_rot24": lambda: M.Rosenbrock(24, rotate=True, seed=8),
     "griewank_rot32": lambda: M.Griewank(32, rotate=True, seed=9),
+    # long genomes (> 256 genes: the chunk-segment kernel, one wave per individual)
+    "rastrigin_1024": lambda: M.Rastrigin(1024),
+    "sum_1024": lambda: M.SumGenes(1024),
+    "rosenbrock_1000": lambda: M.Rosenbrock(1000),
+    "ackley_777_shift": lambda: M.Ackley(777, shift=True, seed=2),
+    "sphere_4096": lambda: M.Sphere(4096),
 }
 
 
@@ -65,6 +71,18 @@ def test_reference_knapsack_optimum():
     s, g = ga.best()
     assert s == 285.0
     assert p.counts(g.unsqueeze(0))[0].tolist() == [0, 0, 1, 1, 0, 0]
+
+
+@pytest.mark.parametrize("xo", ["uniform", "two_point", "arithmetic"])
+@pytest.mark.parametrize("mut", ["gaussian", "reset_one"])
+def test_cpu_long_genome_operators(xo, mut):
+    """L = 1030 (> 256 genes): every operator over a chunk-segment layout."""
+    p = M.Rosenbrock(1030)
+    ga = pga.GeneticAlgorithm(p, 64, seed=4, device="cpu", crossover=xo, mutation=mut, elitism=1)
+    s0 = ga.best_score()
+    ga.run(3)
+    assert ga.best_score() >= s0
+    assert close(p.reference_fitness(ga.genomes()), ga.scores, rel=1e-4, abs_=1.0)
 
 
 def test_sum_genes_improves():
@@ -107,3 +125,26 @@ def test_gpu_rastrigin30_rotated_mfma_1m():
     ref = p.reference_fitness(ga.genomes()[idx])
     assert close(ref, ga.scores[idx], rel=1e-4, abs_=5e-3)
     assert ga.best_score() > b0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("xo", ["uniform", "one_point", "blend"])
+@pytest.mark.parametrize("mut", ["gaussian", "uniform", "reset_one"])
+def test_gpu_long_genome_bitexact_rows(xo, mut):
+    """Sphere-1000 / sum-1024: the long-genome kernel's children equal the
+    CPU backend's bit for bit over several generations (gaussian mutation:
+    to libm tolerance), scores to float rounding."""
+    for p in (M.Sphere(1000), M.SumGenes(1024)):
+        kw = dict(seed=13, elitism=1, crossover=xo, mutation=mut)
+        g = pga.GeneticAlgorithm(p, 512, device="cuda:0", **kw)
+        c = pga.GeneticAlgorithm(p, 512, device="cpu", **kw)
+        g.run(3)
+        c.run(3)
+        torch.cuda.synchronize()
+        if mut == "gaussian":  # Box-Muller: device and host libm differ by ulps
+            same = torch.isclose(g.genomes().cpu(), c.genomes(), rtol=1e-4, atol=1e-4).all(-1).float().mean()
+            assert same.item() > 0.99
+            assert close(p.reference_fitness(g.genomes().cpu()), g.scores.cpu())
+        else:  # children bit for bit; scores to rounding (the device contracts a*b+c into fma)
+            assert torch.equal(g.rows.cpu(), c.rows)
+            assert close(g.scores.cpu(), c.scores, rel=1e-5, abs_=1e-2)
