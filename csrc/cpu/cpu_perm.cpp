@@ -45,7 +45,7 @@ void perm_crossover(int op, const uint16_t* A, const uint16_t* B, uint32_t L, ui
 }
 
 uint32_t perm_run(int mode, const GenArgs& a, unsigned long long* best_parts) {
-  if (a.L > kPermMaxL) throw std::invalid_argument("PERMUTATION encoding supports at most 4096 genes");
+  if (a.L > 65535) throw std::invalid_argument("PERMUTATION encoding supports at most 65535 genes (u16 city ids)");
   const uint32_t L = a.L, nch = a.chunks, lp = 8 * nch, GS = group_size(nch);
   const uint64_t rw = a.row_words;
   const uint16_t* cur = (const uint16_t*)a.cur;

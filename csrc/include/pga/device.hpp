@@ -38,28 +38,31 @@ __device__ __forceinline__ unsigned long long shfl_xor_u64(unsigned long long v,
   return ((unsigned long long)hi << 32) | lo;
 }
 
-// block-wide max of a packed best, result valid in every thread
+// block-wide max of a packed best, result valid in every thread (BLK threads)
+template <int BLK = kBlock>
 __device__ __forceinline__ unsigned long long block_max_u64(unsigned long long v, unsigned long long* lds4) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
     unsigned long long w = shfl_xor_u64(v, o);
     v = w > v ? w : v;
   }
+  if (BLK == 64) return v;
   __syncthreads();
   if (lane_id() == 0) lds4[threadIdx.x >> 6] = v;
   __syncthreads();
   unsigned long long r = lds4[0];
 #pragma unroll
-  for (int i = 1; i < kBlock / 64; ++i) r = lds4[i] > r ? lds4[i] : r;
+  for (int i = 1; i < BLK / 64; ++i) r = lds4[i] > r ? lds4[i] : r;
   return r;
 }
 
 // reduce an array of packed bests with the whole block
+template <int BLK = kBlock>
 __device__ __forceinline__ unsigned long long block_reduce_parts(const unsigned long long* parts, uint32_t n,
                                                                  unsigned long long* lds4) {
   unsigned long long v = 0;
-  for (uint32_t i = threadIdx.x; i < n; i += kBlock) v = parts[i] > v ? parts[i] : v;
-  return block_max_u64(v, lds4);
+  for (uint32_t i = threadIdx.x; i < n; i += BLK) v = parts[i] > v ? parts[i] : v;
+  return block_max_u64<BLK>(v, lds4);
 }
 
 // Child word pool: lane q of a GS-lane group holds Philox block q of the

@@ -9,7 +9,9 @@
 
 namespace pga {
 
-constexpr uint32_t kPermMaxL = 4096;  // LDS-resident crossover limit
+// longest genome of the 4-individuals-per-block kernels (their LDS arrays);
+// longer ones run one individual per 64-lane block (perm.hip go_long)
+constexpr uint32_t kPermMaxL = 4096;
 
 // child-word layout extension for permutations
 //   W_CUT1, W_CUT2  segment [lo, hi) of parent A (PMX / OX)

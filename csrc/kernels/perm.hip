@@ -19,6 +19,8 @@
 // BASELINE config 5.
 #include <hip/hip_runtime.h>
 
+#include <string>
+
 #include "pga/device.hpp"
 #include "pga/ops.hpp"
 #include "pga/perm_ops.hpp"
@@ -30,8 +32,12 @@ using namespace dev;
 constexpr uint16_t kNone = 0xFFFF;
 constexpr uint32_t kHdrF = 144;  // floats: red u64[4] (8 floats) | elite | pad  (16-aligned)
 
-__host__ __device__ inline size_t perm_lds_bytes(uint32_t GS, uint32_t chunks, bool euc) {
-  const uint32_t gpb = 256 / GS;
+inline uint32_t perm_max_length(bool euc) {  // longest genome the one-individual-per-block kernel holds in LDS
+  return (uint32_t)((160 * 1024 - 4 * kHdrF) / (euc ? 16 : 8)) / 8 * 8;
+}
+
+__host__ __device__ inline size_t perm_lds_bytes(uint32_t GS, uint32_t chunks, bool euc, uint32_t blk = 256) {
+  const uint32_t gpb = blk / GS;
   const size_t lp = 8ull * chunks;  // genes per padded row
   return 4ull * kHdrF + (euc ? 8ull * chunks * 8 : 0) + (size_t)gpb * 4 * lp * 2;
 }
@@ -54,8 +60,8 @@ __device__ __forceinline__ void ld8(const uint16_t* p, uint32_t e[8]) {
   e[4] = v.z & 0xFFFF; e[5] = v.z >> 16; e[6] = v.w & 0xFFFF; e[7] = v.w >> 16;
 }
 
-template <int GS, int MODE, int OBJ>
-__global__ __launch_bounds__(kBlock) void perm_kernel(GenArgs a, unsigned long long* best_parts) {
+template <int GS, int MODE, int OBJ, int BLK = kBlock>
+__global__ __launch_bounds__(BLK) void perm_kernel(GenArgs a, unsigned long long* best_parts) {
   resolve_gen(a);
   extern __shared__ __attribute__((aligned(16))) float smem[];
   unsigned long long* lds_red = (unsigned long long*)smem;
@@ -67,7 +73,7 @@ __global__ __launch_bounds__(kBlock) void perm_kernel(GenArgs a, unsigned long l
   const uint32_t lane = lane_id();
   const uint32_t q = lane & (GS - 1);
   const uint32_t gbase = lane & ~(uint32_t)(GS - 1);
-  constexpr uint32_t GPB = kBlock / GS;
+  constexpr uint32_t GPB = BLK / GS;
   const uint32_t g = threadIdx.x / GS;
   uint16_t* A = arena + (size_t)g * 4 * lp;
   uint16_t* B = A + lp;
@@ -82,11 +88,11 @@ __global__ __launch_bounds__(kBlock) void perm_kernel(GenArgs a, unsigned long l
   const bool mut_on = MUTATES && (a.mutation == MUT_SWAP || a.mutation == MUT_INVERSION);
 
   if (MODE == MODE_GEN && a.n_elite > 0 && a.elite_idx == nullptr && blockIdx.x == 0) {
-    unsigned long long b = block_reduce_parts(a.best_cur, a.n_best_cur, lds_red);
+    unsigned long long b = block_reduce_parts<BLK>(a.best_cur, a.n_best_cur, lds_red);
     if (threadIdx.x == 0) *lds_elite = (uint32_t)best_index(b);
   }
   if (OBJ == OBJ_TSP_EUC)
-    for (uint32_t i = threadIdx.x; i < 2 * L; i += kBlock) coords[i] = a.obj_data[i];
+    for (uint32_t i = threadIdx.x; i < 2 * L; i += BLK) coords[i] = a.obj_data[i];
   __syncthreads();
 
   unsigned long long my_best = 0;
@@ -263,7 +269,7 @@ __global__ __launch_bounds__(kBlock) void perm_kernel(GenArgs a, unsigned long l
     __syncthreads();  // C is rewritten next iteration
   }
   if (EVALS && best_parts) {
-    unsigned long long b = block_max_u64(my_best, lds_red);
+    unsigned long long b = block_max_u64<BLK>(my_best, lds_red);
     if (threadIdx.x == 0) best_parts[blockIdx.x] = b;
   }
 }
@@ -482,8 +488,34 @@ __global__ __launch_bounds__(kBlock) void perm_gen_fast(GenArgs a, unsigned long
   }
 }
 
+// Genomes beyond kPermMaxL genes: one 64-lane block per individual, so the
+// four per-child LDS arrays (8 L bytes, +8 L of EUC coordinates) fit in
+// 160 KiB up to ~20 000 cities (u16 ids cap L at 65 535 anyway)
+template <int MODE, int OBJ>
+uint32_t go_long(const GenArgs& a, unsigned long long* parts, hipStream_t s) {
+  const size_t lds = perm_lds_bytes(64, a.chunks, OBJ == OBJ_TSP_EUC, 64);
+  if (lds > 160 * 1024)
+    throw std::invalid_argument("PERMUTATION genome too long for the LDS-resident crossover (" + std::to_string(a.L) +
+                                " genes; at most " + std::to_string(perm_max_length(OBJ == OBJ_TSP_EUC)) + ")");
+  auto k = perm_kernel<64, MODE, OBJ, 64>;
+  static bool configured = false;
+  if (!configured) {
+    PGA_HIP_CHECK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    configured = true;
+  }
+  int per_cu = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)k, 64, lds) != hipSuccess || per_cu <= 0)
+    per_cu = 1;
+  uint64_t cap = (uint64_t)device_cu_count() * per_cu;
+  if (cap > kMaxGrid) cap = kMaxGrid;
+  const uint32_t grid = (uint32_t)(a.S < cap ? a.S : cap);
+  hipLaunchKernelGGL(k, grid, 64, lds, s, a, parts);
+  return grid;
+}
+
 template <int GS, int MODE, int OBJ>
 uint32_t go(const GenArgs& a, unsigned long long* parts, hipStream_t s) {
+  if (GS == 64 && a.L > kPermMaxL) return go_long<MODE, OBJ>(a, parts, s);
   const size_t lds = perm_lds_bytes(GS, a.chunks, OBJ == OBJ_TSP_EUC);
   auto k = perm_kernel<GS, MODE, OBJ>;
   static bool configured = false;
@@ -550,7 +582,7 @@ uint32_t launch_obj(int mode, const GenArgs& a, unsigned long long* parts, hipSt
 }  // namespace
 
 uint32_t perm_launch(int mode, const GenArgs& a, unsigned long long* best_parts, hipStream_t s) {
-  if (a.L > kPermMaxL) throw std::invalid_argument("PERMUTATION encoding supports at most 4096 genes");
+  if (a.L > 65535) throw std::invalid_argument("PERMUTATION encoding supports at most 65535 genes (u16 city ids)");
   uint32_t grid = 0;
   switch (group_size(a.chunks)) {
     case 1: grid = launch_obj<1>(mode, a, best_parts, s); break;

@@ -24,8 +24,8 @@ class TSP(Problem):
         n = self.dist.shape[0]
         if self.dist.shape != (n, n):
             raise ValueError("distance matrix must be square")
-        if n > 4096:
-            raise ValueError("at most 4096 cities")
+        if n > 65535:
+            raise ValueError("at most 65535 cities (u16 ids); on the GPU at most ~20400 (LDS-resident crossover)")
         self.length = n
         self.open_path = open_path
         self.objective = C.OBJ_TSP_OPEN if open_path else C.OBJ_TSP
@@ -64,8 +64,8 @@ class TSPEuclidean(Problem):
         if self.coords.ndim != 2 or self.coords.shape[1] != 2:
             raise ValueError("coords must be [n, 2]")
         self.length = int(self.coords.shape[0])
-        if self.length > 4096:
-            raise ValueError("at most 4096 cities")
+        if self.length > 65535:
+            raise ValueError("at most 65535 cities (u16 ids); on the GPU at most ~10200 (LDS-resident crossover)")
         self.objective = C.OBJ_TSP_EUC
 
     def data(self):

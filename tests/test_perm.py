@@ -101,6 +101,41 @@ def test_gpu_bitexact_selections(sel):
     assert torch.equal(g.scores.cpu(), c.scores)
 
 
+@pytest.mark.parametrize("xo", ["ox", "pmx"])
+def test_cpu_long_genome(xo):
+    """Tours beyond the 4096 genes of the 4-per-block kernels (the GPU runs
+    them one individual per 64-lane block)."""
+    p = M.TSPEuclidean.random(6000, seed=3)
+    ga = pga.GeneticAlgorithm(p, 24, seed=2, device="cpu", crossover=xo, mutation="inversion", elitism=1)
+    ga.run(2)
+    assert is_perm(ga.genomes())
+    assert torch.allclose(p.reference_fitness(ga.genomes()), ga.scores, rtol=1e-4)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("xo", ["ox", "pmx"])
+@pytest.mark.parametrize("n,prob", [(4104, "euc"), (10000, "euc"), (8192, "matrix")])
+def test_gpu_long_genome_bitexact(xo, n, prob):
+    p = M.TSPEuclidean.random(n, seed=7) if prob == "euc" else M.TSP.random_euclidean(n, seed=7)
+    kw = dict(seed=3, crossover=xo, mutation="inversion", mutation_rate=0.5, elitism=1)
+    g = pga.GeneticAlgorithm(p, 300, device="cuda:0", **kw)
+    c = pga.GeneticAlgorithm(p, 300, device="cpu", **kw)
+    for _ in range(2):
+        g.run(1)
+        c.run(1)
+    torch.cuda.synchronize()
+    assert torch.equal(g.rows.cpu(), c.rows)
+    assert torch.equal(g.scores.cpu(), c.scores)
+    assert is_perm(g.genomes().cpu())
+
+
+@pytest.mark.gpu
+def test_gpu_long_genome_too_long():
+    p = M.TSPEuclidean.random(12000, seed=1)
+    with pytest.raises(Exception, match="too long"):
+        pga.GeneticAlgorithm(p, 16, device="cuda:0")
+
+
 def test_cpu_rank_selection_tsp():
     p = M.TSP.random_euclidean(32, seed=4)
     ga = pga.GeneticAlgorithm(p, 512, seed=1, device="cpu", selection="rank", rank_pressure=1.8, elitism=1)
