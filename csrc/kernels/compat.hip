@@ -73,9 +73,11 @@ __global__ __launch_bounds__(kBlock) void compat_kernel(GenArgs a, unsigned long
     }
     __syncthreads();
   }
-  const uint64_t child = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
   unsigned long long my_best = 0;
-  if (child < a.S) {
+  // grid-stride over children (the reference RUN_KERNEL loop serves any S,
+  // src/pga.cu:62-70); the grid is sized to the device, not to S
+  for (uint64_t child = (uint64_t)blockIdx.x * kBlock + threadIdx.x; child < a.S;
+       child += (uint64_t)gridDim.x * kBlock) {
     float* c = nxt + child * rw;
     float* rand = a.compat_rand + child * L;
     float score = 0.f;
@@ -121,7 +123,8 @@ __global__ __launch_bounds__(kBlock) void compat_kernel(GenArgs a, unsigned long
     }
     if (evals) {
       a.score_next[child] = score;
-      my_best = pack_best(score, child);
+      const unsigned long long pb = pack_best(score, child);
+      if (pb > my_best) my_best = pb;
     }
   }
   if (evals && best_parts) {
@@ -134,9 +137,11 @@ __global__ __launch_bounds__(kBlock) void compat_kernel(GenArgs a, unsigned long
 
 uint32_t compat_launch(int mode, const GenArgs& a, unsigned long long* best_parts, hipStream_t s) {
   if (!a.compat_rand) throw std::runtime_error("compat path needs its rand scratch buffer");
+  // indirect calls pin a dynamic stack, so residency (not S) sizes the grid:
+  // a few blocks per CU keep every SIMD busy while the loop covers any S
   const uint64_t need = (a.S + kBlock - 1) / kBlock;
-  if (need > kMaxGrid) throw std::invalid_argument("compat path supports at most 8192*256 individuals");
-  const uint32_t grid = (uint32_t)need;
+  const uint64_t cap = (uint64_t)device_cu_count() * 8;
+  const uint32_t grid = (uint32_t)(need < cap ? (need ? need : 1) : cap);
   switch (mode) {
     case MODE_GEN: hipLaunchKernelGGL(compat_kernel<MODE_GEN>, grid, kBlock, 0, s, a, best_parts); break;
     case MODE_INIT: hipLaunchKernelGGL(compat_kernel<MODE_INIT>, grid, kBlock, 0, s, a, best_parts); break;

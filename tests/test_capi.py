@@ -195,6 +195,14 @@ def test_example_e1_user_objective():
 
 
 @pytest.mark.gpu
+def test_example_e1_callbacks_4m():
+    """User objective + user mutation (the reference-ABI callback kernel) on
+    4M individuals: every score must be a real evaluation (grid-stride)."""
+    rc, out = run_ex([os.path.join(EX, "e1_onemax_float"), "60", str(4 << 20), "cb"])
+    assert rc == 0, out
+
+
+@pytest.mark.gpu
 def test_example_e2_knapsack():
     rc, out = run_ex([os.path.join(EX, "e2_knapsack"), "10"])
     assert rc == 0, out
