@@ -15,6 +15,7 @@ Configs (BASELINE.md "Targets" table):
   e2_knap_refops    reference example E2 (S=100, L=6), launch-bound (hipGraph)
   onemax64_gpu      OneMax 64-bit, pop=1024 on the GPU (launch-bound)
   onemax1024_jit    the headline island with a hipRTC-compiled objective
+  knapsack1024      0/1 knapsack, 1024 items, pop=1M (matrix-core evaluation)
 The 8-GPU island configs are bench.py under torchrun (the driver runs those).
 Each line: gens/s, evals/s, ms/gen, best fitness, effective HBM GB/s (the
 bytes one generation must move at minimum: read 2 parent rows + write 1
@@ -77,6 +78,10 @@ def make(name: str):
     if name == "qubo1024":
         # dense 1024-variable QUBO (1M int8 MACs per individual)
         return M.QUBO.random(1024, seed=1, lo=-128, hi=127), 1 << 18, None, dict(elitism=1), 20
+    if name == "knapsack1024":
+        # 0/1 knapsack, 1024 items (integer values / weights 1..99): the
+        # integer-exact instance runs its evaluation on the int8 matrix cores
+        return M.Knapsack01.random(1024, seed=1), 1 << 20, None, dict(elitism=1), 200
     if name == "onemax1024_rank":
         return M.OneMax(1024), 1 << 20, None, dict(elitism=1, selection="rank", rank_pressure=1.5), 100
     raise KeyError(name)
@@ -84,7 +89,7 @@ def make(name: str):
 
 NAMES = ["onemax64_cpu", "onemax1024", "rastrigin30", "rastrigin30_rot", "tsp256_ox", "tsp256_pmx", "e1_sum100_refops",
          "tsp256_euc_ox", "tsp256_euc_pmx", "e2_knap_refops", "onemax64_gpu", "onemax1024_jit", "maxcut512_qubo",
-         "qubo1024", "onemax1024_rank"]
+         "qubo1024", "onemax1024_rank", "knapsack1024"]
 
 
 def qubo_padded(L: int) -> int:

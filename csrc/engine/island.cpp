@@ -67,7 +67,8 @@ Island::Island(const Config& cfg, int device) : cfg_(cfg), device_(device) {
 Island::~Island() {
   Buffer* all[] = {&rows_[0],   &rows_[1],     &scores_[0],   &scores_[1],  &best_[0],  &best_[1],   &mut_thr_,
                    &obj_data_[0], &obj_data_[1], &keys_[0], &keys_[1], &elite_idx_, &cumfit_, &cum_ws_, &topk_ws_, &stats_,
-                   &out_best_,  &scratch_, &compat_rand_, &ev_parts_, &gen_dev_, &rank_order_, &rank_ws_, &qubo_qt_};
+                   &out_best_,  &scratch_, &compat_rand_, &ev_parts_, &gen_dev_, &rank_order_, &rank_ws_, &qubo_qt_,
+                   &knap_tab_};
   drop_graph();
   if (cap_stream_) (void)hipStreamDestroy(cap_stream_);
   for (Buffer* b : all) {
@@ -190,10 +191,24 @@ void Island::set_objective_data(const float* host, size_t n, int which) {
   obj_data_[which] = alloc(4ull * (n ? n : 1));
   if (n) copy_to_device(obj_data_[which].ptr, host, 4ull * n);
   obj_len_[which] = n;
+  if (which == 0) obj_host0_.assign(host, host + n);
   ++obj_version_;
 }
 
 void Island::prepare_objective() {
+  if (cfg_.objective == OBJ_KNAPSACK && cfg_.encoding == ENC_BINARY && on_gpu() && knap_version_ != obj_version_) {
+    knap_version_ = obj_version_;
+    knap_dig_ = knap_cols_ = 0;
+    std::vector<uint8_t> tab;
+    if (obj_host0_.size() >= 2ull * cfg_.L &&
+        build_knap_table(obj_host0_.data(), obj_host0_.data() + cfg_.L, cfg_.L, chunks_, tab, knap_dig_, knap_cols_)) {
+      if (knap_tab_.bytes < tab.size()) {
+        release(knap_tab_);
+        knap_tab_ = alloc(tab.size());
+      }
+      copy_to_device(knap_tab_.ptr, tab.data(), tab.size());
+    }
+  }
   if (cfg_.objective != OBJ_QUBO) return;
   if (cfg_.encoding != ENC_BINARY) throw std::invalid_argument("the QUBO objective needs the BINARY encoding");
   if (obj_len_[0] < (size_t)cfg_.L * cfg_.L) throw std::invalid_argument("QUBO: objective data must hold the L x L matrix Q");
@@ -213,6 +228,11 @@ GenArgs Island::make_args(int mode) {
   GenArgs a;
   std::memset(&a, 0, sizeof(a));
   a.qubo_qt = (const int8_t*)qubo_qt_.ptr;
+  if (cfg_.objective == OBJ_KNAPSACK && knap_cols_ > 0) {
+    a.knap_tab = knap_tab_.ptr;
+    a.knap_dig = knap_dig_;
+    a.knap_cols = knap_cols_;
+  }
   const int nx = cur_ ^ 1;
   a.cur = rows_[cur_].ptr;
   a.next = rows_[nx].ptr;

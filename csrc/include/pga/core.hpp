@@ -311,6 +311,11 @@ struct GenArgs {
   // derived objective data built by the runtime (QUBO: int8 Q^T padded to
   // qubo_padded_length(L) square); nullptr when unused
   const int8_t* qubo_qt;
+  // BINARY knapsack on the matrix cores (binary.hip knap_mfma): int8 digit
+  // table of [values | weights] in B-fragment order, its digit count and
+  // column count; nullptr when the instance is not integer-exact
+  const void* knap_tab;
+  uint32_t knap_dig, knap_cols;
 
   // padding mask for the last chunk (BINARY)
   u32x4 last_mask;

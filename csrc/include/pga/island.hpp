@@ -142,6 +142,9 @@ class Island {
   void set_graph_generations(uint32_t g);
   uint32_t graph_generations() const { return graph_g_; }
   uint64_t graph_replays() const { return graph_replays_; }
+  // BINARY knapsack: int8 digits per value of the matrix-core evaluation
+  // (0: the instance is not integer-exact and runs the scalar evaluation)
+  uint32_t knapsack_digits() const { return knap_dig_; }
 
   // checkpoint: header + current rows + scores
   void save(const std::string& path);
@@ -173,6 +176,9 @@ class Island {
   uint32_t obj_version_ = 0, qubo_version_ = ~0u;
   void prepare_objective();      // derived objective data (QUBO packing)
   size_t obj_len_[2] = {0, 0};
+  std::vector<float> obj_host0_;  // host copy of objective data slot 0 (derived tables)
+  Buffer knap_tab_;               // BINARY knapsack: matrix-core digit table (GPU, integer instances)
+  uint32_t knap_version_ = ~0u, knap_dig_ = 0, knap_cols_ = 0;
   float mut_inv_ = 0.f;
   bool mut_sparse_ = false;  // BINARY bit-flip uses the sparse (Binomial) sampler
   float mut_rate_eff_ = 0.f;

@@ -11,6 +11,7 @@
 
 #include <stdexcept>
 #include <string>
+#include <vector>
 
 #include "pga/core.hpp"
 
@@ -46,6 +47,12 @@ bool force_generic_kernels();
 // ---- encodings: one launch per call, returns the grid used (= number of
 // valid entries written to best_parts, when the mode evaluates) ----
 uint32_t binary_launch(int mode, const GenArgs& a, unsigned long long* best_parts, hipStream_t s);
+// Knapsack digit table for the matrix-core evaluation (binary.hip): false
+// (table empty) when the instance does not qualify -- non-integer values or
+// weights, sums of magnitudes >= 2^24, fewer than 4 lanes per individual, or
+// more than 16 digit columns
+bool build_knap_table(const float* values, const float* weights, uint32_t L, uint32_t chunks,
+                      std::vector<uint8_t>& tab, uint32_t& digits, uint32_t& cols);
 uint32_t real_launch(int mode, const GenArgs& a, unsigned long long* best_parts, hipStream_t s);
 uint32_t perm_launch(int mode, const GenArgs& a, unsigned long long* best_parts, hipStream_t s);
 

@@ -21,6 +21,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cmath>
 #include <cstdio>
 
 #include "pga/device.hpp"
@@ -115,6 +116,95 @@ __device__ __forceinline__ uint4 bit4(uint32_t b) {  // one bit of a 128-bit chu
 __device__ __forceinline__ uint32_t chunk_len(uint32_t L, uint32_t c) {
   const uint32_t b = c * 128u;
   return L - b >= 128u ? 128u : L - b;
+}
+
+// ---------------------------------------------------------------------------
+// 0/1 knapsack on the matrix cores (the hot kernel's evaluation when the
+// instance is integer-exact, see build_knap_table).
+//
+// score needs V = bits . values and W = bits . weights per child.  A wave's
+// step holds its NG children as 64 16-byte chunks (lane = g*GS + q), staged
+// in its LDS scratch as 16 "virtual rows" of 512 bits: virtual row m = the
+// chunks of lanes 4m..4m+3 = part r = m % R (R = GS/4) of child m / R.  One
+// v_mfma_i32_16x16x64_i8 per 64-bit slice s (8 slices):
+//   A[m][k] = bit k of virtual row m (expanded to int8 0/1),
+//   B[k][c] = digit d of quantity qty (values | weights) of the gene bit k of
+//             part r stands for, column c = (2r + qty) * D + d,
+// with balanced base-256 digits in [-128, 127] (D <= 4), so C[m][c] is an
+// exact partial dot product in i32 and only the columns of row m's own part
+// are used:  V = sum_r sum_d C[gR + r][2rD + d] 256^d  (W: qty = 1).
+// The element order inside a slice (element j of lane group h <-> bit 16h + j
+// of the slice's 64) is the same for A and B, so the hardware's internal k
+// permutation cannot matter; the integer result equals the CPU backend's
+// float sum bit for bit (every partial sum is an integer below 2^24).
+// Reference: test2/test.cu:28-36 (the knapsack objective); SURVEY.md C10.
+// ---------------------------------------------------------------------------
+typedef int v4i __attribute__((ext_vector_type(4)));
+constexpr int kObjKnapMfma = 1000;  // launcher-only objective id: OBJ_KNAPSACK via knap_mfma
+constexpr uint32_t kKnapSlices = 8;  // 512-bit virtual row / 64-bit MFMA k-step
+constexpr uint32_t kKnapMaxCols = 16;
+
+__device__ __forceinline__ v4i expand16(uint32_t h) {  // 16 bits -> 16 int8 {0,1}
+  v4i r;
+  r[0] = (int)(__umul24(h & 0xFu, 0x00204081u) & 0x01010101u);
+  r[1] = (int)(__umul24((h >> 4) & 0xFu, 0x00204081u) & 0x01010101u);
+  r[2] = (int)(__umul24((h >> 8) & 0xFu, 0x00204081u) & 0x01010101u);
+  r[3] = (int)(__umul24((h >> 12) & 0xFu, 0x00204081u) & 0x01010101u);
+  return r;
+}
+
+// LDS written by other lanes of this wave is read after it (LDS ops of one
+// wave complete in order; this only stops the compiler moving them)
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// chunk slot of lane 4m + h in the wave scratch: virtual row m, lane group h,
+// XOR-swizzled so that both the lane-order store and the (h, n) fragment
+// read touch 8 distinct 16-byte bank groups per 8 lanes
+__device__ __forceinline__ uint32_t knap_slot(uint32_t m, uint32_t h) { return 4u * m + (h ^ ((m >> 1) & 3u)); }
+constexpr uint32_t kKnapCStride = 20;  // ints per C column in the scratch (padded against bank conflicts)
+constexpr uint32_t kKnapScratch = 16 * kKnapCStride / 4;  // uint4 per wave (>= 64 chunk slots)
+
+// every lane of the wave calls this with its chunk `v` (zero if it holds
+// none); returns the score of the lane's child.  scr: the wave's scratch
+// (kKnapScratch uint4); tab: the digit table in LDS, [s][h][16 columns] x
+// 16 B, columns >= knap_cols zero.
+template <int GS>
+__device__ __forceinline__ float knap_mfma(const GenArgs& a, uint4 v, uint32_t lane, uint32_t q, uint4* scr,
+                                           const uint4* tab) {
+  constexpr uint32_t R = GS / 4;
+  const uint32_t D = a.knap_dig, NC = a.knap_cols;
+  scr[knap_slot(lane >> 2, lane & 3u)] = v;
+  wave_lds_sync();
+  const uint32_t h = lane >> 4, n = lane & 15u;
+  const uint4 x = scr[knap_slot(n, h)];  // A: virtual row n, lane group h's 128 bits
+  const uint32_t xs[4] = {x.x, x.y, x.z, x.w};
+  const uint4* tb = tab + h * kKnapMaxCols + n;
+  v4i acc = {0, 0, 0, 0};
+#pragma unroll
+  for (uint32_t s = 0; s < kKnapSlices; ++s) {
+    const uint4 t = tb[s * 4u * kKnapMaxCols];
+    const uint32_t bits = (s & 1u) ? (xs[s >> 1] >> 16) : (xs[s >> 1] & 0xFFFFu);
+    acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(expand16(bits), v4i{(int)t.x, (int)t.y, (int)t.z, (int)t.w}, acc,
+                                                0, 0, 0);
+  }
+  wave_lds_sync();
+  int* cl = (int*)scr;  // C, column-major: [column n][row 4h + i], stride kKnapCStride
+  *(v4i*)(cl + n * kKnapCStride + 4u * h) = acc;
+  wave_lds_sync();
+  const uint32_t g = lane / GS;
+  uint32_t V = 0, W = 0;  // mod 2^32: exact, the true sums are below 2^24
+  for (uint32_t e = q; e < NC; e += GS) {
+    const uint32_t r = e / (2u * D), d = e % D;
+    const uint32_t c = (uint32_t)cl[e * kKnapCStride + g * R + r] << (8u * d);
+    if ((e / D) & 1u) W += c;
+    else V += c;
+  }
+  const float vv = (float)(int)group_sum_u<GS>(V), ww = (float)(int)group_sum_u<GS>(W);
+  return ww <= a.obj_f0 ? vv : a.obj_f0 - ww;
 }
 
 // Parents of `child` from the ST_SEL words; group-uniform (every lane of the
@@ -366,7 +456,7 @@ __device__ __forceinline__ uint32_t pos16(uint4 r1, uint32_t k) {  // k-th packe
 }
 
 template <int GS, int OBJ, bool FULL, bool DENSE>
-__global__ __launch_bounds__(kBlock, PGA_TP_WAVES) void binary_gen_tp(GenArgs a, unsigned long long* best_parts) {
+__global__ __launch_bounds__(kBlock, OBJ == kObjKnapMfma ? 4 : PGA_TP_WAVES) void binary_gen_tp(GenArgs a, unsigned long long* best_parts) {
   resolve_gen(a);
   constexpr uint32_t NW = kBlock / 64;
   constexpr uint32_t NG = 64 / GS;  // children per wave per step
@@ -378,6 +468,9 @@ __global__ __launch_bounds__(kBlock, PGA_TP_WAVES) void binary_gen_tp(GenArgs a,
   __shared__ uint32_t lds_thr[kMutCap];
   __shared__ uint32_t lds_el[kTpMaxElite];  // elite sources
   __shared__ unsigned long long lds_red[NW];
+  constexpr bool KMF = OBJ == kObjKnapMfma;
+  __shared__ uint4 lds_kscr[KMF ? NW : 1][kKnapScratch];             // knapsack: per-wave chunk / C scratch
+  __shared__ uint4 lds_ktab[KMF ? kKnapSlices * 4 * kKnapMaxCols : 1];  // knapsack: digit table
 
   const uint32_t lane = lane_id(), wid = threadIdx.x >> 6;
   const uint32_t q = lane & (GS - 1), gbase = lane & ~(uint32_t)(GS - 1), g = lane / GS;
@@ -423,6 +516,9 @@ __global__ __launch_bounds__(kBlock, PGA_TP_WAVES) void binary_gen_tp(GenArgs a,
   }
   if (bitflip)
     for (uint32_t i = threadIdx.x; i < kMutCap; i += kBlock) lds_thr[i] = a.mut_thr[i];
+  if (KMF)
+    for (uint32_t i = threadIdx.x; i < kKnapSlices * 4 * kKnapMaxCols; i += kBlock)
+      lds_ktab[i] = ((const uint4*)a.knap_tab)[i];
   __syncthreads();
 
   unsigned long long my_best = 0;
@@ -576,9 +672,14 @@ __global__ __launch_bounds__(kBlock, PGA_TP_WAVES) void binary_gen_tp(GenArgs a,
       }                                                                                                     \
     }                                                                                                       \
     v = xor4(v, fm);                                                                                        \
-    BinObj<OBJ> acc;                                                                                        \
-    if (have) acc.add(a, v, q);                                                                             \
-    const float sc = acc.template finish<GS>(a);                                                            \
+    float sc;                                                                                               \
+    if constexpr (KMF) {                                                                                    \
+      sc = knap_mfma<GS>(a, have ? v : make_uint4(0, 0, 0, 0), lane, q, lds_kscr[wid], lds_ktab);            \
+    } else {                                                                                                \
+      BinObj<OBJ> acc;                                                                                      \
+      if (have) acc.add(a, v, q);                                                                           \
+      sc = acc.template finish<GS>(a);                                                                      \
+    }                                                                                                       \
     if (have) ROW(nxt, c, q) = v;                                                                           \
     if (EVALS) { /* every lane of the group stores the same score */                                        \
       ELEM(float, a.score_next, c) = sc;                                                                    \
@@ -625,6 +726,19 @@ uint32_t launch_mode(int mode, const GenArgs& a, unsigned long long* parts, hipS
       if (fast && o32 && a.n_elite <= kTpMaxElite && (!INT_OBJ || a.key_cur != nullptr)) {
         const bool dense = a.mutation == MUT_BIT_FLIP && a.mut_rate > 0.f && !a.mut_sparse;
         const bool full = a.chunks == (uint32_t)GS;
+        if constexpr (OBJ == OBJ_KNAPSACK && GS >= 4 && GS <= 32) {
+          if (a.knap_tab != nullptr) {  // integer-exact instance: the matrix-core evaluation
+            if (a.knap_cols == 0 || a.knap_cols > kKnapMaxCols || a.knap_dig == 0 || a.knap_dig > 4 ||
+                a.knap_cols != (uint32_t)GS / 2u * a.knap_dig)
+              throw std::invalid_argument("knapsack digit table does not match the genome geometry");
+            if (full) {
+              if (dense) return go(binary_gen_tp<GS, kObjKnapMfma, true, true>, a, parts, kBlock, s);
+              return go(binary_gen_tp<GS, kObjKnapMfma, true, false>, a, parts, kBlock, s);
+            }
+            if (dense) return go(binary_gen_tp<GS, kObjKnapMfma, false, true>, a, parts, kBlock, s);
+            return go(binary_gen_tp<GS, kObjKnapMfma, false, false>, a, parts, kBlock, s);
+          }
+        }
         // one block = 4 waves x 64 children per batch
         if (full) {
           if (dense) return go(binary_gen_tp<GS, OBJ, true, true>, a, parts, kBlock, s);
@@ -654,6 +768,48 @@ uint32_t launch_obj(int mode, const GenArgs& a, unsigned long long* parts, hipSt
 }
 
 }  // namespace
+
+bool build_knap_table(const float* values, const float* weights, uint32_t L, uint32_t chunks,
+                      std::vector<uint8_t>& tab, uint32_t& digits, uint32_t& cols) {
+  tab.clear();
+  digits = cols = 0;
+  const uint32_t GS = group_size(chunks);
+  if (GS < 4 || GS > 32 || chunks > GS) return false;
+  double sv = 0, sw = 0;
+  int64_t vmax = 0;
+  for (uint32_t i = 0; i < L; ++i) {
+    for (const float x : {values[i], weights[i]}) {
+      if (!(x == std::nearbyint(x)) || std::fabs(x) >= 16777216.f) return false;
+      vmax = std::max<int64_t>(vmax, (int64_t)std::fabs(x));
+    }
+    sv += std::fabs(values[i]);
+    sw += std::fabs(weights[i]);
+  }
+  if (sv >= 16777216.0 || sw >= 16777216.0) return false;
+  uint32_t D = 1;  // balanced base-256 digits in [-128, 127]
+  for (int64_t lim = 127; vmax > lim && D < 4; ++D) lim = lim * 256 + 127;
+  const uint32_t R = GS / 4, NC = 2 * R * D;
+  if (NC > kKnapMaxCols) return false;
+  tab.assign((size_t)kKnapSlices * 4 * kKnapMaxCols * 16, 0);  // [s][h][16 columns], columns >= NC zero
+  for (uint32_t s = 0; s < kKnapSlices; ++s)
+    for (uint32_t h = 0; h < 4; ++h)
+      for (uint32_t c = 0; c < NC; ++c) {
+        const uint32_t r = c / (2 * D), qty = (c / D) & 1u, d = c % D;
+        for (uint32_t j = 0; j < 16; ++j) {
+          const uint32_t gi = 128u * (4u * r + h) + 16u * s + j;
+          int64_t x = gi < L ? (int64_t)(qty ? weights[gi] : values[gi]) : 0;
+          int dig = 0;
+          for (uint32_t k = 0; k <= d; ++k) {
+            dig = (int)(((x + 128) & 255) - 128);
+            x = (x - dig) / 256;
+          }
+          tab[(((size_t)s * 4 + h) * kKnapMaxCols + c) * 16 + j] = (uint8_t)(int8_t)dig;
+        }
+      }
+  digits = D;
+  cols = NC;
+  return true;
+}
 
 uint32_t binary_launch(int mode, const GenArgs& a, unsigned long long* best_parts, hipStream_t s) {
   uint32_t grid = 0;

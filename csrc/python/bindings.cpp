@@ -140,6 +140,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def_property_readonly("has_jit", &Island::has_jit)
       .def_property("graph_generations", &Island::graph_generations, &Island::set_graph_generations)
       .def_property_readonly("graph_replays", &Island::graph_replays)
+      .def_property_readonly("knapsack_digits", &Island::knapsack_digits)
       .def("config", [](Island& i) { return i.config(); })
       .def("set_operators", [](Island& i, const pga::Config& c) { bind_stream(i); i.set_operators(c); })
       .def("set_objective_data",

@@ -62,6 +62,33 @@ def test_objectives_bitexact(prob):
     assert torch.allclose(ref, g.scores.cpu(), rtol=0, atol=1e-2)
 
 
+@pytest.mark.parametrize("L,scale,digits", [(1024, 1, 1), (700, 1, 1), (300, 1, 1), (2000, 1, 1), (3000, 1, 1),
+                                             (1024, 250, 2), (1024, "big", 3), (1024, -1, 1), (1024, 0.5, 0),
+                                             (200, 1, 0)])
+def test_knapsack_matrix_cores_bitexact(L, scale, digits):
+    """Knapsack evaluated on the int8 matrix cores in the hot kernel (tournament
+    2): bit-exact against the CPU's float sums for integer instances (1-3
+    balanced base-256 digits, negative values), and the scalar evaluation for
+    non-integer instances or genomes of fewer than 4 lanes (digits 0)."""
+    base = pga.models.Knapsack01.random(L, seed=3)
+    v, w = base.values.clone(), base.weights.clone()
+    if scale == -1:
+        v = v - 50  # negative values
+    elif scale == "big":
+        v[:3] = torch.tensor([5e6, 3e6, 1e6])  # 3 digits, sums still below 2^24
+    else:
+        v = v * scale
+    p = pga.models.Knapsack01(v, w, base.capacity)
+    g, c = pair(p, 2500, elitism=1)
+    for _ in range(3):
+        g.run(1)
+        c.run(1)
+        same(g, c)
+    assert g.island.knapsack_digits == digits
+    ref = p.reference_fitness(g.genomes().cpu())
+    assert torch.allclose(ref, g.scores.cpu(), rtol=1e-6, atol=1e-2)
+
+
 @pytest.mark.parametrize("mut", [("bit_flip", 0.0), ("bit_flip", 0.05), ("bit_flip", 1.0), ("reset_one", 0.3)])
 def test_mutation_modes_bitexact(mut):
     name, rate = mut
