@@ -691,8 +691,21 @@ void pga_run(pga_t* p, unsigned n) {
   guard(p, [&]() {
     population_t* pop = p->pops[0];
     sync_callbacks(p, pop);
+    pop->isl->stream = p->stream;
     pop->isl->evaluate();  // reference: evaluate precedes every crossover (src/pga.cu:383)
     pop->isl->run(n);      // each fused generation leaves its children evaluated
+  });
+}
+
+int pga_run_until(pga_t* p, unsigned n, float target, unsigned check_every) {
+  if (!p || p->pops.empty()) return -1;
+  return guard_r<int>(p, -1, [&]() {
+    population_t* pop = p->pops[0];
+    sync_callbacks(p, pop);
+    pop->isl->stream = p->stream;
+    pop->isl->evaluate();
+    if (pop->isl->best_score() >= target) return 0;
+    return (int)pop->isl->run_until(n, target, check_every);
   });
 }
 
@@ -731,7 +744,38 @@ namespace {
 // (pga_migrate), then between ranks (migrate_ranks).  Each solver's islands
 // run on their own streams; solvers on different GPUs run concurrently
 // because nothing here waits on the host between migration points.
-void run_islands(const std::vector<pga_t*>& solvers, unsigned n, unsigned m, float pct) {
+// best score over every population of `solvers` and, with a communicator that
+// is still healthy, over every rank (the same value on all of them)
+float global_best(const std::vector<pga_t*>& solvers) {
+  std::vector<pga::LocalRank> local;
+  std::vector<float> mine;
+  float all_best = -INFINITY;
+  for (pga_t* q : solvers) {
+    use_device(q);
+    float b = -INFINITY;
+    for (population_t* pop : q->pops) {
+      pop->isl->stream = q->stream;
+      b = std::max(b, pop->isl->best_score());
+    }
+    mine.push_back(b);
+    all_best = std::max(all_best, b);
+    pga::LocalRank l;
+    l.rank = q->comm_rank;
+    l.device = q->device;
+    l.stream = q->stream;
+    local.push_back(l);
+  }
+  pga_t* p0 = solvers.front();
+  if (!p0->comm || p0->degraded || (p0->comm->size() == 1 && !p0->comm->self_exchange)) return all_best;
+  for (float v : p0->comm->allgather(local, mine)) all_best = std::max(all_best, v);
+  return all_best;
+}
+
+// n generations of every population of every solver in `solvers`, migrating
+// every m generations (see below); with a target (not NaN) the run stops at
+// the first check point (every m generations, 10 when m == 0) whose global
+// best reaches it.  Returns the generations run.
+unsigned run_islands_until(const std::vector<pga_t*>& solvers, unsigned n, unsigned m, float pct, float target) {
   for (pga_t* p : solvers) {
     use_device(p);
     for (population_t* pop : p->pops) {
@@ -740,12 +784,16 @@ void run_islands(const std::vector<pga_t*>& solvers, unsigned n, unsigned m, flo
       pop->isl->evaluate();
     }
   }
+  const bool until = !std::isnan(target);
+  const unsigned every = m > 0 ? m : 10u;  // check points of a target run
+  if (until && global_best(solvers) >= target) return 0;
   unsigned g = 0;
   while (g < n) {
-    // generations until the next migration point (or the end)
+    // generations until the next migration / check point (or the end)
     unsigned step = n - g;
-    if (m > 0) {
-      const unsigned next = (g / m + 1) * m;
+    const unsigned period = m > 0 ? m : (until ? every : 0u);
+    if (period > 0) {
+      const unsigned next = (g / period + 1) * period;
       if (next < n) step = next - g;
     }
     for (pga_t* p : solvers) {
@@ -756,6 +804,7 @@ void run_islands(const std::vector<pga_t*>& solvers, unsigned n, unsigned m, flo
       if (gpu) join_islands(p);
     }
     g += step;
+    if (until && global_best(solvers) >= target) break;
     if (m > 0 && g % m == 0 && g < n) {
       for (pga_t* p : solvers) {
         use_device(p);
@@ -764,6 +813,7 @@ void run_islands(const std::vector<pga_t*>& solvers, unsigned n, unsigned m, flo
       migrate_ranks(solvers, pct);
     }
   }
+  return g;
 }
 }  // namespace
 
@@ -772,7 +822,17 @@ void pga_run_islands(pga_t* p, unsigned n, unsigned m, float pct) {
   guard(p, [&]() {
     if (p->comm && p->comm->drives_all_ranks() && p->comm->size() > 1)
       throw std::invalid_argument("this communicator drives all ranks from one process: use pga_run_islands_multi");
-    run_islands({p}, n, m, pct);
+    (void)run_islands_until({p}, n, m, pct, NAN);
+  });
+}
+
+int pga_run_islands_until(pga_t* p, unsigned n, unsigned m, float pct, float target) {
+  if (!p || p->pops.empty()) return -1;
+  return guard_r<int>(p, -1, [&]() {
+    if (p->comm && p->comm->drives_all_ranks() && p->comm->size() > 1)
+      throw std::invalid_argument("this communicator drives all ranks from one process: use pga_run_islands_multi");
+    if (std::isnan(target)) throw std::invalid_argument("pga_run_islands_until: target is NaN");
+    return (int)run_islands_until({p}, n, m, pct, target);
   });
 }
 
@@ -788,7 +848,7 @@ int pga_run_islands_multi(pga_t** solvers, int count, unsigned n, unsigned m, fl
     if (p0->comm && p0->comm->size() > 1 && (!p0->comm->drives_all_ranks() || count != p0->comm->size()))
       throw std::invalid_argument("pga_run_islands_multi: pass every rank of an InitAll / loopback group");
     std::sort(v.begin(), v.end(), [](pga_t* a, pga_t* b) { return a->comm_rank < b->comm_rank; });
-    run_islands(v, n, m, pct);
+    (void)run_islands_until(v, n, m, pct, NAN);
     return 0;
   });
 }
@@ -831,6 +891,25 @@ int pga_get_genome(pga_t* p, population_t* pop, unsigned long i, void* out) {
     std::vector<uint32_t> r = pop->isl->row_host(i);
     std::memcpy(out, r.data(), 4 * r.size());
     return 0;
+  });
+}
+
+int pga_set_stats_history(pga_t* p, population_t* pop, int on) {
+  if (!valid_pop(p, pop)) return -1;
+  return guard_r<int>(p, -1, [&]() {
+    pop->isl->set_stats_history(on != 0);
+    return 0;
+  });
+}
+
+long pga_get_stats_history(pga_t* p, population_t* pop, float* out, unsigned long max_rows) {
+  if (!valid_pop(p, pop)) return -1;
+  return guard_r<long>(p, -1, [&]() {
+    pop->isl->stream = p->stream;
+    const std::vector<float> h = pop->isl->history();
+    const unsigned long rows = h.size() / 4;
+    if (out) std::memcpy(out, h.data(), 16ull * std::min(rows, max_rows));
+    return (long)rows;
   });
 }
 

@@ -48,6 +48,7 @@ Island::Island(const Config& cfg, int device) : cfg_(cfg), device_(device) {
     rows_[i] = alloc(rb);
     scores_[i] = alloc(4ull * Sp);
     best_[i] = alloc(8ull * kMaxGrid);
+    if (on_gpu()) stats_parts_[i] = alloc(8ull * kMaxGrid);
     keys_[i] = alloc(2ull * Sp);
   }
   out_best_ = alloc(64);
@@ -68,7 +69,7 @@ Island::~Island() {
   Buffer* all[] = {&rows_[0],   &rows_[1],     &scores_[0],   &scores_[1],  &best_[0],  &best_[1],   &mut_thr_,
                    &obj_data_[0], &obj_data_[1], &keys_[0], &keys_[1], &elite_idx_, &cumfit_, &cum_ws_, &topk_ws_, &stats_,
                    &out_best_,  &scratch_, &compat_rand_, &ev_parts_, &gen_dev_, &rank_order_, &rank_ws_, &qubo_qt_,
-                   &knap_tab_};
+                   &knap_tab_, &stats_parts_[0], &stats_parts_[1], &hist_};
   drop_graph();
   if (cap_stream_) (void)hipStreamDestroy(cap_stream_);
   for (Buffer* b : all) {
@@ -291,6 +292,7 @@ GenArgs Island::make_args(int mode) {
     a.gen_dev = (const uint32_t*)gen_dev_.ptr;
     a.gen_off = gen_ - capture_base_;
   }
+  if (fused_stats()) a.stats_parts = (float*)stats_parts_[(mode == MODE_INIT || mode == MODE_EVAL) ? cur_ : nx].ptr;
   if (integer_objective(cfg_.objective, cfg_.L)) {
     a.key_cur = (const uint16_t*)keys_[cur_].ptr;
     a.key_next = (uint16_t*)keys_[nx].ptr;
@@ -308,21 +310,29 @@ void Island::initialize() {
   TraceRange tr("pga.initialize");
   GenArgs a = make_args(MODE_INIT);
   n_best_[cur_] = launch(MODE_INIT, a, (unsigned long long*)best_[cur_].ptr);
-  if (jit_) n_best_[cur_] = jit_eval(rows_[cur_].ptr, (float*)scores_[cur_].ptr, cfg_.S, (unsigned long long*)best_[cur_].ptr);
-  else if (cfg_.objective == OBJ_NONE) rebest();
+  stats_ok_[cur_] = a.stats_parts != nullptr;
+  if (jit_) {
+    n_best_[cur_] = jit_eval(rows_[cur_].ptr, (float*)scores_[cur_].ptr, cfg_.S, (unsigned long long*)best_[cur_].ptr);
+    stats_ok_[cur_] = false;
+  } else if (cfg_.objective == OBJ_NONE) {
+    rebest();
+  }
 }
 
 void Island::evaluate() {
   TraceRange tr("pga.evaluate");
   if (jit_) {
     n_best_[cur_] = jit_eval(rows_[cur_].ptr, (float*)scores_[cur_].ptr, cfg_.S, (unsigned long long*)best_[cur_].ptr);
+    stats_ok_[cur_] = false;
     return;
   }
   GenArgs a = make_args(MODE_EVAL);
   n_best_[cur_] = launch(MODE_EVAL, a, (unsigned long long*)best_[cur_].ptr);
+  stats_ok_[cur_] = a.stats_parts != nullptr;
 }
 
 void Island::rebest() {
+  stats_ok_[cur_] = false;
   const float* sc = (const float*)scores_[cur_].ptr;
   if (on_gpu()) {
     uint16_t* keys = integer_objective(cfg_.objective, cfg_.L) ? (uint16_t*)keys_[cur_].ptr : nullptr;
@@ -351,7 +361,7 @@ void Island::prepare_generation() {
 
 void Island::run(uint32_t n) {
   TraceRange tr("pga.run");
-  if (on_gpu() && graph_g_ > 0 && !graph_broken_ && n >= graph_g_ + 2) {
+  if (on_gpu() && graph_g_ > 0 && !graph_broken_ && !hist_on_ && n >= graph_g_ + 2) {
     const bool fresh = gexec_ && g_cur_ == cur_ && g_epoch_ == epoch_ && g_version_ == version_ &&
                        g_nbest_ == n_best_[cur_] && g_len_ == graph_g_;
     if (!fresh) {
@@ -372,11 +382,74 @@ void Island::run_plain(uint32_t n) {
     prepare_generation();
     GenArgs a = make_args(MODE_GEN);
     n_best_[cur_ ^ 1] = launch(MODE_GEN, a, (unsigned long long*)best_[cur_ ^ 1].ptr);
-    if (jit_)
+    stats_ok_[cur_ ^ 1] = a.stats_parts != nullptr;
+    if (jit_) {
       n_best_[cur_ ^ 1] = jit_eval(rows_[cur_ ^ 1].ptr, (float*)scores_[cur_ ^ 1].ptr, cfg_.S,
                                    (unsigned long long*)best_[cur_ ^ 1].ptr);
+      stats_ok_[cur_ ^ 1] = false;
+    }
     swap();
+    if (hist_on_ && !capturing_) append_history();
   }
+}
+
+uint32_t Island::run_until(uint32_t n, float target, uint32_t check_every) {
+  TraceRange tr("pga.run_until");
+  if (check_every == 0) check_every = 10;
+  uint32_t done = 0;
+  while (done < n) {
+    const uint32_t k = std::min(check_every, n - done);
+    run(k);
+    done += k;
+    if (best_score() >= target) break;  // one sync per check
+  }
+  return done;
+}
+
+bool Island::fused_stats() const {
+  // JIT objectives and the QUBO evaluation pass store best partials only
+  return on_gpu() && !jit_ && cfg_.objective != OBJ_QUBO && cfg_.objective != OBJ_NONE;
+}
+
+void Island::set_stats_history(bool on) {
+  hist_on_ = on;
+  if (!on) return;  // off keeps the rows so far
+  hist_n_ = 0;
+  hist_host_.clear();
+}
+
+void Island::append_history() {
+  if (!on_gpu()) {
+    float r[4];
+    cpu::score_stats((const float*)scores_[cur_].ptr, cfg_.S, r);
+    hist_host_.insert(hist_host_.end(), r, r + 4);
+    ++hist_n_;
+    return;
+  }
+  if (hist_.bytes < 16ull * (hist_n_ + 1)) {  // grow (rare): keep the rows so far
+    const uint64_t cap = std::max<uint64_t>(1024, 2 * (hist_n_ + 1));
+    Buffer nb = alloc(16ull * cap);
+    if (hist_n_) PGA_HIP_CHECK(hipMemcpyAsync(nb.ptr, hist_.ptr, 16ull * hist_n_, hipMemcpyDeviceToDevice, stream));
+    synchronize();
+    release(hist_);
+    hist_ = nb;
+  }
+  float* row = (float*)hist_.ptr + 4 * hist_n_;
+  if (stats_ok_[cur_]) {
+    stats_from_parts_launch((const float*)stats_parts_[cur_].ptr, (const unsigned long long*)best_[cur_].ptr,
+                            n_best_[cur_], cfg_.S, row, stream);
+  } else {
+    score_stats_launch((const float*)scores_[cur_].ptr, cfg_.S, (float*)stats_.ptr, stream);
+    PGA_HIP_CHECK(hipMemcpyAsync(row, stats_.ptr, 16, hipMemcpyDeviceToDevice, stream));
+  }
+  ++hist_n_;
+}
+
+std::vector<float> Island::history() {
+  if (!on_gpu()) return hist_host_;
+  std::vector<float> out(4 * hist_n_);
+  if (hist_n_) copy_to_host(out.data(), hist_.ptr, 16ull * hist_n_);
+  return out;
 }
 
 void Island::crossover_stage() {
@@ -411,7 +484,11 @@ unsigned long long Island::best_packed() {
 
 void Island::stats(float out[4]) {
   const float* sc = (const float*)scores_[cur_].ptr;
-  if (on_gpu()) {
+  if (on_gpu() && stats_ok_[cur_]) {  // fused partials of the kernel that scored this generation
+    stats_from_parts_launch((const float*)stats_parts_[cur_].ptr, (const unsigned long long*)best_[cur_].ptr,
+                            n_best_[cur_], cfg_.S, (float*)stats_.ptr, stream);
+    copy_to_host(out, stats_.ptr, 16);
+  } else if (on_gpu()) {
     score_stats_launch(sc, cfg_.S, (float*)stats_.ptr, stream);
     copy_to_host(out, stats_.ptr, 16);
   } else {
@@ -522,6 +599,7 @@ void Island::immigrate(uint32_t k, const void* in_rows, const float* in_scores) 
     // the victims' keys were written with their rows: only the best partials follow
     n_best_[cur_] = best_of_scores_launch((const float*)scores_[cur_].ptr, cfg_.S,
                                           (unsigned long long*)best_[cur_].ptr, stream, nullptr);
+    stats_ok_[cur_] = false;
     return;
   }
   uint32_t* idx = (uint32_t*)scratch(4ull * k);
@@ -546,6 +624,7 @@ bool Island::evaluate_rows(void* rows, float* scores, uint32_t n) {
   a.S = n;
   a.key_cur = nullptr;
   a.key_next = nullptr;
+  a.stats_parts = nullptr;  // the island's own statistics are not these rows'
   a.n_elite = 0;
   a.elite_idx = nullptr;
   launch(MODE_EVAL, a, (unsigned long long*)ev_parts_.ptr);

@@ -317,6 +317,10 @@ struct GenArgs {
   const void* knap_tab;
   uint32_t knap_dig, knap_cols;
 
+  // fused statistics: when set, evaluating kernels store a {min, sum} pair per
+  // block (same blocks as best_parts); see device.hpp ScoreStats
+  float* stats_parts;
+
   // padding mask for the last chunk (BINARY)
   u32x4 last_mask;
 

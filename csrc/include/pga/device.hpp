@@ -65,6 +65,54 @@ __device__ __forceinline__ unsigned long long block_reduce_parts(const unsigned 
   return block_max_u64<BLK>(v, lds4);
 }
 
+// Fused per-generation statistics: every evaluating kernel keeps a running
+// {min, sum} of the scores its lanes produce and, when GenArgs::stats_parts is
+// set, stores one {min, sum} pair per block next to its packed best (the max),
+// so min / max / mean of a generation need no pass over the scores.
+struct ScoreStats {
+  float mn = __builtin_inff(), sm = 0.f;
+  __device__ __forceinline__ void add(float v) {
+    mn = fminf(mn, v);
+    sm += v;
+  }
+  __device__ __forceinline__ void add_if(bool ok, float v) {
+    mn = ok ? fminf(mn, v) : mn;
+    sm += ok ? v : 0.f;
+  }
+};
+
+// block reduction of the lanes' ScoreStats -> parts[2*blockIdx.x .. +1]; every
+// thread of the block calls it (block-uniform control flow)
+template <int BLK = kBlock>
+__device__ __forceinline__ void block_stats_store(ScoreStats st, float* parts) {
+  __shared__ float lds_st[2][BLK / 64];
+  float mn = st.mn, sm = st.sm;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    mn = fminf(mn, __shfl_xor(mn, o, 64));
+    sm += __shfl_xor(sm, o, 64);
+  }
+  if (BLK > 64) {
+    __syncthreads();
+    if (lane_id() == 0) {
+      lds_st[0][threadIdx.x >> 6] = mn;
+      lds_st[1][threadIdx.x >> 6] = sm;
+    }
+    __syncthreads();
+    mn = lds_st[0][0];
+    sm = lds_st[1][0];
+#pragma unroll
+    for (int i = 1; i < BLK / 64; ++i) {
+      mn = fminf(mn, lds_st[0][i]);
+      sm += lds_st[1][i];
+    }
+  }
+  if (threadIdx.x == 0) {
+    parts[2 * blockIdx.x] = mn;
+    parts[2 * blockIdx.x + 1] = sm;
+  }
+}
+
 // Child word pool: lane q of a GS-lane group holds Philox block q of the
 // child's ST_CHILD stream.  Child word t < 3*GS lives in register t%3 of lane
 // t/3 and is fetched with one ds_bpermute (t must be group-uniform); later

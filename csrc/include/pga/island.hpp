@@ -91,6 +91,10 @@ class Island {
   void initialize();          // random population + evaluation (generation 0)
   void evaluate();            // scores(cur) <- objective(rows(cur))
   void run(uint32_t n);       // n fused generations
+  // up to n generations, stopping once the best score reaches `target`; the
+  // best is read (one stream sync) every `check_every` generations (0: 10).
+  // Returns the generations run.
+  uint32_t run_until(uint32_t n, float target, uint32_t check_every);
   void crossover_stage();     // next <- crossover(select(cur))  (no mutation / evaluation)
   void mutate_stage();        // mutate next in place
   void swap();                // cur <-> next, generation++
@@ -101,6 +105,13 @@ class Island {
   float best_score() { return pga::best_score(best_packed()); }
   uint64_t best_index() { return pga::best_index(best_packed()); }
   void stats(float out4[4]);  // min, max, sum, count of current scores
+  // Per-generation statistics history: when on, every generation appends its
+  // {min, max, sum, count} row on the device (from the generation kernel's
+  // fused partials, no pass over the scores); history() copies the rows out.
+  // Turning it on clears the history and disables hipGraph replay.
+  void set_stats_history(bool on);
+  bool stats_history() const { return hist_on_; }
+  std::vector<float> history();
   std::vector<uint32_t> topk_host(uint32_t k, bool largest);
   std::vector<uint32_t> row_host(uint64_t i);
 
@@ -126,7 +137,10 @@ class Island {
   float* scores(int which) { return (float*)scores_[which ^ cur_].ptr; }
   unsigned long long* best_parts() { return (unsigned long long*)best_[cur_].ptr; }
   uint32_t n_best() const { return n_best_[cur_]; }
-  void set_n_best(uint32_t n) { n_best_[cur_] = n; }
+  void set_n_best(uint32_t n) {
+    n_best_[cur_] = n;
+    stats_ok_[cur_] = false;
+  }
   size_t row_bytes() const { return 4ull * row_words_; }
 
   // scratch buffers for callers (migration staging)
@@ -179,6 +193,16 @@ class Island {
   std::vector<float> obj_host0_;  // host copy of objective data slot 0 (derived tables)
   Buffer knap_tab_;               // BINARY knapsack: matrix-core digit table (GPU, integer instances)
   uint32_t knap_version_ = ~0u, knap_dig_ = 0, knap_cols_ = 0;
+  // fused statistics partials per parity ({min, sum} per block of the kernel
+  // that wrote best_[p]); stats_ok_[p]: they belong to the current best_[p]
+  Buffer stats_parts_[2];
+  bool stats_ok_[2] = {false, false};
+  bool fused_stats() const;  // the evaluating kernels of this configuration store them
+  void append_history();
+  Buffer hist_;
+  std::vector<float> hist_host_;  // CPU backend
+  uint64_t hist_n_ = 0;
+  bool hist_on_ = false;
   float mut_inv_ = 0.f;
   bool mut_sparse_ = false;  // BINARY bit-flip uses the sparse (Binomial) sampler
   float mut_rate_eff_ = 0.f;

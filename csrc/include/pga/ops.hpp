@@ -40,6 +40,9 @@ uint32_t launch_grid(uint64_t S, uint32_t per_block);
 uint32_t launch_grid_occ(uint64_t S, uint32_t per_block, const void* kernel);
 uint32_t occupancy_blocks(const void* kernel, int block);
 int device_cu_count();
+// raise a kernel's dynamic-LDS limit to what its static LDS leaves of the
+// CU's 160 KiB; returns that many bytes
+size_t allow_dynamic_lds(const void* kernel);
 // PGA_FORCE_GENERIC=1: every encoding runs its generic (non-pipelined) GEN
 // kernel.  Verification / debugging only: the fast kernels are bit-identical.
 bool force_generic_kernels();
@@ -100,6 +103,9 @@ void scores_to_keys_launch(const float* scores, uint64_t S, uint16_t* keys, hipS
 void advance_counter_launch(uint32_t* counter, uint32_t delta, hipStream_t s);
 // stats[0..3] = {min, max, sum, count} of scores (count as float)
 void score_stats_launch(const float* scores, uint64_t S, float* stats, hipStream_t s);
+// the same 4 floats from a generation kernel's fused partials (n blocks)
+void stats_from_parts_launch(const float* parts, const unsigned long long* best, uint32_t n, uint64_t S, float* out,
+                             hipStream_t s);
 // roulette: cumfit = inclusive prefix sum of max(score - min, 0); workspace >= 2*kMaxGrid floats
 void roulette_prefix_launch(const float* scores, uint64_t S, float* cumfit, float* workspace, hipStream_t s);
 // rank selection: order = indices by ascending (score_key, index); workspace: rank_order_workspace_bytes(S)

@@ -342,6 +342,7 @@ __global__ __launch_bounds__(kBlock) void binary_kernel(GenArgs a, unsigned long
   __syncthreads();
 
   unsigned long long my_best = 0;
+  ScoreStats st;
   const uint64_t stride = (uint64_t)gridDim.x * GPB;
   for (uint64_t child = (uint64_t)blockIdx.x * GPB + g_in_block; child < a.S; child += stride) {
     float score = 0.f;
@@ -410,11 +411,13 @@ __global__ __launch_bounds__(kBlock) void binary_kernel(GenArgs a, unsigned long
       if (a.key_next) a.key_next[child] = (uint16_t)score;
       const unsigned long long pb = pack_best(score, child);
       my_best = pb > my_best ? pb : my_best;
+      st.add(score);
     }
   }
   if (EVALS && best_parts) {
     unsigned long long b = block_max_u64(my_best, lds_red);
     if (threadIdx.x == 0) best_parts[blockIdx.x] = b;
+    if (a.stats_parts) block_stats_store(st, a.stats_parts);
   }
 }
 
@@ -522,6 +525,7 @@ __global__ __launch_bounds__(kBlock, OBJ == kObjKnapMfma ? 4 : PGA_TP_WAVES) voi
   __syncthreads();
 
   unsigned long long my_best = 0;
+  ScoreStats st;
   if (nsteps > 0) {  // wave-uniform
     uint4(*rec)[64][2] = lds_rec[wid];
     // keys of the tournament in flight (lane = child `lane` of the batch)
@@ -686,6 +690,7 @@ __global__ __launch_bounds__(kBlock, OBJ == kObjKnapMfma ? 4 : PGA_TP_WAVES) voi
       if (KEY) ELEM(uint16_t, a.key_next, c) = (uint16_t)sc;                                                \
       const unsigned long long pk = c < S ? pack_best(sc, c) : 0ull;                                        \
       my_best = pk > my_best ? pk : my_best;                                                                \
+      st.add_if(q == 0u && c < S, sc);                                                                      \
     }                                                                                                       \
   }
 
@@ -703,6 +708,7 @@ __global__ __launch_bounds__(kBlock, OBJ == kObjKnapMfma ? 4 : PGA_TP_WAVES) voi
 #undef ELEM
   unsigned long long bb = block_max_u64(my_best, lds_red);
   if (threadIdx.x == 0 && best_parts && EVALS) best_parts[blockIdx.x] = bb;
+  if (EVALS && best_parts && a.stats_parts) block_stats_store(st, a.stats_parts);
 }
 
 template <typename K>

@@ -74,6 +74,7 @@ __global__ __launch_bounds__(kBlock) void compat_kernel(GenArgs a, unsigned long
     __syncthreads();
   }
   unsigned long long my_best = 0;
+  ScoreStats st;
   // grid-stride over children (the reference RUN_KERNEL loop serves any S,
   // src/pga.cu:62-70); the grid is sized to the device, not to S
   for (uint64_t child = (uint64_t)blockIdx.x * kBlock + threadIdx.x; child < a.S;
@@ -125,11 +126,13 @@ __global__ __launch_bounds__(kBlock) void compat_kernel(GenArgs a, unsigned long
       a.score_next[child] = score;
       const unsigned long long pb = pack_best(score, child);
       if (pb > my_best) my_best = pb;
+      st.add(score);
     }
   }
   if (evals && best_parts) {
     unsigned long long b = block_max_u64(my_best, lds_red);
     if (threadIdx.x == 0) best_parts[blockIdx.x] = b;
+    if (a.stats_parts) block_stats_store(st, a.stats_parts);
   }
 }
 

@@ -33,7 +33,7 @@ constexpr uint16_t kNone = 0xFFFF;
 constexpr uint32_t kHdrF = 144;  // floats: red u64[4] (8 floats) | elite | pad  (16-aligned)
 
 inline uint32_t perm_max_length(bool euc) {  // longest genome the one-individual-per-block kernel holds in LDS
-  return (uint32_t)((160 * 1024 - 4 * kHdrF) / (euc ? 16 : 8)) / 8 * 8;
+  return (uint32_t)((160 * 1024 - 4 * kHdrF - 64 /* static LDS */) / (euc ? 16 : 8)) / 8 * 8;
 }
 
 __host__ __device__ inline size_t perm_lds_bytes(uint32_t GS, uint32_t chunks, bool euc, uint32_t blk = 256) {
@@ -96,6 +96,7 @@ __global__ __launch_bounds__(BLK) void perm_kernel(GenArgs a, unsigned long long
   __syncthreads();
 
   unsigned long long my_best = 0;
+  ScoreStats st;
   for (uint64_t base = (uint64_t)blockIdx.x * GPB; base < a.S; base += (uint64_t)gridDim.x * GPB) {  // block-uniform
     const uint64_t child = base + g;
     const bool valid = child < a.S;  // group-uniform
@@ -264,6 +265,7 @@ __global__ __launch_bounds__(BLK) void perm_kernel(GenArgs a, unsigned long long
         a.score_next[child] = score;
         const unsigned long long pb = pack_best(score, child);
         my_best = pb > my_best ? pb : my_best;
+        st.add(score);
       }
     }
     __syncthreads();  // C is rewritten next iteration
@@ -271,6 +273,7 @@ __global__ __launch_bounds__(BLK) void perm_kernel(GenArgs a, unsigned long long
   if (EVALS && best_parts) {
     unsigned long long b = block_max_u64<BLK>(my_best, lds_red);
     if (threadIdx.x == 0) best_parts[blockIdx.x] = b;
+    if (a.stats_parts) block_stats_store<BLK>(st, a.stats_parts);
   }
 }
 
@@ -341,6 +344,7 @@ __global__ __launch_bounds__(kBlock) void perm_gen_fast(GenArgs a, unsigned long
   __syncthreads();
 
   unsigned long long my_best = 0;
+  ScoreStats st;
   for (uint64_t base = (uint64_t)blockIdx.x * GPB; base < a.S; base += (uint64_t)gridDim.x * GPB) {
     const uint64_t child = base + g;
     const bool valid = child < a.S;  // group-uniform
@@ -480,11 +484,13 @@ __global__ __launch_bounds__(kBlock) void perm_gen_fast(GenArgs a, unsigned long
       a.score_next[child] = score;
       const unsigned long long pb2 = pack_best(score, child);
       my_best = pb2 > my_best ? pb2 : my_best;
+      st.add(score);
     }
   }
   if (best_parts) {
     unsigned long long b = block_max_u64(my_best, lds_red);
     if (threadIdx.x == 0) best_parts[blockIdx.x] = b;
+    if (a.stats_parts) block_stats_store(st, a.stats_parts);
   }
 }
 
@@ -494,15 +500,12 @@ __global__ __launch_bounds__(kBlock) void perm_gen_fast(GenArgs a, unsigned long
 template <int MODE, int OBJ>
 uint32_t go_long(const GenArgs& a, unsigned long long* parts, hipStream_t s) {
   const size_t lds = perm_lds_bytes(64, a.chunks, OBJ == OBJ_TSP_EUC, 64);
-  if (lds > 160 * 1024)
+  auto k = perm_kernel<64, MODE, OBJ, 64>;
+  static size_t avail = 0;
+  if (!avail) avail = allow_dynamic_lds((const void*)k);
+  if (lds > avail)
     throw std::invalid_argument("PERMUTATION genome too long for the LDS-resident crossover (" + std::to_string(a.L) +
                                 " genes; at most " + std::to_string(perm_max_length(OBJ == OBJ_TSP_EUC)) + ")");
-  auto k = perm_kernel<64, MODE, OBJ, 64>;
-  static bool configured = false;
-  if (!configured) {
-    PGA_HIP_CHECK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-    configured = true;
-  }
   int per_cu = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)k, 64, lds) != hipSuccess || per_cu <= 0)
     per_cu = 1;
@@ -520,7 +523,7 @@ uint32_t go(const GenArgs& a, unsigned long long* parts, hipStream_t s) {
   auto k = perm_kernel<GS, MODE, OBJ>;
   static bool configured = false;
   if (!configured) {
-    PGA_HIP_CHECK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    allow_dynamic_lds((const void*)k);
     configured = true;
   }
   const uint32_t gpb = kBlock / GS;
@@ -541,7 +544,7 @@ uint32_t go_fast(const GenArgs& a, unsigned long long* parts, hipStream_t s) {
   auto k = perm_gen_fast<GS, OBJ>;
   static bool configured = false;
   if (!configured) {
-    PGA_HIP_CHECK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    allow_dynamic_lds((const void*)k);
     configured = true;
   }
   const uint32_t gpb = kBlock / GS;

@@ -121,6 +121,7 @@ __global__ __launch_bounds__(kBlock) void real_kernel(GenArgs a, unsigned long l
   __syncthreads();
 
   unsigned long long my_best = 0;
+  ScoreStats st;
   for (uint64_t base = (uint64_t)blockIdx.x * GPB; base < a.S; base += (uint64_t)gridDim.x * GPB) {  // block-uniform
     const uint64_t child = base + g;
     const bool valid = child < a.S;  // group-uniform
@@ -265,6 +266,7 @@ __global__ __launch_bounds__(kBlock) void real_kernel(GenArgs a, unsigned long l
         a.score_next[child] = score;
         const unsigned long long pb = pack_best(score, child);
         my_best = pb > my_best ? pb : my_best;
+        st.add(score);
       }
       if (tile_needed) __syncthreads();  // tiles are rewritten next iteration
     }
@@ -272,6 +274,7 @@ __global__ __launch_bounds__(kBlock) void real_kernel(GenArgs a, unsigned long l
   if (evals && best_parts) {
     unsigned long long b = block_max_u64(my_best, lds_red);
     if (threadIdx.x == 0) best_parts[blockIdx.x] = b;
+    if (a.stats_parts) block_stats_store(st, a.stats_parts);
   }
 }
 
@@ -314,6 +317,7 @@ __global__ __launch_bounds__(kBlock) void real_long_kernel(GenArgs a, unsigned l
   __syncthreads();
 
   unsigned long long my_best = 0;
+  ScoreStats st;
   for (uint64_t child = (uint64_t)blockIdx.x * GPB + g; child < a.S; child += (uint64_t)gridDim.x * GPB) {
     const bool elite = MODE == MODE_GEN && child < a.n_elite;  // wave-uniform
     const uint32_t src = elite ? (a.elite_idx ? a.elite_idx[child] : lds_elite) : 0u;
@@ -417,11 +421,13 @@ __global__ __launch_bounds__(kBlock) void real_long_kernel(GenArgs a, unsigned l
       a.score_next[child] = score;
       const unsigned long long pk = pack_best(score, child);
       my_best = pk > my_best ? pk : my_best;
+      st.add(score);
     }
   }
   if (evals && best_parts) {
     unsigned long long b = block_max_u64(my_best, lds_red);
     if (threadIdx.x == 0) best_parts[blockIdx.x] = b;
+    if (a.stats_parts) block_stats_store(st, a.stats_parts);
   }
 }
 
@@ -430,8 +436,7 @@ uint32_t launch_occ(K k, uint32_t children_per_block, size_t lds, const GenArgs&
                     hipStream_t s, bool& configured) {
   if (!configured) {
     // only the dynamic-LDS kernels may need more than the default 64 KiB
-    if (lds > 0)
-      PGA_HIP_CHECK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    if (lds > 0) allow_dynamic_lds((const void*)k);
     configured = true;
   }
   uint64_t need = (a.S + children_per_block - 1) / children_per_block;
@@ -521,6 +526,7 @@ __global__ __launch_bounds__(kBlock) void real_gen_fast(GenArgs a, unsigned long
   __syncthreads();
 
   unsigned long long my_best = 0;
+  ScoreStats st;
   for (uint64_t base = (uint64_t)blockIdx.x * ROWS; base < a.S; base += (uint64_t)gridDim.x * ROWS) {
     uint64_t ch[U];
     u32x4 pw[U];
@@ -676,6 +682,7 @@ __global__ __launch_bounds__(kBlock) void real_gen_fast(GenArgs a, unsigned long
         a.score_next[ch[u]] = score;
         const unsigned long long pb2 = pack_best(score, ch[u]);
         my_best = pb2 > my_best ? pb2 : my_best;
+        st.add(score);
       }
     }
     if (ROT) __syncthreads();  // X/Z are rewritten next iteration
@@ -683,6 +690,7 @@ __global__ __launch_bounds__(kBlock) void real_gen_fast(GenArgs a, unsigned long
   if (evals && best_parts) {
     unsigned long long b = block_max_u64(my_best, lds_red);
     if (threadIdx.x == 0) best_parts[blockIdx.x] = b;
+    if (a.stats_parts) block_stats_store(st, a.stats_parts);
   }
 }
 
@@ -809,6 +817,7 @@ __global__ __launch_bounds__(kBlock, ROT ? 4 : 1) void real_gen_pipe(GenArgs a, 
   __syncthreads();
 
   unsigned long long my_best = 0;
+  ScoreStats st;
   const uint64_t stride = (uint64_t)gridDim.x * GPB;
   uint64_t c0 = (uint64_t)blockIdx.x * GPB + threadIdx.x / GS;
   while (c0 < a.n_elite && c0 < a.S) {  // elites: copy row and score
@@ -819,6 +828,7 @@ __global__ __launch_bounds__(kBlock, ROT ? 4 : 1) void real_gen_pipe(GenArgs a, 
       a.score_next[c0] = sc;
       const unsigned long long pb = pack_best(sc, c0);
       my_best = pb > my_best ? pb : my_best;
+      st.add(sc);
     }
     c0 += stride;
   }
@@ -914,6 +924,7 @@ __global__ __launch_bounds__(kBlock, ROT ? 4 : 1) void real_gen_pipe(GenArgs a, 
       a.score_next[(c)] = sc_;                                                                  \
       const unsigned long long pb_ = pack_best(sc_, (c));                                       \
       my_best = pb_ > my_best ? pb_ : my_best;                                                  \
+      st.add(sc_);                                                                              \
     }                                                                                           \
   }
 
@@ -971,6 +982,7 @@ __global__ __launch_bounds__(kBlock, ROT ? 4 : 1) void real_gen_pipe(GenArgs a, 
   if (evals && best_parts) {
     unsigned long long b = block_max_u64(my_best, lds_red);
     if (threadIdx.x == 0) best_parts[blockIdx.x] = b;
+    if (a.stats_parts) block_stats_store(st, a.stats_parts);
   }
 }
 

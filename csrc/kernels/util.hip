@@ -60,6 +60,14 @@ bool force_generic_kernels() {
   return v;
 }
 
+size_t allow_dynamic_lds(const void* kernel) {
+  hipFuncAttributes at;
+  PGA_HIP_CHECK(hipFuncGetAttributes(&at, kernel));
+  const size_t avail = 160 * 1024 - at.sharedSizeBytes;
+  PGA_HIP_CHECK(hipFuncSetAttribute(kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)avail));
+  return avail;
+}
+
 uint32_t launch_grid_occ(uint64_t S, uint32_t per_block, const void* kernel) {
   uint64_t need = (S + per_block - 1) / per_block;
   uint64_t cap = (uint64_t)device_cu_count() * occupancy_blocks(kernel, dev::kBlock);
@@ -821,6 +829,36 @@ uint32_t best_of_scores_launch(const float* scores, uint64_t S, unsigned long lo
 void scores_to_keys_launch(const float* scores, uint64_t S, uint16_t* keys, hipStream_t s) {
   uint32_t grid = launch_grid(S, kBlock * 4);
   hipLaunchKernelGGL(scores_to_keys_kernel, grid, kBlock, 0, s, scores, S, keys);
+  PGA_HIP_CHECK(hipGetLastError());
+}
+
+// {min, max, sum, count} of a generation from the fused partials its kernel
+// stored: {min, sum} pairs (GenArgs::stats_parts) and packed bests (the max)
+__global__ __launch_bounds__(kBlock) void stats_from_parts_kernel(const float* parts, const unsigned long long* best,
+                                                                 uint32_t n, uint64_t S, float* out) {
+  __shared__ float lds[kBlock / 64];
+  __shared__ unsigned long long lds_b[kBlock / 64];
+  float mn = INFINITY, sm = 0.f;
+  unsigned long long b = 0;
+  for (uint32_t i = threadIdx.x; i < n; i += kBlock) {
+    mn = fminf(mn, parts[2 * i]);
+    sm += parts[2 * i + 1];
+    b = best[i] > b ? best[i] : b;
+  }
+  mn = block_reduce(mn, lds, FMin());
+  sm = block_reduce(sm, lds, FAdd());
+  b = block_max_u64(b, lds_b);
+  if (threadIdx.x == 0) {
+    out[0] = mn;
+    out[1] = best_score(b);
+    out[2] = sm;
+    out[3] = (float)S;
+  }
+}
+
+void stats_from_parts_launch(const float* parts, const unsigned long long* best, uint32_t n, uint64_t S, float* out,
+                             hipStream_t s) {
+  hipLaunchKernelGGL(stats_from_parts_kernel, 1, kBlock, 0, s, parts, best, n, S, out);
   PGA_HIP_CHECK(hipGetLastError());
 }
 

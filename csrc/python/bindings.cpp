@@ -153,6 +153,22 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("initialize", [](Island& i) { bind_stream(i); i.initialize(); })
       .def("evaluate", [](Island& i) { bind_stream(i); i.evaluate(); })
       .def("run", [](Island& i, uint32_t n) { bind_stream(i); i.run(n); }, py::arg("n") = 1)
+      .def("run_until",
+           [](Island& i, uint32_t n, float target, uint32_t every) {
+             bind_stream(i);
+             return i.run_until(n, target, every);
+           },
+           py::arg("n"), py::arg("target"), py::arg("check_every") = 10)
+      .def("set_stats_history", &Island::set_stats_history)
+      .def_property_readonly("stats_history", &Island::stats_history)
+      .def("history",
+           [](Island& i) {
+             bind_stream(i);
+             std::vector<float> h = i.history();
+             torch::Tensor t = torch::empty({(int64_t)(h.size() / 4), 4}, torch::kFloat32);
+             if (!h.empty()) std::memcpy(t.data_ptr<float>(), h.data(), 4 * h.size());
+             return t;
+           })
       .def("crossover_stage", [](Island& i) { bind_stream(i); i.crossover_stage(); })
       .def("mutate_stage", [](Island& i) { bind_stream(i); i.mutate_stage(); })
       .def("swap", &Island::swap)

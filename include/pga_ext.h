@@ -74,6 +74,12 @@ int pga_get_scores(pga_t *p, population_t *pop, float *out);             /* S fl
 int pga_get_genome(pga_t *p, population_t *pop, unsigned long i, void *out); /* raw row (row bytes) */
 size_t pga_row_bytes(const population_t *pop);
 int pga_stats(pga_t *p, population_t *pop, float out[4]);                /* min, max, sum, count */
+/* Per-generation history of {min, max, sum, count}: on != 0 clears and starts
+ * recording (each generation appends one row from its kernel's fused
+ * partials, stream-ordered); pga_get_stats_history copies up to max_rows rows
+ * (4 floats each) and returns the number recorded (-1 on error). */
+int pga_set_stats_history(pga_t *p, population_t *pop, int on);
+long pga_get_stats_history(pga_t *p, population_t *pop, float *out, unsigned long max_rows);
 int pga_synchronize(pga_t *p);
 
 /* ---- checkpoint / resume (exact: the generation counter is the RNG state) ---- */
@@ -131,6 +137,19 @@ int pga_comm_exchange(pga_t **solvers, int count, float pct);
 int pga_comm_best(pga_t *p, float *score, int *rank);
 /* pga_run_islands over every rank of an InitAll / loopback group at once */
 int pga_run_islands_multi(pga_t **solvers, int n, unsigned generations, unsigned m, float pct);
+
+/* ---- target-fitness termination ("until n generations or obj(best) ==
+ * value", include/pga.h of the reference) ----
+ * pga_run_until: pga_run, stopping once population 0's best score >= target;
+ * the best is read every check_every generations (0: 10), so there is one
+ * stream sync per check, none per generation.  Returns the generations run
+ * (-1 on error).
+ * pga_run_islands_until: pga_run_islands, checked at every migration point
+ * (every m generations; every 10 when m == 0) against the best over all
+ * populations and, with a communicator, over all ranks (an all-gather, so
+ * every rank stops at the same generation).  Returns the generations run. */
+int pga_run_until(pga_t *p, unsigned generations, float target, unsigned check_every);
+int pga_run_islands_until(pga_t *p, unsigned generations, unsigned m, float pct, float target);
 
 #ifdef __cplusplus
 }

@@ -165,6 +165,11 @@ class GeneticAlgorithm:
         if self.torch_objective is None and callback is None and target is None:
             self._island.run(int(generations))
             return int(generations)
+        if self.torch_objective is None and callback is None:
+            # native loop: one stream sync per check, none per generation
+            if self.best_score() >= target:
+                return 0
+            return int(self._island.run_until(int(generations), float(target), max(1, int(check_every))))
         done = 0
         while done < generations:
             n = min(check_every, generations - done)
@@ -203,6 +208,20 @@ class GeneticAlgorithm:
     def stats(self) -> dict:
         mn, mx, sm, n = self._island.stats()
         return {"min": mn, "max": mx, "mean": sm / max(n, 1.0), "generation": self.generation}
+
+    def record_history(self, on: bool = True) -> None:
+        """Start (clearing) or stop the per-generation statistics history:
+        every generation appends {min, max, sum, count} on the device from
+        its kernel's fused partials (no pass over the scores, no sync)."""
+        self._island.set_stats_history(bool(on))
+
+    def history(self) -> torch.Tensor:
+        """[generations, 4] float tensor of (min, max, mean, count) rows
+        recorded since record_history()."""
+        h = self._island.history()
+        if h.numel():
+            h[:, 2] = h[:, 2] / h[:, 3].clamp(min=1.0)
+        return h
 
     @property
     def scores(self) -> torch.Tensor:

@@ -66,6 +66,11 @@ def lib():
     L.pga_save.argtypes = [vp, vp, C.c_char_p]
     L.pga_load.argtypes = [vp, vp, C.c_char_p]
     L.pga_set_objective_source.argtypes = [vp, vp, C.c_char_p, C.c_char_p, C.POINTER(C.c_float), C.c_size_t]
+    L.pga_run_until.argtypes = [vp, C.c_uint, C.c_float, C.c_uint]
+    L.pga_run_islands_until.argtypes = [vp, C.c_uint, C.c_uint, C.c_float, C.c_float]
+    L.pga_set_stats_history.argtypes = [vp, vp, C.c_int]
+    L.pga_get_stats_history.restype = C.c_long
+    L.pga_get_stats_history.argtypes = [vp, vp, C.POINTER(C.c_float), C.c_ulong]
     L.free_ = C.CDLL(None).free
     L.free_.argtypes = [vp]
     return L
@@ -181,6 +186,65 @@ def test_binary_and_checkpoint(lib, tmp_path):
     assert lib.pga_generation(pop2) == 5
     lib.pga_deinit(p)
     lib.pga_deinit(q)
+
+
+def onemax_pop(lib, p, S=512, L=64):
+    pop = lib.pga_create_population_ext(p, S, L, PGA_BINARY)
+    lib.pga_set_objective_builtin(p, pop, 1, None, 0, None, 0, 0, 0.0, 0.0)
+    lib.pga_set_operators(p, pop, 0, 2, 2, 1.0, 0, -1.0, 0.0, 1)
+    return pop
+
+
+def test_run_until_target(lib):
+    """pga_run_until stops at the first check point whose best reaches the
+    target (reference include/pga.h: "until n-generations or
+    obj_func(best_genome) == value"); the same seed run to the reported
+    generation count reaches it too."""
+    p = new(lib, seed=5)
+    pop = onemax_pop(lib, p)
+    g = lib.pga_run_until(p, 500, 64.0, 5)
+    assert 0 < g < 500 and g % 5 == 0
+    assert lib.pga_best_score(p, pop) == 64.0
+    assert lib.pga_generation(pop) == g
+    # checked every 5: the target was not yet reached 5 generations earlier
+    q = new(lib, seed=5)
+    pop2 = onemax_pop(lib, q)
+    lib.pga_run(q, g - 5)
+    assert lib.pga_best_score(q, pop2) < 64.0
+    # an unreachable target runs every generation
+    assert lib.pga_run_until(q, 7, 1e9, 3) == 7
+    lib.pga_deinit(p)
+    lib.pga_deinit(q)
+
+
+def test_run_islands_until_target(lib):
+    p = new(lib, seed=6)
+    pops = [onemax_pop(lib, p, S=256) for _ in range(3)]
+    g = lib.pga_run_islands_until(p, 400, 10, 0.05, 64.0)
+    assert 0 < g < 400 and g % 10 == 0
+    assert max(lib.pga_best_score(p, q) for q in pops) == 64.0
+    lib.pga_deinit(p)
+
+
+def test_stats_history(lib):
+    """Per-generation {min, max, sum, count} rows equal pga_stats taken after
+    each generation."""
+    p = new(lib, seed=7)
+    pop = onemax_pop(lib, p)
+    assert lib.pga_set_stats_history(p, pop, 1) == 0
+    ref = []
+    out4 = (C.c_float * 4)()
+    for _ in range(6):
+        lib.pga_run(p, 1)
+        lib.pga_stats(p, pop, out4)
+        ref.append(list(out4))
+    buf = (C.c_float * 40)()
+    assert lib.pga_get_stats_history(p, pop, buf, 10) == 6
+    rows = [list(buf[4 * i:4 * i + 4]) for i in range(6)]
+    assert rows == ref
+    assert lib.pga_set_stats_history(p, pop, 1) == 0  # restart clears
+    assert lib.pga_get_stats_history(p, pop, None, 0) == 0
+    lib.pga_deinit(p)
 
 
 def run_ex(args, inp=None, timeout=300):
