@@ -4,10 +4,12 @@
 One process, torch.distributed backend "nccl" (= RCCL) with world size 1 on
 the box's one GPU.  The island model is told it has a peer, but both peers
 are rank 0, so every migration epoch runs the real overlapped RCCL path
-(side-stream top-k + pack, batch_isend_irecv = grouped ncclSend/ncclRecv,
+(fused top-k + pack, batch_isend_irecv = grouped ncclSend/ncclRecv,
 stream wait, bottom-k + scatter) with the migrants going back to the
 sending island.  The result must be bit-identical to the same run whose
-"network" is a device copy on the posting stream.
+"network" is a device copy on the posting stream.  Mode "match" runs this
+twice: with emigrant selection + packing on the compute stream (the default)
+and on the side stream (side_stream=True).
 """
 import os
 import sys
@@ -39,7 +41,13 @@ def main(port: int) -> None:
 
     torch.cuda.set_device(0)
     dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
-    a = model(pga, IslandModel)
+    for side in (False, True):
+        match(pga, IslandModel, side)
+    dist.destroy_process_group()
+
+
+def match(pga, IslandModel, side: bool) -> None:
+    a = model(pga, IslandModel, side_stream=side)
     a.run(31)
     torch.cuda.synchronize()
 
@@ -54,7 +62,7 @@ def main(port: int) -> None:
     dist.batch_isend_irecv = fake_batch
     dist.P2POp = lambda op, t, peer, group=None: types.SimpleNamespace(op=op, tensor=t)
     try:
-        b = model(pga, IslandModel)
+        b = model(pga, IslandModel, side_stream=side)
         b.run(31)
         torch.cuda.synchronize()
     finally:
@@ -64,8 +72,7 @@ def main(port: int) -> None:
     assert not a.degraded and a.failures == 0
     assert torch.equal(a.ga.rows, b.ga.rows), "RCCL self-exchange diverged from the loopback exchange"
     assert torch.equal(a.ga.scores, b.ga.scores)
-    dist.destroy_process_group()
-    print("rccl self-exchange ok", a.migrations, a.bytes_sent)
+    print("rccl self-exchange ok", "side stream" if side else "compute stream", a.migrations, a.bytes_sent)
 
 
 def withhold(port: int) -> None:

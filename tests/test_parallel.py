@@ -116,7 +116,7 @@ def test_rccl_self_exchange_matches_loopback_gpu():
     r = subprocess.run([sys.executable, os.path.join(HERE, "rccl_self_worker.py"), str(free_port())], env=env,
                        capture_output=True, text=True, timeout=110)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
-    assert "rccl self-exchange ok" in r.stdout
+    assert r.stdout.count("rccl self-exchange ok") == 2  # compute-stream and side-stream emigrant packing
 
 
 @pytest.mark.gpu
