@@ -1002,6 +1002,17 @@ int pga_comm_init_loopback(pga_t** solvers, int n) { return init_group(solvers, 
 int pga_comm_rank(const pga_t* p) { return p && p->comm ? p->comm_rank : 0; }
 int pga_comm_size(const pga_t* p) { return p && p->comm ? p->comm->size() : 1; }
 
+static_assert((int)PGA_MIGRATE_TOPK == pga::MIG_TOPK && (int)PGA_MIGRATE_STRIPE == pga::MIG_STRIPE,
+              "pga_ext.h migration policies mirror core.hpp");
+
+int pga_set_migration_policy(pga_t* p, population_t* pop, enum pga_migration_policy policy) {
+  if (!valid_pop(p, pop)) return -1;
+  return guard_r<int>(p, -1, [&]() {
+    pop->isl->set_migration_policy((int)policy);
+    return 0;
+  });
+}
+
 int pga_comm_set_topology(pga_t* p, enum pga_topology t) {
   if (!p || (t != PGA_TOPO_RING && t != PGA_TOPO_RANDOM && t != PGA_TOPO_ALL_TO_ALL)) return -1;
   if (p->comm_members)

@@ -385,6 +385,32 @@ void topk(const float* scores, uint64_t S, uint32_t k, bool largest, uint32_t* i
     }
 }
 
+void stripe_emigrate(const float* scores, const void* rows, uint32_t row_words, uint64_t S, uint32_t k,
+                     void* out_rows, float* out_scores) {
+  for (uint32_t i = 0; i < k; ++i) {
+    const uint64_t lo = (uint64_t)i * S / k, hi = (uint64_t)(i + 1) * S / k;
+    unsigned long long b = 0;
+    for (uint64_t j = lo; j < hi; ++j) b = std::max(b, pack_best(scores[j], j));
+    const uint64_t src = best_index(b);
+    std::memcpy((uint32_t*)out_rows + (uint64_t)i * row_words, (const uint32_t*)rows + src * row_words,
+                4ull * row_words);
+    out_scores[i] = scores[src];
+  }
+}
+
+void stripe_immigrate(float* scores, void* rows, uint32_t row_words, uint64_t S, uint32_t k, const void* in_rows,
+                      const float* in_scores) {
+  for (uint32_t i = 0; i < k; ++i) {
+    const uint64_t lo = (uint64_t)i * S / k, hi = (uint64_t)(i + 1) * S / k;
+    unsigned long long w = ~0ull;  // (score key << 32 | index): the minimum is the worst, lowest index
+    for (uint64_t j = lo; j < hi; ++j) w = std::min(w, ((unsigned long long)score_key(scores[j]) << 32) | j);
+    const uint64_t dst = (uint32_t)w;
+    std::memcpy((uint32_t*)rows + dst * row_words, (const uint32_t*)in_rows + (uint64_t)i * row_words,
+                4ull * row_words);
+    scores[dst] = in_scores[i];
+  }
+}
+
 void gather_rows(const void* rows, const float* scores, uint32_t row_words, const uint32_t* idx, uint32_t n,
                  void* out_rows, float* out_scores) {
   for (uint32_t r = 0; r < n; ++r) {

@@ -556,10 +556,24 @@ void Island::scatter(const uint32_t* idx, uint32_t n, const void* in_rows, const
   rebest();  // best partials and tournament keys follow the new scores
 }
 
+void Island::set_migration_policy(int p) {
+  if (p != MIG_TOPK && p != MIG_STRIPE) throw std::invalid_argument("migration policy must be MIG_TOPK or MIG_STRIPE");
+  mig_policy_ = p;
+}
+
 void Island::emigrate(uint32_t k, void* out_rows, float* out_scores) {
   TraceRange tr("pga.migrate.emigrate");
   if (k == 0) return;
   if (k > cfg_.S) throw std::invalid_argument("k exceeds population size");
+  if (mig_policy_ == MIG_STRIPE) {
+    if (on_gpu())
+      stripe_emigrate_launch((const float*)scores_[cur_].ptr, rows_[cur_].ptr, row_words_, cfg_.S, k, out_rows,
+                             out_scores, stream);
+    else
+      cpu::stripe_emigrate((const float*)scores_[cur_].ptr, rows_[cur_].ptr, row_words_, cfg_.S, k, out_rows,
+                           out_scores);
+    return;
+  }
   const uint16_t* k16 = integer_objective(cfg_.objective, cfg_.L) ? (const uint16_t*)keys_[cur_].ptr : nullptr;
   if (on_gpu() && topk_move_supported(k16, cfg_.L + 1, cfg_.S)) {
     ensure_topk_ws(k);
@@ -584,6 +598,19 @@ void Island::immigrate(uint32_t k, const void* in_rows, const float* in_scores) 
   if (k == 0) return;
   if (k > cfg_.S) throw std::invalid_argument("k exceeds population size");
   uint16_t* k16 = integer_objective(cfg_.objective, cfg_.L) ? (uint16_t*)keys_[cur_].ptr : nullptr;
+  if (mig_policy_ == MIG_STRIPE) {
+    if (on_gpu()) {
+      // victims, their keys, and the island's best partials + statistics in one pass
+      float* sp = fused_stats() ? (float*)stats_parts_[cur_].ptr : nullptr;
+      n_best_[cur_] = stripe_immigrate_launch((float*)scores_[cur_].ptr, k16, rows_[cur_].ptr, row_words_, cfg_.S, k,
+                                              in_rows, in_scores, (unsigned long long*)best_[cur_].ptr, sp, stream);
+      stats_ok_[cur_] = sp != nullptr;
+    } else {
+      cpu::stripe_immigrate((float*)scores_[cur_].ptr, rows_[cur_].ptr, row_words_, cfg_.S, k, in_rows, in_scores);
+      rebest();
+    }
+    return;
+  }
   if (on_gpu() && topk_move_supported(k16, cfg_.L + 1, cfg_.S)) {
     ensure_topk_ws(k);
     TopkMove mv;

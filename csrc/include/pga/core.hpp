@@ -89,6 +89,13 @@ enum Objective : int32_t {
   OBJ_USER_FNPTR = 64,   // REAL: reference-ABI device function pointer obj_f
 };
 
+// Island migration policy (Island::emigrate / immigrate)
+enum MigrationPolicy : int32_t {
+  MIG_TOPK = 0,    // exact: the top-k emigrate, the bottom-k are replaced (two radix selections)
+  MIG_STRIPE = 1,  // the population is cut into k contiguous stripes; stripe i's best
+                   // emigrates and its worst is replaced by immigrant i (one pass each)
+};
+
 // Philox streams (purpose tags, high byte of counter word 0)
 enum Stream : uint32_t {
   ST_INIT = 1,     // initial population

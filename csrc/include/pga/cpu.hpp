@@ -28,6 +28,11 @@ void score_stats(const float* scores, uint64_t S, float* out4);
 void roulette_prefix(const float* scores, uint64_t S, float* cumfit);
 void rank_order(const float* scores, uint64_t S, uint32_t* order);
 void topk(const float* scores, uint64_t S, uint32_t k, bool largest, uint32_t* idx_out, bool sorted = true);
+// MIG_STRIPE migration (see ops.hpp stripe_*_launch)
+void stripe_emigrate(const float* scores, const void* rows, uint32_t row_words, uint64_t S, uint32_t k,
+                     void* out_rows, float* out_scores);
+void stripe_immigrate(float* scores, void* rows, uint32_t row_words, uint64_t S, uint32_t k, const void* in_rows,
+                      const float* in_scores);
 void gather_rows(const void* rows, const float* scores, uint32_t row_words, const uint32_t* idx, uint32_t n,
                  void* out_rows, float* out_scores);
 void scatter_rows(void* rows, float* scores, uint32_t row_words, const uint32_t* idx, uint32_t n,

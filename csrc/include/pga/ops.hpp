@@ -138,6 +138,17 @@ bool topk_move_supported(const uint16_t* keys16, uint32_t key_range, uint64_t S)
 void topk_launch(const float* scores, const uint16_t* keys16, uint32_t key_range, uint64_t S, uint32_t k, bool largest,
                  bool sorted, uint32_t* idx_out, void* workspace, hipStream_t s, const TopkMove* mv = nullptr);
 // rows: out[i] = rows[idx[i]] (row_words 32-bit words per row), optional scores
+// MIG_STRIPE migration (util.hip): stripe i of k = individuals [i*S/k, (i+1)*S/k).
+// emigrate: the best of every stripe (ties: lowest index) -> out rows/scores[i].
+// immigrate: in row/score i replaces the worst of stripe i (ties: lowest
+// index), the tournament key follows, and the kernel writes the island's new
+// per-block best partials (+ {min, sum} statistics when stats_parts is set) —
+// the stripes cover the population, so they are complete.  Returns their count.
+void stripe_emigrate_launch(const float* scores, const void* rows, uint32_t row_words, uint64_t S, uint32_t k,
+                            void* out_rows, float* out_scores, hipStream_t s);
+uint32_t stripe_immigrate_launch(float* scores, uint16_t* keys, void* rows, uint32_t row_words, uint64_t S, uint32_t k,
+                                 const void* in_rows, const float* in_scores, unsigned long long* best_parts,
+                                 float* stats_parts, hipStream_t s);
 void gather_rows_launch(const void* rows, const float* scores, uint32_t row_words, const uint32_t* idx, uint32_t n,
                         void* out_rows, float* out_scores, hipStream_t s);
 // rows[idx[i]] = in[i]

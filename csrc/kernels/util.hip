@@ -793,6 +793,109 @@ __global__ __launch_bounds__(kBlock) void scatter_rows_kernel(uint4* rows, float
   }
 }
 
+// ---- MIG_STRIPE migration: one wave per stripe (grid-stride over stripes) ----
+__device__ __forceinline__ uint16_t score_to_key16(float v) {
+  return (uint16_t)(!(v > 0.f) ? 0.f : (v >= 65535.f ? 65535.f : v));
+}
+
+// 16 lanes per stripe (4 stripes per wave): at 1% of 1M the k = 10486 stripes
+// of ~100 individuals are 2622 waves, all resident at once, each lane loading
+// its ~7 scores in one burst
+constexpr uint32_t kStripeLanes = 16;
+constexpr uint32_t kStripeCache = 8;  // scores per lane kept in registers (stripes <= 128)
+
+__global__ __launch_bounds__(kBlock) void stripe_emigrate_kernel(const float* __restrict__ scores,
+                                                                 const uint4* __restrict__ rows, uint32_t rw16,
+                                                                 uint64_t S, uint32_t k, uint4* __restrict__ out,
+                                                                 float* __restrict__ out_scores) {
+  const uint32_t sl = threadIdx.x & (kStripeLanes - 1);
+  const uint32_t ng = gridDim.x * (kBlock / kStripeLanes);
+  for (uint32_t i = (blockIdx.x * kBlock + threadIdx.x) / kStripeLanes; i < k; i += ng) {  // group-uniform
+    const uint64_t lo = (uint64_t)i * S / k, hi = (uint64_t)(i + 1) * S / k;
+    unsigned long long b = 0;
+    for (uint64_t j = lo + sl; j < hi; j += kStripeLanes) {
+      const unsigned long long p = pack_best(scores[j], j);
+      b = p > b ? p : b;
+    }
+#pragma unroll
+    for (int o = kStripeLanes / 2; o > 0; o >>= 1) {
+      const unsigned long long x = shfl_xor_u64(b, o);
+      b = x > b ? x : b;
+    }
+    const uint64_t src = best_index(b);
+    for (uint32_t c = sl; c < rw16; c += kStripeLanes) out[(uint64_t)i * rw16 + c] = rows[src * rw16 + c];
+    if (sl == 0) out_scores[i] = best_score(b);
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void stripe_immigrate_kernel(float* __restrict__ scores, uint16_t* keys,
+                                                                  uint4* __restrict__ rows, uint32_t rw16, uint64_t S,
+                                                                  uint32_t k, const uint4* __restrict__ in,
+                                                                  const float* __restrict__ in_scores,
+                                                                  unsigned long long* best_parts, float* stats_parts) {
+  __shared__ unsigned long long lds_red[kBlock / 64];
+  const uint32_t sl = threadIdx.x & (kStripeLanes - 1);
+  const uint32_t ng = gridDim.x * (kBlock / kStripeLanes);
+  unsigned long long my_best = 0;
+  ScoreStats st;
+  for (uint32_t i = (blockIdx.x * kBlock + threadIdx.x) / kStripeLanes; i < k; i += ng) {  // group-uniform
+    const uint64_t lo = (uint64_t)i * S / k, hi = (uint64_t)(i + 1) * S / k;
+    const bool cached = hi - lo <= (uint64_t)kStripeLanes * kStripeCache;  // group-uniform
+    // the immigrant (independent of the victim: issued with the score loads)
+    const float sin = in_scores[i];
+    const uint4 r0 = sl < rw16 ? in[(uint64_t)i * rw16 + sl] : make_uint4(0, 0, 0, 0);
+    float v[kStripeCache];
+    unsigned long long w = ~0ull;  // min of (score key << 32 | index): the worst, lowest index
+#pragma unroll
+    for (uint32_t t = 0; t < kStripeCache; ++t) {
+      const uint64_t j = lo + sl + (uint64_t)t * kStripeLanes;
+      v[t] = (cached && j < hi) ? scores[j] : 0.f;
+      const unsigned long long p = ((unsigned long long)score_key(v[t]) << 32) | j;
+      w = (cached && j < hi && p < w) ? p : w;
+    }
+    if (!cached)
+      for (uint64_t j = lo + sl; j < hi; j += kStripeLanes) {
+        const unsigned long long p = ((unsigned long long)score_key(scores[j]) << 32) | j;
+        w = p < w ? p : w;
+      }
+#pragma unroll
+    for (int o = kStripeLanes / 2; o > 0; o >>= 1) {
+      const unsigned long long x = shfl_xor_u64(w, o);
+      w = x < w ? x : w;
+    }
+    const uint64_t dst = (uint32_t)w;
+    if (sl < rw16) rows[dst * rw16 + sl] = r0;
+    for (uint32_t c = sl + kStripeLanes; c < rw16; c += kStripeLanes) rows[dst * rw16 + c] = in[(uint64_t)i * rw16 + c];
+    if (sl == 0) {
+      scores[dst] = sin;
+      if (keys) keys[dst] = score_to_key16(sin);
+    }
+    // the stripe after the replacement: best partial and statistics
+    if (cached) {
+#pragma unroll
+      for (uint32_t t = 0; t < kStripeCache; ++t) {
+        const uint64_t j = lo + sl + (uint64_t)t * kStripeLanes;
+        if (j < hi) {
+          const float x = j == dst ? sin : v[t];
+          const unsigned long long p = pack_best(x, j);
+          my_best = p > my_best ? p : my_best;
+          st.add(x);
+        }
+      }
+    } else {
+      for (uint64_t j = lo + sl; j < hi; j += kStripeLanes) {
+        const float x = j == dst ? sin : scores[j];
+        const unsigned long long p = pack_best(x, j);
+        my_best = p > my_best ? p : my_best;
+        st.add(x);
+      }
+    }
+  }
+  const unsigned long long b = block_max_u64(my_best, lds_red);
+  if (threadIdx.x == 0) best_parts[blockIdx.x] = b;
+  if (stats_parts) block_stats_store(st, stats_parts);
+}
+
 __global__ __launch_bounds__(kBlock) void scores_to_keys_kernel(const float* s, uint64_t S, uint16_t* k) {
   for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < S; i += (uint64_t)gridDim.x * kBlock) {
     const float v = s[i];
@@ -1062,6 +1165,29 @@ void gather_rows_launch(const void* rows, const float* scores, uint32_t row_word
   hipLaunchKernelGGL(gather_rows_kernel, grid, kBlock, 0, s, (const uint4*)rows, scores, rw16, idx, n,
                      (uint4*)out_rows, out_scores);
   PGA_HIP_CHECK(hipGetLastError());
+}
+
+void stripe_emigrate_launch(const float* scores, const void* rows, uint32_t row_words, uint64_t S, uint32_t k,
+                            void* out_rows, float* out_scores, hipStream_t s) {
+  if (k == 0) return;
+  if (k > S) throw std::invalid_argument("stripe migration: k exceeds the population");
+  uint64_t grid = ((uint64_t)k + kBlock / kStripeLanes - 1) / (kBlock / kStripeLanes);
+  if (grid > kMaxGrid) grid = kMaxGrid;
+  hipLaunchKernelGGL(stripe_emigrate_kernel, (uint32_t)grid, kBlock, 0, s, scores, (const uint4*)rows, row_words / 4,
+                     S, k, (uint4*)out_rows, out_scores);
+  PGA_HIP_CHECK(hipGetLastError());
+}
+
+uint32_t stripe_immigrate_launch(float* scores, uint16_t* keys, void* rows, uint32_t row_words, uint64_t S, uint32_t k,
+                                 const void* in_rows, const float* in_scores, unsigned long long* best_parts,
+                                 float* stats_parts, hipStream_t s) {
+  if (k == 0 || k > S) throw std::invalid_argument("stripe migration: k must be in [1, S]");
+  uint64_t grid = ((uint64_t)k + kBlock / kStripeLanes - 1) / (kBlock / kStripeLanes);
+  if (grid > kMaxGrid) grid = kMaxGrid;
+  hipLaunchKernelGGL(stripe_immigrate_kernel, (uint32_t)grid, kBlock, 0, s, scores, keys, (uint4*)rows, row_words / 4,
+                     S, k, (const uint4*)in_rows, in_scores, best_parts, stats_parts);
+  PGA_HIP_CHECK(hipGetLastError());
+  return (uint32_t)grid;
 }
 
 void scatter_rows_launch(void* rows, float* scores, uint32_t row_words, const uint32_t* idx, uint32_t n,

@@ -52,6 +52,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   E(SEL_TOURNAMENT); E(SEL_ROULETTE); E(SEL_RANDOM); E(SEL_RANK);
   E(XO_UNIFORM); E(XO_ONE_POINT); E(XO_TWO_POINT); E(XO_BLEND); E(XO_ARITHMETIC); E(XO_PMX); E(XO_OX); E(XO_NONE);
   E(MUT_BIT_FLIP); E(MUT_GAUSSIAN); E(MUT_UNIFORM); E(MUT_RESET_ONE); E(MUT_SWAP); E(MUT_INVERSION); E(MUT_NONE);
+  E(MIG_TOPK); E(MIG_STRIPE);
   E(OBJ_NONE); E(OBJ_ONEMAX); E(OBJ_KNAPSACK); E(OBJ_TRAP); E(OBJ_LEADING_ONES); E(OBJ_QUBO);
   E(OBJ_SPHERE); E(OBJ_RASTRIGIN); E(OBJ_ROSENBROCK); E(OBJ_ACKLEY); E(OBJ_GRIEWANK); E(OBJ_SCHWEFEL);
   E(OBJ_LINEAR); E(OBJ_KNAPSACK_REAL); E(OBJ_TSP_RANDOM_KEY); E(OBJ_TSP); E(OBJ_TSP_OPEN); E(OBJ_TSP_EUC); E(OBJ_USER_FNPTR);
@@ -141,6 +142,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def_property("graph_generations", &Island::graph_generations, &Island::set_graph_generations)
       .def_property_readonly("graph_replays", &Island::graph_replays)
       .def_property_readonly("knapsack_digits", &Island::knapsack_digits)
+      .def_property("migration_policy", &Island::migration_policy, &Island::set_migration_policy)
       .def("config", [](Island& i) { return i.config(); })
       .def("set_operators", [](Island& i, const pga::Config& c) { bind_stream(i); i.set_operators(c); })
       .def("set_objective_data",

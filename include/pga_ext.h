@@ -116,6 +116,14 @@ int pga_comm_init_loopback(pga_t **solvers, int n);
 int pga_comm_rank(const pga_t *p);
 int pga_comm_size(const pga_t *p);
 int pga_comm_set_topology(pga_t *p, enum pga_topology t); /* applies to the whole local group */
+/* Emigrant / victim choice of every migration of `pop` (pga_migrate*,
+ * pga_run_islands*, inter-rank epochs).  STRIPE (default): the population is
+ * cut into k contiguous stripes; stripe i's best emigrates and its worst is
+ * replaced by immigrant i — one pass over the scores each way, so the global
+ * best always emigrates.  TOPK: the exact top-k emigrate and the bottom-k are
+ * replaced (two radix selections). */
+enum pga_migration_policy { PGA_MIGRATE_TOPK = 0, PGA_MIGRATE_STRIPE = 1 };
+int pga_set_migration_policy(pga_t *p, population_t *pop, enum pga_migration_policy policy);
 /* > 0: after each exchange wait at most `seconds` on the host (RCCL: event
  * polling + async error check); a failed or late exchange aborts the
  * communicator and the islands continue alone (degraded).  0 (default):

@@ -6,12 +6,14 @@ exports its top ``migrate_pct`` individuals and imports the same number from
 its peer(s), replacing its worst individuals.
 
 Data path per migration (all on-device, no host synchronisation):
-  top-k selection with the row gather fused in (Island.emigrate: u16-key
-  histogram + one ticketed select kernel writing rows+scores into ONE packed
-  send buffer) -> RCCL send/recv on torch's NCCL stream -> [next generation
-  kernel runs concurrently on the compute stream] -> stream wait on the NCCL
-  work -> re-score -> bottom-k selection with the scatter fused in
-  (Island.immigrate).
+  emigrant selection with the row gather fused in (Island.emigrate; policy
+  "stripe": the best of each of k population stripes, one pass; "topk": the
+  exact top-k, u16-key histogram + one ticketed select kernel) writing
+  rows+scores into ONE packed send buffer -> RCCL send/recv on torch's NCCL
+  stream -> [next generation kernel runs concurrently on the compute stream]
+  -> stream wait on the NCCL work -> re-score -> victims replaced with the
+  scatter fused in (Island.immigrate: each stripe's worst, or the bottom-k),
+  best partials and statistics written by the same kernel.
 
 Why this shape on MI355X: the 8 GPUs of a node are fully connected by xGMI,
 7 point-to-point links of ~153 GB/s each.  A ring migration uses one link per
@@ -54,6 +56,7 @@ import torch.distributed as dist
 
 from ..ga import GeneticAlgorithm
 from ..utils.log import get_logger
+from .local import migration_policy
 
 log = get_logger(__name__)
 
@@ -97,6 +100,7 @@ class IslandModel:
         validate: bool = True,
         timeout_s: Optional[float] = None,
         fault_hook: Optional[Callable[[torch.Tensor, int], bool]] = None,
+        policy: str = "stripe",
     ):
         if topology not in TOPOLOGIES:
             raise ValueError(f"topology must be one of {TOPOLOGIES}")
@@ -122,6 +126,7 @@ class IslandModel:
             per = max(1, self.k // (self.world - 1))
             self.k = per * (self.world - 1)
         isl = ga.island
+        isl.migration_policy = migration_policy(policy)  # stripe: one pass each way; topk: exact
         self.rw = int(isl.row_words)
         dev = isl.rows(0).device
         n = self.k * (self.rw + 1)

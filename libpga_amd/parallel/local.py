@@ -24,10 +24,21 @@ from ..ga import GeneticAlgorithm
 from ..models.base import Problem
 
 
+def migration_policy(name: str) -> int:
+    """"stripe" (default): the population is cut into k stripes; each stripe's
+    best emigrates and its worst is replaced — one pass each.  "topk": the
+    exact top-k emigrate and the bottom-k are replaced (two radix selections)."""
+    from .._ext import C
+    try:
+        return {"stripe": C.MIG_STRIPE, "topk": C.MIG_TOPK}[name]
+    except KeyError:
+        raise ValueError("migration policy must be 'stripe' or 'topk'") from None
+
+
 class LocalIslands:
     def __init__(self, problem: Problem, n_islands: int, pop_size: int, *, seed: Optional[int] = None,
                  device=None, migrate_every: int = 10, migrate_pct: float = 0.01, topology: str = "ring",
-                 first_island: int = 0, **op_overrides):
+                 first_island: int = 0, policy: str = "stripe", **op_overrides):
         if n_islands < 1:
             raise ValueError("n_islands must be >= 1")
         if topology not in ("ring", "random"):
@@ -36,6 +47,8 @@ class LocalIslands:
             GeneticAlgorithm(problem, pop_size, seed=seed, island=first_island + i, device=device, **op_overrides)
             for i in range(n_islands)
         ]
+        for ga in self.islands:
+            ga.island.migration_policy = migration_policy(policy)
         self.device = self.islands[0].device
         self.migrate_every = int(migrate_every)
         self.topology = topology

@@ -24,8 +24,14 @@ def run(rank: int, world: int, port: int, topology: str, out_dir: str) -> None:
     ga.run(5)
     send_scores = ga.scores.clone()
     k = model.k
-    top_idx = ga.island.topk(k, True).long()
-    emigrants = ga.rows.clone()[top_idx]
+    # the default stripe policy: the best of each of k stripes (ties: lowest index)
+    S = send_scores.numel()
+    top_idx = []
+    for i in range(k):
+        lo, hi = i * S // k, (i + 1) * S // k
+        seg = send_scores[lo:hi]
+        top_idx.append(lo + int(torch.nonzero(seg == seg.max())[0]))
+    emigrants = ga.rows.clone()[torch.tensor(top_idx)]
     model.start_migration()
     model.finish_migration()
     torch.save({"rank": rank, "emigrants": emigrants, "rows_after": ga.rows.clone(), "k": k,

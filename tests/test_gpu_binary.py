@@ -263,6 +263,7 @@ def test_fused_migration_matches_unfused(S, k):
     a.run(3)
     b.run(3)
     ia, ib = a.island, b.island
+    ia.migration_policy = pga._ext.C.MIG_TOPK
     rw = int(ia.row_words)
     ra, sa = torch.empty(k * rw, dtype=torch.int32, device=DEV), torch.empty(k, device=DEV)
     rb, sb = torch.empty_like(ra), torch.empty_like(sa)
@@ -284,3 +285,62 @@ def test_fused_migration_matches_unfused(S, k):
     b.run(2)  # identical keys => identical tournaments
     torch.cuda.synchronize()
     assert torch.equal(a.rows, b.rows) and torch.equal(a.scores, b.scores)
+
+
+def stripe_reference(scores, rows, k):
+    """Plain-torch MIG_STRIPE: per stripe [i*S//k, (i+1)*S//k) the best
+    (ties: lowest index) and the worst (ties: lowest index)."""
+    S = scores.numel()
+    best, worst = [], []
+    for i in range(k):
+        lo, hi = i * S // k, (i + 1) * S // k
+        s = scores[lo:hi].double()
+        best.append(lo + int(torch.nonzero(s == s.max())[0]))
+        worst.append(lo + int(torch.nonzero(s == s.min())[0]))
+    return best, worst
+
+
+@pytest.mark.parametrize("S,k", [(5000, 50), (100003, 997)])
+@pytest.mark.parametrize("prob", ["onemax", "knapsack"])
+def test_stripe_migration_gpu(S, k, prob):
+    """Stripe policy (the default): GPU == CPU backend bit for bit, == the
+    torch reference, and the immigrate kernel's fused best partials and
+    statistics describe the new population exactly."""
+    p = pga.models.OneMax(1024) if prob == "onemax" else pga.models.Knapsack01.random(700, seed=4)
+    g, c = pair(p, S, elitism=1)
+    g.run(3)
+    c.run(3)
+    same(g, c)
+    gi, ci = g.island, c.island
+    assert gi.migration_policy == pga._ext.C.MIG_STRIPE
+    rw = int(gi.row_words)
+    out_g = torch.empty(k * rw, dtype=torch.int32, device=DEV), torch.empty(k, device=DEV)
+    out_c = torch.empty(k * rw, dtype=torch.int32), torch.empty(k)
+    gi.emigrate(k, *out_g)
+    ci.emigrate(k, *out_c)
+    torch.cuda.synchronize()
+    assert torch.equal(out_g[0].cpu(), out_c[0]) and torch.equal(out_g[1].cpu(), out_c[1])
+    best, worst = stripe_reference(c.scores, c.rows, k)
+    assert torch.equal(out_c[1], c.scores[best])
+    assert torch.equal(out_c[0].view(k, rw), c.rows[best])
+    # immigrants: another island's emigrants replace each stripe's worst
+    d = pga.GeneticAlgorithm(p, S, seed=77, device="cpu", elitism=1)
+    d.run(4)
+    inc = torch.empty(k * rw, dtype=torch.int32), torch.empty(k)
+    d.island.emigrate(k, *inc)
+    expect_rows, expect_scores = c.rows.clone(), c.scores.clone()
+    expect_rows[worst] = inc[0].view(k, rw)
+    expect_scores[worst] = inc[1]
+    gi.immigrate(k, inc[0].to(DEV), inc[1].to(DEV))
+    ci.immigrate(k, *inc)
+    torch.cuda.synchronize()
+    assert torch.equal(c.rows, expect_rows) and torch.equal(c.scores, expect_scores)
+    same(g, c)
+    assert g.best_score() == c.best_score() == float(expect_scores.max())
+    assert g.island.best()[1] == int(torch.nonzero(expect_scores == expect_scores.max())[0])
+    st = g.stats()
+    assert st["min"] == float(expect_scores.min()) and st["max"] == float(expect_scores.max())
+    assert st["mean"] == pytest.approx(float(expect_scores.double().mean()), rel=1e-5)
+    g.run(2)
+    c.run(2)  # keys of the replaced individuals follow their scores
+    same(g, c)

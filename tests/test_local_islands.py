@@ -7,12 +7,24 @@ import libpga_amd as pga
 from libpga_amd.parallel import LocalIslands
 
 
-def test_local_islands_ring_migration_cpu():
-    li = LocalIslands(pga.models.OneMax(100), 4, 200, seed=3, device="cpu", migrate_every=5, migrate_pct=0.05)
+def stripe_best(scores, k):
+    S = scores.numel()
+    out = []
+    for i in range(k):
+        lo, hi = i * S // k, (i + 1) * S // k
+        s = scores[lo:hi]
+        out.append(lo + int(torch.nonzero(s == s.max())[0]))
+    return torch.tensor(out)
+
+
+@pytest.mark.parametrize("policy", ["stripe", "topk"])
+def test_local_islands_ring_migration_cpu(policy):
+    li = LocalIslands(pga.models.OneMax(100), 4, 200, seed=3, device="cpu", migrate_every=5, migrate_pct=0.05,
+                      policy=policy)
     li.run(4)
     tops = []
     for ga in li.islands:
-        idx = ga.island.topk(li.k, True).long()
+        idx = ga.island.topk(li.k, True).long() if policy == "topk" else stripe_best(ga.scores, li.k)
         tops.append(ga.rows.clone()[idx])
     li.migrate()
     assert li.migrations == 1
