@@ -67,6 +67,7 @@ def lib():
     L.pga_load.argtypes = [vp, vp, C.c_char_p]
     L.pga_set_objective_source.argtypes = [vp, vp, C.c_char_p, C.c_char_p, C.POINTER(C.c_float), C.c_size_t]
     L.pga_run_until.argtypes = [vp, C.c_uint, C.c_float, C.c_uint]
+    L.pga_set_migration_policy.argtypes = [vp, vp, C.c_int]
     L.pga_run_islands_until.argtypes = [vp, C.c_uint, C.c_uint, C.c_float, C.c_float]
     L.pga_set_stats_history.argtypes = [vp, vp, C.c_int]
     L.pga_get_stats_history.restype = C.c_long
@@ -223,6 +224,29 @@ def test_run_islands_until_target(lib):
     g = lib.pga_run_islands_until(p, 400, 10, 0.05, 64.0)
     assert 0 < g < 400 and g % 10 == 0
     assert max(lib.pga_best_score(p, q) for q in pops) == 64.0
+    lib.pga_deinit(p)
+
+
+@pytest.mark.parametrize("policy", [0, 1])  # PGA_MIGRATE_TOPK, PGA_MIGRATE_STRIPE
+def test_migrate_between_policies(lib, policy):
+    """Both policies move the source's best into the destination and replace
+    only worse individuals: the destination's best becomes the source's, its
+    score multiset changes by exactly k entries."""
+    p = new(lib, seed=12)
+    a, b = onemax_pop(lib, p, S=400), onemax_pop(lib, p, S=400)
+    for q in (a, b):
+        assert lib.pga_set_migration_policy(p, q, policy) == 0
+    lib.pga_run(p, 3)
+    sa, sb = (C.c_float * 400)(), (C.c_float * 400)()
+    lib.pga_get_scores(p, a, sa)
+    lib.pga_get_scores(p, b, sb)
+    before = sorted(sb)
+    lib.pga_migrate_between(p, a, b, 0.05)  # k = 20
+    lib.pga_get_scores(p, b, sb)
+    assert max(sb) == max(max(sa), before[-1])
+    gone = sum(1 for x, y in zip(sorted(sb), before) if x != y)
+    assert 0 < gone <= 20 and sum(sb) >= sum(before)
+    assert lib.pga_set_migration_policy(p, a, 7) == -1  # unknown policy refused
     lib.pga_deinit(p)
 
 
