@@ -836,8 +836,9 @@ int pga_run_islands_until(pga_t* p, unsigned n, unsigned m, float pct, float tar
   });
 }
 
-int pga_run_islands_multi(pga_t** solvers, int count, unsigned n, unsigned m, float pct) {
-  if (!solvers || count < 1) return -1;
+namespace {
+int run_multi(pga_t** solvers, int count, unsigned n, unsigned m, float pct, float target) {
+  if (!solvers || count < 1 || !solvers[0]) return -1;
   pga_t* p0 = solvers[0];
   return guard_r<int>(p0, -1, [&]() {
     std::vector<pga_t*> v(solvers, solvers + count);
@@ -848,9 +849,18 @@ int pga_run_islands_multi(pga_t** solvers, int count, unsigned n, unsigned m, fl
     if (p0->comm && p0->comm->size() > 1 && (!p0->comm->drives_all_ranks() || count != p0->comm->size()))
       throw std::invalid_argument("pga_run_islands_multi: pass every rank of an InitAll / loopback group");
     std::sort(v.begin(), v.end(), [](pga_t* a, pga_t* b) { return a->comm_rank < b->comm_rank; });
-    (void)run_islands_until(v, n, m, pct, NAN);
-    return 0;
+    return (int)run_islands_until(v, n, m, pct, target);
   });
+}
+}  // namespace
+
+int pga_run_islands_multi(pga_t** solvers, int count, unsigned n, unsigned m, float pct) {
+  return run_multi(solvers, count, n, m, pct, NAN) < 0 ? -1 : 0;
+}
+
+int pga_run_islands_multi_until(pga_t** solvers, int count, unsigned n, unsigned m, float pct, float target) {
+  if (std::isnan(target)) return -1;
+  return run_multi(solvers, count, n, m, pct, target);
 }
 
 // -------------------------------------------------------------------- queries

@@ -158,6 +158,8 @@ int pga_run_islands_multi(pga_t **solvers, int n, unsigned generations, unsigned
  * every rank stops at the same generation).  Returns the generations run. */
 int pga_run_until(pga_t *p, unsigned generations, float target, unsigned check_every);
 int pga_run_islands_until(pga_t *p, unsigned generations, unsigned m, float pct, float target);
+/* the same over every rank of an InitAll / loopback group at once */
+int pga_run_islands_multi_until(pga_t **solvers, int n, unsigned generations, unsigned m, float pct, float target);
 
 #ifdef __cplusplus
 }

@@ -57,6 +57,7 @@ def lib():
     L.pga_comm_init_loopback.argtypes = [C.POINTER(vp), C.c_int]
     L.pga_comm_init_local.argtypes = [C.POINTER(vp), C.c_int]
     L.pga_run_islands_multi.argtypes = [C.POINTER(vp), C.c_int, C.c_uint, C.c_uint, C.c_float]
+    L.pga_run_islands_multi_until.argtypes = [C.POINTER(vp), C.c_int, C.c_uint, C.c_uint, C.c_float, C.c_float]
     L.pga_comm_set_topology.argtypes = [vp, C.c_int]
     L.pga_comm_set_timeout.argtypes = [vp, C.c_double]
     L.pga_comm_set_validation.argtypes = [vp, C.c_int]
@@ -120,6 +121,24 @@ def test_ring_delivers_the_best(lib):
     score, rank = C.c_float(), C.c_int()
     assert lib.pga_comm_best(solvers[0], C.byref(score), C.byref(rank)) == 0
     assert score.value == max(lib.pga_best_score(p, q) for p, q in zip(solvers, pops))
+    for p in solvers:
+        lib.pga_deinit(p)
+
+
+def test_multi_rank_target_stop(lib):
+    """pga_run_islands_multi_until: every rank stops at the same check point,
+    the first at which the best over all ranks reaches the target (all-gather
+    over the communicator)."""
+    solvers, pops, arr = make_group(lib, 3, seed=5)
+    assert lib.pga_comm_init_loopback(arr, 3) == 0
+    lib.pga_run(solvers[0], 5)  # rank 0 ahead: its best decides the first call
+    target = lib.pga_best_score(solvers[0], pops[0])
+    assert target < LEN
+    assert lib.pga_run_islands_multi_until(arr, 3, 500, 10, 0.05, target) == 0  # already reached
+    g = lib.pga_run_islands_multi_until(arr, 3, 500, 10, 0.05, float(LEN))
+    assert 0 < g < 500 and g % 10 == 0, g
+    assert max(lib.pga_best_score(p, q) for p, q in zip(solvers, pops)) == LEN
+    assert len({lib.pga_generation(q) for q in pops[1:]}) == 1  # ranks stopped together
     for p in solvers:
         lib.pga_deinit(p)
 
