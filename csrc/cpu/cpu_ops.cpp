@@ -153,9 +153,11 @@ uint32_t binary_run(int mode, const GenArgs& a, unsigned long long* best_parts) 
   uint32_t elite0 = 0;
   if (gen && a.n_elite > 0 && a.elite_idx == nullptr) elite0 = (uint32_t)best_index(reduce_best(a.best_cur, a.n_best_cur));
 
+  std::vector<unsigned long long> bests(cpu_threads(), 0ull);
+  parallel_for(a.S, 64, [&](uint64_t c_begin, uint64_t c_end, unsigned slot) {
   unsigned long long best = 0;
   std::vector<uint32_t> seg((size_t)GS * 4), flips;
-  for (uint64_t child = 0; child < a.S; ++child) {
+  for (uint64_t child = c_begin; child < c_end; ++child) {
     float score = 0.f;
     {
       // elitism: child = copy of the elite row, re-evaluated like every child
@@ -297,6 +299,9 @@ uint32_t binary_run(int mode, const GenArgs& a, unsigned long long* best_parts) 
       best = std::max(best, pack_best(score, child));
     }
   }
+  bests[slot] = best;
+  });
+  const unsigned long long best = *std::max_element(bests.begin(), bests.end());
   if (evaluates && best_parts) best_parts[0] = best;
   return 1;
 }

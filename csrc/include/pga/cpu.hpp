@@ -9,10 +9,18 @@
 // "CPU reference path" config of BASELINE.json.
 #pragma once
 
+#include <functional>
+
 #include "pga/core.hpp"
 
 namespace pga {
 namespace cpu {
+
+// worker pool of the CPU backend (parallel.cpp): fn(begin, end, slot) over
+// contiguous ranges of [0, n), slot < cpu_threads(); serial when n < 2 grains
+// or when another generation holds the pool
+unsigned cpu_threads();
+void parallel_for(uint64_t n, uint64_t grain, const std::function<void(uint64_t, uint64_t, unsigned)>& fn);
 
 // returns number of best parts written (always 1)
 uint32_t encoding_run(int mode, const GenArgs& a, unsigned long long* best_parts);

@@ -21,7 +21,7 @@ for s in csrc/kernels/binary.hip csrc/kernels/real.hip csrc/kernels/perm.hip csr
   [ $o -nt $s ] && [ $o -nt $HDR ] || echo "$HIPCC --offload-arch=gfx950 $COMMON -Xarch_host -fsanitize=address -Xarch_host -fsanitize=undefined -Xarch_host -fno-omit-frame-pointer -c $s -o $o"
 done > $O/cmds.txt
 for s in csrc/engine/island.cpp csrc/engine/trace.cpp csrc/engine/jit.cpp csrc/cpu/cpu_ops.cpp csrc/cpu/cpu_real.cpp \
-         csrc/cpu/cpu_perm.cpp csrc/capi/pga_capi.cpp csrc/capi/comm_rccl.cpp; do
+         csrc/cpu/cpu_perm.cpp csrc/cpu/parallel.cpp csrc/capi/pga_capi.cpp csrc/capi/comm_rccl.cpp; do
   o=$O/$(basename $s .cpp).o; objs+=($o)
   [ $o -nt $s ] && [ $o -nt $HDR ] || echo "$HIPCC -x c++ -D__HIP_PLATFORM_AMD__=1 -I/opt/rocm/include $COMMON $SAN -fno-gpu-sanitize -Wno-unused-command-line-argument -c $s -o $o"
 done >> $O/cmds.txt
