@@ -4,8 +4,9 @@
 // ranges over persistent worker threads and stays bit-identical to the serial
 // loop; the packed best is a max, so its combination order is irrelevant.
 //
-// PGA_CPU_THREADS=N runs the CPU backend on N threads (default 1: the hosts
-// this was measured on share their cores, see docs/ARCHITECTURE.md §9).
+// PGA_CPU_THREADS=N sets the thread count; default min(8, CPUs in the affinity
+// mask).  OneMax-64 pop 1024 on the MI355X host: 11.5k gens/s on 1 thread,
+// 19.9k on 4, 24.3k on 8, 13.2k on 16 (wake-up cost outgrows the work).
 #include <algorithm>
 #include <atomic>
 #include <condition_variable>
@@ -14,6 +15,7 @@
 #include <thread>
 #include <vector>
 
+#include <sched.h>
 #include <unistd.h>
 
 #include "pga/cpu.hpp"
@@ -86,7 +88,11 @@ unsigned configured_threads() {
     const long v = std::strtol(e, nullptr, 10);
     if (v >= 1) return (unsigned)std::min<long>(v, 256);
   }
-  return 1;
+  cpu_set_t set;
+  unsigned n = 0;
+  if (sched_getaffinity(0, sizeof(set), &set) == 0) n = (unsigned)CPU_COUNT(&set);
+  if (n == 0) n = std::thread::hardware_concurrency();
+  return std::max(1u, std::min(n, 8u));
 }
 
 // one pool per process: a child forked from a process that had started the
