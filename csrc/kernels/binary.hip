@@ -427,30 +427,42 @@ __global__ __launch_bounds__(kBlock) void binary_kernel(GenArgs a, unsigned long
 // A wave owns a contiguous range of children and breeds NG = 64/GS of them per
 // STEP (group g: child begin + t*NG + g).  Steps come in BATCHES of GS steps =
 // 64 children, and the per-child work that does not touch the genome runs
-// transposed, one lane per child of a whole batch:
-//   ISSUE    one Philox block = the 4 tournament contestants, 4 key loads
-//   RESOLVE  (next step) compare -> parents; the misc block (crossover test,
-//            cut points, mutation count K); the sparse bit-flip positions
-//            (one more block, first K distinct by a pairwise check); write a
-//            32-byte child RECORD to the wave's LDS ring (2 batches)
-// so a child costs 3/64 of a Philox per lane for its child-level words
-// instead of one, its tournament 4 load instructions per 64 children instead
-// of per 8, and mutation is a short loop over the record's positions instead
-// of a divergent geometric search in every chunk.  Breeding a step: XO mask
-// Philox (one block per chunk), mix, flips, popcount, group butterfly, stores.
+// transposed, one lane per child of a whole batch.  The range is cut into
+// SEGMENTS of up to kSegBatches batches, each in two phases:
+//   TOURNAMENTS  every batch of the segment at once: one Philox block = the 4
+//                contestants of a child, all 4 x kSegBatches key loads in
+//                flight together, compare -> (parent A, parent B) in LDS
+//   BREED        per batch, RESOLVE: the misc block (crossover test, cut
+//                points, mutation count K) and the sparse bit-flip positions
+//                (one more block, first K distinct by a pairwise check) -> a
+//                32-byte child RECORD in the wave's LDS ring (2 batches);
+//                per step: XO mask Philox (one block per chunk), mix, flips,
+//                popcount, group butterfly, stores.
+// Why two phases: the EA (L2 -> fabric) traffic is the bound (PMC: ~530 MB
+// per generation at 1M x 1024 bits, ~5.7 TB/s).  Tournament keys are a 2 MB
+// array read at random; interleaved with the row gathers, ~1/4 of the key
+// reads missed the XCD's 4 MB L2 (a 128-B line each, ~1/4 of all EA bytes).
+// At kernel start every wave is in its tournament phase, so the L2 holds
+// little but key lines and the key reads cost ~2 MB of fabric per XCD.
+// A child costs 3/64 of a Philox per lane for its child-level words, and
+// mutation is a short loop over the record's positions instead of a
+// divergent geometric search in every chunk.
 //
-// Pipeline (per step t): RESOLVE batch (t+1)/GS if (t+1)%GS==0; ISSUE batch
-// (t+2)/GS if (t+2)%GS==0; load the parent rows of step t+1; breed step t
-// from the rows loaded one step earlier.  Every load is issued on EVERY step
-// (the 4 key loads of a non-ISSUE step read one dummy line): s_waitcnt
-// vmcnt retires in order and hipcc assumes the fewest outstanding loads over
-// all paths, so a conditionally issued load would make the next wait drain it.
+// Breed pipeline (per step t): RESOLVE batch (t+1)/GS if (t+1)%GS==0; load
+// the parent rows of step t+1; breed step t from the rows loaded one step
+// earlier.  Every vector memory operation is unconditional (s_waitcnt vmcnt
+// retires in order and hipcc assumes the fewest outstanding loads over all
+// paths, so a conditionally issued load would make the next wait drain it).
 // ---------------------------------------------------------------------------
 
 constexpr uint32_t kTpMaxElite = 64;  // elites the fast kernel routes through its records
+constexpr uint32_t kSegBatches = 4;   // batches (x 64 children) per tournament segment
 
+// 5 waves/SIMD: 4, 5 and 6 measured alike for the breed phase alone (the
+// fabric, not occupancy, is the bound); 5 gives the tournament phase its
+// 16 key loads in flight without spilling (6: 23 spilled VGPRs, +8%)
 #ifndef PGA_TP_WAVES
-#define PGA_TP_WAVES 6
+#define PGA_TP_WAVES 5
 #endif
 
 __device__ __forceinline__ uint32_t pos16(uint4 r1, uint32_t k) {  // k-th packed 16-bit position
@@ -466,8 +478,8 @@ __global__ __launch_bounds__(kBlock, OBJ == kObjKnapMfma ? 4 : PGA_TP_WAVES) voi
   constexpr bool EVALS = OBJ != OBJ_NONE;
   // integer objectives tournament on their exact u16 keys (L2-resident)
   constexpr bool KEY = OBJ == OBJ_ONEMAX || OBJ == OBJ_LEADING_ONES || OBJ == OBJ_TRAP;
-  __shared__ uint4 lds_rec[NW][2][64][2];  // per wave: 2 batches x 64 records x 32 B
-  __shared__ uint4 lds_idx[NW][64];        // contestants of the tournament in flight
+  __shared__ uint4 lds_rec[NW][2][64][2];           // per wave: 2 batches x 64 records x 32 B
+  __shared__ uint2 lds_par[NW][kSegBatches * 64];  // per wave: the segment's (parent A, parent B)
   __shared__ uint32_t lds_thr[kMutCap];
   __shared__ uint32_t lds_el[kTpMaxElite];  // elite sources
   __shared__ unsigned long long lds_red[NW];
@@ -499,13 +511,12 @@ __global__ __launch_bounds__(kBlock, OBJ == kObjKnapMfma ? 4 : PGA_TP_WAVES) voi
 #define ELEM(T, base, i) (*(T*)((char*)(base) + (uint32_t)(i) * (uint32_t)sizeof(T)))
 #define ROW(base, row, ch) (*(uint4*)((char*)(base) + ((uint32_t)(row) * rb + (uint32_t)(ch) * 16u)))
 
-  // this wave's children [begin, end): contiguous, a multiple of NG long
+  // this wave's children [wbegin, wend): contiguous, a multiple of NG long
   const uint64_t W = (uint64_t)gridDim.x * NW, w = (uint64_t)blockIdx.x * NW + wid;
   uint64_t per = (S + W - 1) / W;
   per = (per + NG - 1) / NG * NG;
-  const uint32_t begin = (uint32_t)(w * per < S ? w * per : S);
-  const uint32_t end = (uint32_t)(begin + per < S ? begin + per : S);
-  const uint32_t nsteps = (end - begin + NG - 1) / NG;
+  const uint32_t wbegin = (uint32_t)(w * per < S ? w * per : S);
+  const uint32_t wend = (uint32_t)(wbegin + per < S ? wbegin + per : S);
 
   // elite sources of children [0, n_elite) (n_elite <= kTpMaxElite), for the
   // blocks that hold any of them
@@ -526,55 +537,61 @@ __global__ __launch_bounds__(kBlock, OBJ == kObjKnapMfma ? 4 : PGA_TP_WAVES) voi
 
   unsigned long long my_best = 0;
   ScoreStats st;
-  if (nsteps > 0) {  // wave-uniform
-    uint4(*rec)[64][2] = lds_rec[wid];
-    // keys of the tournament in flight (lane = child `lane` of the batch)
-    float t0 = 0.f, t1 = 0.f, t2 = 0.f, t3 = 0.f;
+  uint4(*rec)[64][2] = lds_rec[wid];
+  uint2* par = lds_par[wid];
+  static_assert(sizeof(lds_rec[0]) >= kSegBatches * 64 * sizeof(uint4), "contestant staging");
+  for (uint32_t begin = wbegin; begin < wend; begin += kSegBatches * 64u) {  // wave-uniform
+    const uint32_t end = begin + kSegBatches * 64u < wend ? begin + kSegBatches * 64u : wend;
+    const uint32_t nsteps = (end - begin + NG - 1) / NG;
     const uint32_t nbatch = (end - begin + 63) / 64;
 
-    // ISSUE: contestants of batch B (lane = batch child) and their key loads.
-    // The 4 loads are issued on every step (line 0 when not a real issue).
-#define PGA_TP_ISSUE(B, real)                                                          \
-  {                                                                                    \
-    uint32_t j0 = 0, j1 = 0, j2 = 0, j3 = 0;                                           \
-    if (real) {                                                                        \
-      const uint32_t tc = begin + (B) * 64u + lane;                                    \
-      const uint32_t cc = tc < end ? tc : end - 1;                                     \
-      const u32x4 blk = draw<true>(a.key, ST_SEL, cc, 0);                              \
-      const uint4 ix = make_uint4(word_to_index(blk.x, S), word_to_index(blk.y, S),    \
-                                  word_to_index(blk.z, S), word_to_index(blk.w, S));   \
-      lds_idx[wid][lane] = ix;                                                         \
-      if (tourn) {                                                                     \
-        j0 = ix.x;                                                                     \
-        j1 = ix.y;                                                                     \
-        j2 = ix.z;                                                                     \
-        j3 = ix.w;                                                                     \
-      }                                                                                \
-    }                                                                                  \
-    if (KEY) {                                                                         \
-      t0 = (float)ELEM(const uint16_t, a.key_cur, j0);                                 \
-      t1 = (float)ELEM(const uint16_t, a.key_cur, j1);                                 \
-      t2 = (float)ELEM(const uint16_t, a.key_cur, j2);                                 \
-      t3 = (float)ELEM(const uint16_t, a.key_cur, j3);                                 \
-    } else {                                                                           \
-      t0 = ELEM(const float, a.score_cur, j0);                                         \
-      t1 = ELEM(const float, a.score_cur, j1);                                         \
-      t2 = ELEM(const float, a.score_cur, j2);                                         \
-      t3 = ELEM(const float, a.score_cur, j3);                                         \
-    }                                                                                  \
-  }
+    // TOURNAMENTS of the whole segment: all key loads in flight at once; the
+    // contestants wait in the record ring (free until the first RESOLVE)
+    {
+      uint4* ixs = &rec[0][0][0];  // [B * 64 + lane]: 4 x 64 x 16 B = the ring's 4 KiB
+      float k0[kSegBatches], k1[kSegBatches], k2[kSegBatches], k3[kSegBatches];
+#pragma unroll
+      for (uint32_t B = 0; B < kSegBatches; ++B) {
+        const uint32_t tc = begin + B * 64u + lane;
+        const uint32_t cc = tc < end ? tc : end - 1;
+        const u32x4 blk = draw<true>(a.key, ST_SEL, cc, 0);
+        const uint4 ix = make_uint4(word_to_index(blk.x, S), word_to_index(blk.y, S), word_to_index(blk.z, S),
+                                    word_to_index(blk.w, S));
+        ixs[B * 64u + lane] = ix;
+        const uint4 j = tourn ? ix : make_uint4(0, 0, 0, 0);
+        if (KEY) {
+          k0[B] = (float)ELEM(const uint16_t, a.key_cur, j.x);
+          k1[B] = (float)ELEM(const uint16_t, a.key_cur, j.y);
+          k2[B] = (float)ELEM(const uint16_t, a.key_cur, j.z);
+          k3[B] = (float)ELEM(const uint16_t, a.key_cur, j.w);
+        } else {
+          k0[B] = ELEM(const float, a.score_cur, j.x);
+          k1[B] = ELEM(const float, a.score_cur, j.y);
+          k2[B] = ELEM(const float, a.score_cur, j.z);
+          k3[B] = ELEM(const float, a.score_cur, j.w);
+        }
+        if (B + 1 >= nbatch) break;  // wave-uniform
+      }
+#pragma unroll
+      for (uint32_t B = 0; B < kSegBatches; ++B) {
+        const uint4 ix = ixs[B * 64u + lane];
+        uint32_t pa = ix.x, pb = ix.y;
+        if (tourn) {
+          pa = k0[B] < k1[B] ? ix.y : ix.x;
+          pb = k2[B] < k3[B] ? ix.w : ix.z;
+        }
+        par[B * 64u + lane] = make_uint2(pa, pb);
+        if (B + 1 >= nbatch) break;
+      }
+    }
 
     // RESOLVE: parents, crossover plan and flip positions of batch B -> records
 #define PGA_TP_RESOLVE(B)                                                                                       \
   {                                                                                                             \
     const uint32_t tc = begin + (B) * 64u + lane;                                                               \
     const uint32_t cc = tc < end ? tc : end - 1;                                                                \
-    const uint4 ix = lds_idx[wid][lane];                                                                        \
-    uint32_t pa = ix.x, pb = ix.y;                                                                              \
-    if (tourn) {                                                                                                \
-      pa = t0 < t1 ? ix.y : ix.x;                                                                               \
-      pb = t2 < t3 ? ix.w : ix.z;                                                                               \
-    }                                                                                                           \
+    const uint2 pp = par[(B) * 64u + lane];                                                                     \
+    uint32_t pa = pp.x, pb = pp.y;                                                                              \
     const u32x4 misc = bin_misc<true>(a.key, cc);                                                               \
     const bool elite = tc < a.n_elite;                                                                          \
     const bool xo = !elite && xo_on && do_crossover(a, misc.x);                                                 \
@@ -619,10 +636,8 @@ __global__ __launch_bounds__(kBlock, OBJ == kObjKnapMfma ? 4 : PGA_TP_WAVES) voi
     r[lane][1] = P;                                                                                             \
   }
 
-    // prologue: batch 0 resolved (and batch 1 issued when GS == 1), rows of step 0 in flight
-    PGA_TP_ISSUE(0u, true)
+    // prologue: batch 0 resolved, rows of step 0 in flight
     PGA_TP_RESOLVE(0u)
-    if (GS == 1) PGA_TP_ISSUE(1u, 1u < nbatch)
     uint4 A0, B0, A1, B1;
     {
       const uint4 r = rec[0][g][0];
@@ -636,10 +651,6 @@ __global__ __launch_bounds__(kBlock, OBJ == kObjKnapMfma ? 4 : PGA_TP_WAVES) voi
   {                                                                                                         \
     const uint32_t b = (t) / GS, i = (t) & (GS - 1);                                                        \
     if ((((t) + 1) & (GS - 1)) == 0u && b + 1 < nbatch) PGA_TP_RESOLVE(b + 1)                               \
-    {                                                                                                       \
-      const uint32_t bi = ((t) + 2) / GS;                                                                   \
-      PGA_TP_ISSUE(bi, (((t) + 2) & (GS - 1)) == 0u && bi < nbatch)                                         \
-    }                                                                                                       \
     {                                                                                                       \
       /* parent rows of step t+1 (the last step re-reads its own) */                                        \
       const uint32_t tn = (t) + 1 < nsteps ? (t) + 1 : (t);                                                 \
@@ -700,7 +711,6 @@ __global__ __launch_bounds__(kBlock, OBJ == kObjKnapMfma ? 4 : PGA_TP_WAVES) voi
       PGA_TP_STEP(t + 1, A1, B1, A0, B0)
     }
     if (t < nsteps) PGA_TP_STEP(t, A0, B0, A1, B1)
-#undef PGA_TP_ISSUE
 #undef PGA_TP_RESOLVE
 #undef PGA_TP_STEP
   }

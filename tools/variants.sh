@@ -1,0 +1,32 @@
+#!/bin/bash
+# Build gen_bench (bench/gen_bench.cpp) against compile-time variants of one
+# kernel source, for interleaved A/B runs on the GPU (tools/ab.sh):
+#
+#   tools/variants.sh csrc/kernels/binary.hip "pd1:-DPGA_TP_PD=1" "pd2:-DPGA_TP_PD=2 -DPGA_TP_PD_WAVES=5"
+#   -> build/variants/gen_<name>
+#
+# Needs the regular build first (tools/build.py): the other kernels, the
+# engine and the CPU backend link from build/obj.  Nothing here is shipped.
+set -e
+cd "$(dirname "$0")/.."
+src=$1; shift
+base=$(basename "$src" .hip)
+O=build/obj
+mkdir -p build/variants
+flags="-O3 -std=c++17 -Icsrc/include -Iinclude -x hip --offload-arch=gfx950 -munsafe-fp-atomics -ffp-contract=fast"
+/opt/rocm/bin/hipcc $flags -c bench/gen_bench.cpp -o build/variants/gen_bench.o
+others=""
+for k in binary perm qubo real util compat; do
+  [ "$k" = "$base" ] || others="$others $O/csrc_kernels_$k.k.o"
+done
+for spec in "$@"; do
+  name=${spec%%:*}
+  defs=${spec#*:}
+  (
+    /opt/rocm/bin/hipcc $flags $defs -c "$src" -o "build/variants/${base}_$name.o" &&
+    /opt/rocm/bin/hipcc --offload-arch=gfx950 -o "build/variants/gen_$name" build/variants/gen_bench.o \
+      "build/variants/${base}_$name.o" $others $O/csrc_engine_*.h.o $O/csrc_cpu_*.h.o -lpthread -ldl
+  ) &
+done
+wait
+ls build/variants/gen_*
