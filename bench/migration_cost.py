@@ -111,9 +111,11 @@ def rccl_self_overhead(S=1 << 20, every=10, gens=500):
     torch.cuda.set_device(0)
     dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
     out = {}
-    for name, ev, side in (("none", 0, True), ("rccl_self", every, True), ("rccl_self_noside", every, False)):
+    arms = (("none", 0, True, True), ("rccl_self", every, True, True), ("rccl_self_noside", every, False, True),
+            ("rccl_self_serial", every, False, False))
+    for name, ev, side, overlap in arms:
         ga = pga.GeneticAlgorithm(pga.models.OneMax(1024), S, seed=1, device="cuda:0", elitism=1)
-        m = IslandModel(ga, migrate_every=ev, migrate_pct=0.01, side_stream=side)
+        m = IslandModel(ga, migrate_every=ev, migrate_pct=0.01, side_stream=side, overlap=overlap)
         m.world, m.rank = 2, 0
         m._peers = lambda: (0, 0)
         m.connect() if ev else None
@@ -127,7 +129,7 @@ def rccl_self_overhead(S=1 << 20, every=10, gens=500):
         b.synchronize()
         out["us_per_gen_" + name] = a.elapsed_time(b) / gens * 1e3
         out["migrations_" + name] = m.migrations
-    for v in ("rccl_self", "rccl_self_noside"):
+    for v in ("rccl_self", "rccl_self_noside", "rccl_self_serial"):
         out["overhead_pct_" + v] = 100.0 * (out["us_per_gen_" + v] / out["us_per_gen_none"] - 1.0)
     out.update(pop=S, every=every)
     emit(out)

@@ -73,6 +73,30 @@ def test_gpu_bitexact(xo, n, S, prob, elitism):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("xo", ["ox", "pmx"])
+@pytest.mark.parametrize("n", [64, 256])
+@pytest.mark.parametrize("shape", ["asymmetric", "nonzero_diagonal"])
+def test_gpu_bitexact_general_matrix(xo, n, shape):
+    """Distance matrices that are not symmetric, or have a non-zero diagonal
+    (the closing edge and clamped ids read it): bit-exact vs the CPU."""
+    g0 = torch.Generator().manual_seed(n)
+    d = torch.rand(n, n, generator=g0) * 10
+    if shape == "nonzero_diagonal":
+        d = (d + d.T) / 2
+    else:
+        d.fill_diagonal_(0)
+    p = M.TSP(d)
+    kw = dict(seed=8, crossover=xo, mutation="swap", mutation_rate=0.4, elitism=1)
+    g = pga.GeneticAlgorithm(p, 1024, device="cuda:0", **kw)
+    c = pga.GeneticAlgorithm(p, 1024, device="cpu", **kw)
+    g.run(3)
+    c.run(3)
+    torch.cuda.synchronize()
+    assert torch.equal(g.rows.cpu(), c.rows)
+    assert torch.equal(g.scores.cpu(), c.scores)
+
+
+@pytest.mark.gpu
 def test_gpu_tsp256_pop256k():
     """BASELINE config 5 shape on one GPU: TSP-256, pop = 256K, OX."""
     p = M.TSPEuclidean.random(256, seed=9)
