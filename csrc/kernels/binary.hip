@@ -23,6 +23,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <type_traits>
 
 #include "pga/device.hpp"
 #include "pga/ops.hpp"
@@ -549,7 +550,11 @@ __global__ __launch_bounds__(kBlock, OBJ == kObjKnapMfma ? 4 : PGA_TP_WAVES) voi
     // contestants wait in the record ring (free until the first RESOLVE)
     {
       uint4* ixs = &rec[0][0][0];  // [B * 64 + lane]: 4 x 64 x 16 B = the ring's 4 KiB
-      float k0[kSegBatches], k1[kSegBatches], k2[kSegBatches], k3[kSegBatches];
+      // raw keys (u16 zero-extended, or f32 scores), compared only after every
+      // load of the segment is issued: a conversion here would make hipcc wait
+      // for each batch's loads before issuing the next batch's
+      using KT = typename std::conditional<KEY, uint32_t, float>::type;
+      KT k0[kSegBatches], k1[kSegBatches], k2[kSegBatches], k3[kSegBatches];
 #pragma unroll
       for (uint32_t B = 0; B < kSegBatches; ++B) {
         const uint32_t tc = begin + B * 64u + lane;
@@ -559,18 +564,20 @@ __global__ __launch_bounds__(kBlock, OBJ == kObjKnapMfma ? 4 : PGA_TP_WAVES) voi
                                     word_to_index(blk.w, S));
         ixs[B * 64u + lane] = ix;
         const uint4 j = tourn ? ix : make_uint4(0, 0, 0, 0);
-        if (KEY) {
-          k0[B] = (float)ELEM(const uint16_t, a.key_cur, j.x);
-          k1[B] = (float)ELEM(const uint16_t, a.key_cur, j.y);
-          k2[B] = (float)ELEM(const uint16_t, a.key_cur, j.z);
-          k3[B] = (float)ELEM(const uint16_t, a.key_cur, j.w);
+        if constexpr (KEY) {
+          k0[B] = ELEM(const uint16_t, a.key_cur, j.x);
+          k1[B] = ELEM(const uint16_t, a.key_cur, j.y);
+          k2[B] = ELEM(const uint16_t, a.key_cur, j.z);
+          k3[B] = ELEM(const uint16_t, a.key_cur, j.w);
         } else {
           k0[B] = ELEM(const float, a.score_cur, j.x);
           k1[B] = ELEM(const float, a.score_cur, j.y);
           k2[B] = ELEM(const float, a.score_cur, j.z);
           k3[B] = ELEM(const float, a.score_cur, j.w);
         }
-        if (B + 1 >= nbatch) break;  // wave-uniform
+        // no early exit past the segment's last batch: straight-line code keeps
+        // every key in a register (a wave-uniform break spilled the last four);
+        // the extra batches draw clamped children and are never resolved
       }
 #pragma unroll
       for (uint32_t B = 0; B < kSegBatches; ++B) {
@@ -581,7 +588,6 @@ __global__ __launch_bounds__(kBlock, OBJ == kObjKnapMfma ? 4 : PGA_TP_WAVES) voi
           pb = k2[B] < k3[B] ? ix.w : ix.z;
         }
         par[B * 64u + lane] = make_uint2(pa, pb);
-        if (B + 1 >= nbatch) break;
       }
     }
 
