@@ -17,7 +17,8 @@
 //   binary_kernel<GS,OBJ,MODE>   every mode / operator / genome length; one
 //                                child per group at a time
 //   binary_gen_tp<GS,OBJ,XO,KEY> the hot generation path (L <= 8192 bits,
-//                                tournament-2 or random selection), see below
+//                                tournament-2, linear ranking or random
+//                                selection), see below
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -433,6 +434,7 @@ __global__ __launch_bounds__(kBlock) void binary_kernel(GenArgs a, unsigned long
 //   TOURNAMENTS  every batch of the segment at once: one Philox block = the 4
 //                contestants of a child, all 4 x kSegBatches key loads in
 //                flight together, compare -> (parent A, parent B) in LDS
+//                (linear ranking: two rank picks, two rank-order loads)
 //   BREED        per batch, RESOLVE: the misc block (crossover test, cut
 //                points, mutation count K) and the sparse bit-flip positions
 //                (one more block, first K distinct by a pairwise check) -> a
@@ -497,7 +499,8 @@ __global__ __launch_bounds__(kBlock, OBJ == kObjKnapMfma ? 4 : PGA_TP_WAVES) voi
   const bool have = FULL || q < a.chunks, last = q == a.chunks - 1;
   const uint32_t qq = have ? q : 0u;
   const uint32_t clen = have ? chunk_len(L, q) : 0u;
-  const bool tourn = a.selection == SEL_TOURNAMENT;  // tour_k == 2 guaranteed by the launcher, else random
+  const bool tourn = a.selection == SEL_TOURNAMENT;  // tour_k == 2 guaranteed by the launcher
+  const bool rank = a.selection == SEL_RANK;         // else random
   const bool xo_on = a.crossover != XO_NONE;
   const bool range = a.crossover != XO_UNIFORM;  // ONE/TWO_POINT, or NONE (empty range)
   // DENSE: per-chunk geometric bit-flips; otherwise the record carries the
@@ -564,7 +567,13 @@ __global__ __launch_bounds__(kBlock, OBJ == kObjKnapMfma ? 4 : PGA_TP_WAVES) voi
                                     word_to_index(blk.w, S));
         ixs[B * 64u + lane] = ix;
         const uint4 j = tourn ? ix : make_uint4(0, 0, 0, 0);
-        if constexpr (KEY) {
+        if (rank) {  // wave-uniform: linear ranking, the two parents straight from the rank order
+          const u32x4 b1 = draw<true>(a.key, ST_SEL, cc, 1);
+          const uint32_t ra = rank_pick(blk.x, blk.y, blk.z, S, a.rank_thresh);
+          const uint32_t rb = rank_pick(blk.w, b1.x, b1.y, S, a.rank_thresh);
+          k0[B] = __builtin_bit_cast(KT, ELEM(const uint32_t, a.rank_order, ra));
+          k1[B] = __builtin_bit_cast(KT, ELEM(const uint32_t, a.rank_order, rb));
+        } else if constexpr (KEY) {
           k0[B] = ELEM(const uint16_t, a.key_cur, j.x);
           k1[B] = ELEM(const uint16_t, a.key_cur, j.y);
           k2[B] = ELEM(const uint16_t, a.key_cur, j.z);
@@ -586,6 +595,9 @@ __global__ __launch_bounds__(kBlock, OBJ == kObjKnapMfma ? 4 : PGA_TP_WAVES) voi
         if (tourn) {
           pa = k0[B] < k1[B] ? ix.y : ix.x;
           pb = k2[B] < k3[B] ? ix.w : ix.z;
+        } else if (rank) {
+          pa = __builtin_bit_cast(uint32_t, k0[B]);
+          pb = __builtin_bit_cast(uint32_t, k1[B]);
         }
         par[B * 64u + lane] = make_uint2(pa, pb);
       }
@@ -740,7 +752,8 @@ uint32_t launch_mode(int mode, const GenArgs& a, unsigned long long* parts, hipS
   switch (mode) {
     case MODE_GEN: {
       const bool fast = a.chunks <= (uint32_t)GS &&
-                        ((a.selection == SEL_TOURNAMENT && a.tour_k == 2) || a.selection == SEL_RANDOM) &&
+                        ((a.selection == SEL_TOURNAMENT && a.tour_k == 2) || a.selection == SEL_RANDOM ||
+                         (a.selection == SEL_RANK && a.rank_order != nullptr)) &&
                         !(a.n_elite > 1 && a.elite_idx == nullptr) && !force_generic_kernels();
       constexpr bool INT_OBJ = OBJ == OBJ_ONEMAX || OBJ == OBJ_LEADING_ONES || OBJ == OBJ_TRAP;
       // 32-bit offsets: the (S + kRowPad)-row buffers must stay below 4 GiB

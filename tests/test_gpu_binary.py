@@ -210,6 +210,24 @@ def test_rank_selection_bitexact(sp):
     same(g, c)
 
 
+@pytest.mark.parametrize("prob", ["onemax1024", "onemax100", "knapsack_real"])
+@pytest.mark.parametrize("elitism", [1, 3])
+def test_rank_selection_fast_kernel_bitexact(prob, elitism):
+    """Linear ranking in the fast kernel's first phase (two rank picks, two
+    rank-order loads per child): u16-key objectives at full and partial lane
+    groups, and an f32-score objective (non-integer knapsack), bit-exact vs
+    the CPU backend."""
+    g0 = torch.Generator().manual_seed(3)
+    problem = {"onemax1024": lambda: pga.models.OneMax(1024), "onemax100": lambda: pga.models.OneMax(100),
+               "knapsack_real": lambda: pga.models.Knapsack01(torch.rand(256, generator=g0) * 10,
+                                                            torch.rand(256, generator=g0) * 10, 300.0)}[prob]()
+    g, c = pair(problem, 3000, selection="rank", rank_pressure=1.7, elitism=elitism)
+    for _ in range(3):
+        g.run(1)
+        c.run(1)
+        same(g, c)
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("S", [1 << 20, (1 << 22) + 12345])
 def test_gpu_topk_selection_order_many_blocks(S):
