@@ -84,12 +84,15 @@ def make(name: str):
         return M.Knapsack01.random(1024, seed=1), 1 << 20, None, dict(elitism=1), 200
     if name == "onemax1024_rank":
         return M.OneMax(1024), 1 << 20, None, dict(elitism=1, selection="rank", rank_pressure=1.5), 100
+    if name == "onemax1024_roulette_2pt":
+        # BASELINE north-star operator set: roulette selection, two-point crossover, bit-flip, elitism
+        return M.OneMax(1024), 1 << 20, None, dict(elitism=1, selection="roulette", crossover="two_point"), 100
     raise KeyError(name)
 
 
 NAMES = ["onemax64_cpu", "onemax1024", "rastrigin30", "rastrigin30_rot", "tsp256_ox", "tsp256_pmx", "e1_sum100_refops",
          "tsp256_euc_ox", "tsp256_euc_pmx", "e2_knap_refops", "onemax64_gpu", "onemax1024_jit", "maxcut512_qubo",
-         "qubo1024", "onemax1024_rank", "knapsack1024"]
+         "qubo1024", "onemax1024_rank", "knapsack1024", "onemax1024_roulette_2pt"]
 
 
 def qubo_padded(L: int) -> int:

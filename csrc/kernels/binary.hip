@@ -17,8 +17,8 @@
 //   binary_kernel<GS,OBJ,MODE>   every mode / operator / genome length; one
 //                                child per group at a time
 //   binary_gen_tp<GS,OBJ,XO,KEY> the hot generation path (L <= 8192 bits,
-//                                tournament-2, linear ranking or random
-//                                selection), see below
+//                                tournament-2, roulette, linear ranking or
+//                                random selection), see below
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -500,7 +500,8 @@ __global__ __launch_bounds__(kBlock, OBJ == kObjKnapMfma ? 4 : PGA_TP_WAVES) voi
   const uint32_t qq = have ? q : 0u;
   const uint32_t clen = have ? chunk_len(L, q) : 0u;
   const bool tourn = a.selection == SEL_TOURNAMENT;  // tour_k == 2 guaranteed by the launcher
-  const bool rank = a.selection == SEL_RANK;         // else random
+  const bool rank = a.selection == SEL_RANK;
+  const bool roul = a.selection == SEL_ROULETTE;     // else random
   const bool xo_on = a.crossover != XO_NONE;
   const bool range = a.crossover != XO_UNIFORM;  // ONE/TWO_POINT, or NONE (empty range)
   // DENSE: per-chunk geometric bit-flips; otherwise the record carries the
@@ -567,7 +568,10 @@ __global__ __launch_bounds__(kBlock, OBJ == kObjKnapMfma ? 4 : PGA_TP_WAVES) voi
                                     word_to_index(blk.w, S));
         ixs[B * 64u + lane] = ix;
         const uint4 j = tourn ? ix : make_uint4(0, 0, 0, 0);
-        if (rank) {  // wave-uniform: linear ranking, the two parents straight from the rank order
+        if (roul) {  // wave-uniform: the two selection words, searched below for every batch at once
+          k0[B] = __builtin_bit_cast(KT, blk.x);
+          k1[B] = __builtin_bit_cast(KT, blk.y);
+        } else if (rank) {  // wave-uniform: linear ranking, the two parents straight from the rank order
           const u32x4 b1 = draw<true>(a.key, ST_SEL, cc, 1);
           const uint32_t ra = rank_pick(blk.x, blk.y, blk.z, S, a.rank_thresh);
           const uint32_t rb = rank_pick(blk.w, b1.x, b1.y, S, a.rank_thresh);
@@ -588,6 +592,40 @@ __global__ __launch_bounds__(kBlock, OBJ == kObjKnapMfma ? 4 : PGA_TP_WAVES) voi
         // every key in a register (a wave-uniform break spilled the last four);
         // the extra batches draw clamped children and are never resolved
       }
+      if (roul) {
+        // fitness-proportional: the 2 x kSegBatches binary searches of
+        // roulette_pick (smallest i with cumfit[i] >= u * total) advance in
+        // lock step, one load each per halving, ceil(log2 S) halvings
+        constexpr uint32_t NS = 2 * kSegBatches;
+        const float total = a.cumfit[S - 1];
+        uint32_t lo[NS], hi[NS];
+        float tg[NS];
+#pragma unroll
+        for (uint32_t i = 0; i < NS; ++i) {
+          const uint32_t w = __builtin_bit_cast(uint32_t, (i & 1u) ? k1[i >> 1] : k0[i >> 1]);
+          tg[i] = word_to_unit(w) * total;
+          lo[i] = total > 0.f ? 0u : word_to_index(w, S);
+          hi[i] = total > 0.f ? S - 1 : lo[i];
+        }
+        for (uint32_t n = S; n > 1; n = (n + 1) >> 1) {  // wave-uniform trip count
+          float v[NS];
+#pragma unroll
+          for (uint32_t i = 0; i < NS; ++i) v[i] = ELEM(const float, a.cumfit, (lo[i] + hi[i]) >> 1);
+#pragma unroll
+          for (uint32_t i = 0; i < NS; ++i) {
+            const uint32_t mid = (lo[i] + hi[i]) >> 1;
+            if (lo[i] < hi[i]) {
+              if (v[i] < tg[i]) lo[i] = mid + 1;
+              else hi[i] = mid;
+            }
+          }
+        }
+#pragma unroll
+        for (uint32_t B = 0; B < kSegBatches; ++B) {
+          k0[B] = __builtin_bit_cast(KT, lo[2 * B]);
+          k1[B] = __builtin_bit_cast(KT, lo[2 * B + 1]);
+        }
+      }
 #pragma unroll
       for (uint32_t B = 0; B < kSegBatches; ++B) {
         const uint4 ix = ixs[B * 64u + lane];
@@ -595,7 +633,7 @@ __global__ __launch_bounds__(kBlock, OBJ == kObjKnapMfma ? 4 : PGA_TP_WAVES) voi
         if (tourn) {
           pa = k0[B] < k1[B] ? ix.y : ix.x;
           pb = k2[B] < k3[B] ? ix.w : ix.z;
-        } else if (rank) {
+        } else if (rank || roul) {
           pa = __builtin_bit_cast(uint32_t, k0[B]);
           pb = __builtin_bit_cast(uint32_t, k1[B]);
         }
@@ -753,7 +791,8 @@ uint32_t launch_mode(int mode, const GenArgs& a, unsigned long long* parts, hipS
     case MODE_GEN: {
       const bool fast = a.chunks <= (uint32_t)GS &&
                         ((a.selection == SEL_TOURNAMENT && a.tour_k == 2) || a.selection == SEL_RANDOM ||
-                         (a.selection == SEL_RANK && a.rank_order != nullptr)) &&
+                         (a.selection == SEL_RANK && a.rank_order != nullptr) ||
+                         (a.selection == SEL_ROULETTE && a.cumfit != nullptr)) &&
                         !(a.n_elite > 1 && a.elite_idx == nullptr) && !force_generic_kernels();
       constexpr bool INT_OBJ = OBJ == OBJ_ONEMAX || OBJ == OBJ_LEADING_ONES || OBJ == OBJ_TRAP;
       // 32-bit offsets: the (S + kRowPad)-row buffers must stay below 4 GiB

