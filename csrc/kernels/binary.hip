@@ -563,7 +563,8 @@ __global__ __launch_bounds__(kBlock, OBJ == kObjKnapMfma ? 4 : PGA_TP_WAVES) voi
       for (uint32_t B = 0; B < kSegBatches; ++B) {
         const uint32_t tc = begin + B * 64u + lane;
         const uint32_t cc = tc < end ? tc : end - 1;
-        const u32x4 blk = draw<true>(a.key, ST_SEL, cc, 0);
+        u32x4 blk{0u, 0u, 0u, 0u};
+        if (B < nbatch) blk = draw<true>(a.key, ST_SEL, cc, 0);  // wave-uniform; batches past the end load line 0
         const uint4 ix = make_uint4(word_to_index(blk.x, S), word_to_index(blk.y, S), word_to_index(blk.z, S),
                                     word_to_index(blk.w, S));
         ixs[B * 64u + lane] = ix;
@@ -588,9 +589,9 @@ __global__ __launch_bounds__(kBlock, OBJ == kObjKnapMfma ? 4 : PGA_TP_WAVES) voi
           k2[B] = ELEM(const float, a.score_cur, j.z);
           k3[B] = ELEM(const float, a.score_cur, j.w);
         }
-        // no early exit past the segment's last batch: straight-line code keeps
+        // no early exit past the segment's last batch: straight-line loads keep
         // every key in a register (a wave-uniform break spilled the last four);
-        // the extra batches draw clamped children and are never resolved
+        // the extra batches skip the Philox draw and are never resolved
       }
       if (roul) {
         // fitness-proportional: the 2 x kSegBatches binary searches of
