@@ -99,8 +99,8 @@ void select_parents(const GenArgs& a, uint64_t child, uint32_t& pa, uint32_t& pb
 
 static inline uint32_t popc(uint32_t x) { return (uint32_t)__builtin_popcount(x); }
 
-// BINARY parent choice from the ST_SEL words (core.hpp "BINARY randomness layout")
-static void bin_select_parents(const GenArgs& a, uint64_t child, uint32_t& pa, uint32_t& pb) {
+// BINARY / REAL parent choice from the ST_SEL words (core.hpp "BINARY randomness layout")
+void bin_select_parents(const GenArgs& a, uint64_t child, uint32_t& pa, uint32_t& pb) {
   const uint32_t S = (uint32_t)a.S;
   auto w = [&](uint32_t t) { return bin_sel_word(a.key, child, t); };
   if (a.selection == SEL_TOURNAMENT) {

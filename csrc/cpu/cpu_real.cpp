@@ -1,9 +1,9 @@
 // cpu_real.cpp — CPU reference backend for the REAL encoding; mirrors
-// csrc/kernels/real.hip (same per-gene semantics from real_ops.hpp, same
-// GS-lane butterfly reductions, rotation as a k-ordered fma chain = the MFMA
-// result).  Transcendental functions differ from the device by a few ulps, so
-// REAL generations agree with the GPU to within float tolerance rather than
-// bit for bit.
+// csrc/kernels/real.hip (same randomness layout and per-gene semantics from
+// real_ops.hpp, same GS-lane butterfly reductions, rotation as a k-ordered fma
+// chain = the MFMA result).  Rows are bit-identical to the GPU for every
+// operator (gaussian included: real_ops.hpp gauss_z); scores of the
+// polynomial objectives too, those of the transcendental ones to a few ulps.
 #include <algorithm>
 #include <cmath>
 #include <cstring>
@@ -33,7 +33,8 @@ uint32_t real_run(int mode, const GenArgs& a, unsigned long long* best_parts) {
   const uint32_t L = a.L, nchunks = a.chunks;
   const bool gen = mode == MODE_GEN, cross = mode == MODE_CROSS, mutm = mode == MODE_MUTATE;
   const bool evals = a.objective != OBJ_NONE && (gen || mode == MODE_INIT || mode == MODE_EVAL);
-  const bool per_gene_mut = (gen || mutm) && (a.mutation == MUT_GAUSSIAN || a.mutation == MUT_UNIFORM) && a.mut_rate > 0.f;
+  const bool per_gene = (gen || mutm) && real_per_gene_mutation(a);
+  const bool sparse = per_gene && a.mut_sparse;
   const bool reset_one = (gen || mutm) && a.mutation == MUT_RESET_ONE;
   const bool rot = (a.obj_i & 2) && a.obj_data && real_obj_rotatable(a.objective);
   const bool shift = (a.obj_i & 1) && a.obj_data2 && real_obj_rotatable(a.objective);
@@ -52,56 +53,52 @@ uint32_t real_run(int mode, const GenArgs& a, unsigned long long* best_parts) {
   parallel_for(a.S, 64, [&](uint64_t c_begin, uint64_t c_end, unsigned slot) {
   unsigned long long best = 0;
   std::vector<float> v(nv), x(std::max<uint32_t>(nv, dp) + 4), z(std::max<uint32_t>(nv, dp) + 4);
+  std::vector<uint32_t> pos;
   for (uint64_t child = c_begin; child < c_end; ++child) {
     std::fill(v.begin(), v.end(), 0.f);
-    bool elite = false;
-    float score = 0.f;
-    if (gen && child < a.n_elite) {
-      elite = true;
+    // elitism: child = copy of the elite row (no variation), re-evaluated like every child
+    const bool elite = gen && child < a.n_elite;
+    const u32x4 misc = real_misc(a.key, child);
+    if (elite) {
       const uint32_t src = a.elite_idx ? a.elite_idx[child] : elite0;
       std::memcpy(v.data(), cur + (uint64_t)src * rw, 16ull * nchunks);
-      score = a.score_cur[src];
     } else if (mode == MODE_INIT) {
       for (uint32_t q = 0; q < nchunks; ++q) real_init_chunk(a, child, q, &v[4 * q]);
     } else if (mode == MODE_EVAL || mutm) {
       std::memcpy(v.data(), cur + child * rw, 16ull * nchunks);
     }
-    if (!elite && (gen || cross || mutm)) {
-      if (gen || cross) {
-        uint32_t pa, pb;
-        select_parents(a, child, pa, pb);
-        const bool xo = a.crossover != XO_NONE && do_crossover(a, pool_word(a.key, child, W_XOPROB));
-        uint32_t blo = 0, bhi = 0;
-        float ua = 0.f;
-        if (a.crossover == XO_ONE_POINT) {
-          blo = word_to_index(pool_word(a.key, child, W_CUT1), L);
-          bhi = L;
-        } else if (a.crossover == XO_TWO_POINT) {
-          const uint32_t c1 = word_to_index(pool_word(a.key, child, W_CUT1), L);
-          const uint32_t c2 = word_to_index(pool_word(a.key, child, W_CUT2), L);
-          blo = std::min(c1, c2);
-          bhi = std::max(c1, c2);
-        } else if (a.crossover == XO_ARITHMETIC) {
-          ua = word_to_unit(pool_word(a.key, child, W_CUT1));
-        }
-        for (uint32_t q = 0; q < nchunks; ++q)
-          real_cross_chunk(a, child, q, cur + (uint64_t)pa * rw + 4 * q, cur + (uint64_t)pb * rw + 4 * q, xo, blo, bhi,
-                           ua, &v[4 * q]);
+    if (!elite && (gen || cross)) {
+      uint32_t pa, pb;
+      bin_select_parents(a, child, pa, pb);
+      const bool xo = a.crossover != XO_NONE && do_crossover(a, misc.x);
+      const uint32_t cut = real_cut_word(a, misc);
+      for (uint32_t q = 0; q < nchunks; ++q) {
+        const uint32_t ub = (xo && a.crossover == XO_UNIFORM) ? real_uniform_bits(a.key, child, q) : 0u;
+        real_cross_chunk(a, child, q, cur + (uint64_t)pa * rw + 4 * q, cur + (uint64_t)pb * rw + 4 * q, xo, cut, ub,
+                         &v[4 * q]);
       }
-      if (per_gene_mut) {
-        for (uint32_t q = 0; q < nchunks; ++q) {
-          const uint32_t clen = std::min(4u, L - 4 * q);
-          real_mutate_chunk(a, child, q, clen, chunk_mut_word(a.key, child, q), a.mut_thr, &v[4 * q]);
-        }
-      } else if (reset_one && pool_word(a.key, child, W_MUTIND) < a.mut_ind_thresh) {
-        const uint32_t pos = word_to_index(pool_word(a.key, child, W_MUTPOS), L);
-        v[pos] = real_reset_value(a, pool_word(a.key, child, W_SEL + sel_words(a)));
+    }
+    if (!elite && (sparse || reset_one)) {
+      // the first K distinct positions of the mutation words, the n-th takes value draw n
+      const uint32_t K = sparse ? binom_count(misc.w, a.mut_thr) : (misc.w < a.mut_ind_thresh ? 1u : 0u);
+      pos.clear();
+      for (uint32_t j = 0; pos.size() < K; ++j) {
+        const uint32_t p = word_to_index(bin_mut_word(a.key, child, j), L);
+        if (std::find(pos.begin(), pos.end(), p) != pos.end()) continue;
+        v[p] = real_mut_apply(a, real_mut_draw(a, child, (uint32_t)pos.size()), v[p]);
+        pos.push_back(p);
+      }
+    } else if (!elite && per_gene) {
+      for (uint32_t q = 0; q < nchunks; ++q) {
+        const uint32_t clen = std::min(4u, L - 4 * q);
+        real_mutate_chunk(a, child, q, clen, bin_chunk_mut_word(a.key, child, q), a.mut_thr, &v[4 * q]);
       }
     }
     for (uint32_t d = L; d < 4 * nchunks; ++d) v[d] = 0.f;
     if (mode != MODE_EVAL) std::memcpy(nxt + child * rw, v.data(), 16ull * nchunks);
 
-    if (evals && !elite) {
+    float score = 0.f;
+    if (evals) {
       std::fill(x.begin(), x.end(), 0.f);
       for (uint32_t d = 0; d < L; ++d) x[d] = shift ? v[d] - a.obj_data2[d] : v[d];
       if (rot) {
@@ -138,8 +135,6 @@ uint32_t real_run(int mode, const GenArgs& a, unsigned long long* best_parts) {
         RealAcc t{butterfly_sum(s0, GS), butterfly_sum(s1, GS), butterfly_prod(s2, GS)};
         score = real_obj_finish(a, t);
       }
-    }
-    if (evals) {
       a.score_next[child] = score;
       best = std::max(best, pack_best(score, child));
     }
@@ -150,7 +145,6 @@ uint32_t real_run(int mode, const GenArgs& a, unsigned long long* best_parts) {
   if (evals && best_parts) best_parts[0] = best;
   return 1;
 }
-
 
 }  // namespace cpu
 }  // namespace pga

@@ -139,7 +139,11 @@ void Island::rebuild_mut_table() {
   if (mut_rate_eff_ > 1.f) mut_rate_eff_ = 1.f;
   std::vector<uint32_t> thr(kMutCap);
   build_mut_table(per_ind ? 0.f : mut_rate_eff_, kMutCap, thr.data(), &mut_inv_);
-  mut_sparse_ = cfg_.encoding == ENC_BINARY && cfg_.mutation == MUT_BIT_FLIP && bin_sparse_mutation(cfg_.L, mut_rate_eff_);
+  // sparse samplers (K ~ Binomial(L, p), then K distinct positions): BINARY
+  // bit-flip and REAL per-gene mutation at the usual ~1/L rates
+  const bool per_gene = (cfg_.encoding == ENC_BINARY && cfg_.mutation == MUT_BIT_FLIP) ||
+                        (cfg_.encoding == ENC_REAL && (cfg_.mutation == MUT_GAUSSIAN || cfg_.mutation == MUT_UNIFORM));
+  mut_sparse_ = per_gene && bin_sparse_mutation(cfg_.L, mut_rate_eff_);
   if (mut_sparse_) build_binom_table(mut_rate_eff_, cfg_.L, thr.data());
   if (!mut_thr_.ptr) mut_thr_ = alloc(4ull * kMutCap);
   if (on_gpu()) synchronize();

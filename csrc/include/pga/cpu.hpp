@@ -3,9 +3,10 @@
 // Same operator semantics as the gfx950 kernels, evaluated one individual at a
 // time on host memory.  Because every random draw is addressed by
 // (seed, generation, island, individual, purpose, block) and group
-// reductions follow the same lane butterfly, BINARY and PERMUTATION
-// generations are bit-identical to the GPU; REAL generations match up to
-// transcendental-function ulps.  This is the oracle of the test-suite and the
+// reductions follow the same lane butterfly, generations are bit-identical to
+// the GPU: rows of every encoding, scores up to the transcendental objectives
+// (REAL Rastrigin / Ackley / Griewank / Schwefel, whose libm calls differ from
+// the device's by ulps).  This is the oracle of the test-suite and the
 // "CPU reference path" config of BASELINE.json.
 #pragma once
 
@@ -60,6 +61,8 @@ inline float butterfly_sum(float* v, uint32_t GS) {
 inline uint32_t pool_word(const RngKey& key, uint64_t child, uint32_t t) { return child_word(key, child, t); }
 
 void select_parents(const GenArgs& a, uint64_t child, uint32_t& pa, uint32_t& pb);
+// parents from the ST_SEL words (the BINARY and REAL layouts)
+void bin_select_parents(const GenArgs& a, uint64_t child, uint32_t& pa, uint32_t& pb);
 
 }  // namespace cpu
 }  // namespace pga

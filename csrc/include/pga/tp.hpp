@@ -1,0 +1,135 @@
+// tp.hpp — the first phase of the transposed generation kernels (gfx950).
+//
+// A wave owns a contiguous range of children; a SEGMENT of up to
+// kSegBatches batches of 64 children is selected one lane per child with
+// every score / key load of the segment in flight at once (the second phase,
+// breeding, is encoding specific: real.hip real_gen_tp; binary.hip keeps its
+// own inlined copy of this phase).  Selection words are the ST_SEL layout of
+// core.hpp, so the result equals st_select_parents() child by child.
+#pragma once
+
+#include <type_traits>
+
+#include "pga/device.hpp"
+
+namespace pga {
+namespace dev {
+
+constexpr uint32_t kSegBatches = 4;   // batches (x 64 children) per tournament segment
+constexpr uint32_t kTpMaxElite = 64;  // elites the transposed kernels route through their records
+
+// element i of a buffer with a 32-bit byte offset (uniform base + one VGPR)
+template <typename T>
+__device__ __forceinline__ T ld32(const void* base, uint32_t i) {
+  return *(const T*)((const char*)base + i * (uint32_t)sizeof(T));
+}
+
+// Parents (A, B) of children [begin + 64 B + lane] for the segment's batches
+// B < kSegBatches -> par[B * 64 + lane].  ixs: 4 x 64 uint4 of LDS scratch
+// (the contestants wait there while the loads fly).  KEY: integer
+// objectives compare their u16 tournament keys instead of the f32 scores.
+template <bool KEY>
+__device__ __forceinline__ void tp_select_segment(const GenArgs& a, uint32_t begin, uint32_t end, uint32_t lane,
+                                                  uint4* ixs, uint2* par) {
+  const uint32_t S = (uint32_t)a.S;
+  const uint32_t nbatch = (end - begin + 63) / 64;
+  const bool tourn = a.selection == SEL_TOURNAMENT;  // tour_k == 2 guaranteed by the launcher
+  const bool rank = a.selection == SEL_RANK;
+  const bool roul = a.selection == SEL_ROULETTE;  // else random
+  // raw keys (u16 zero-extended, or f32 scores), compared only after every
+  // load of the segment is issued: a conversion here would make hipcc wait
+  // for each batch's loads before issuing the next batch's
+  using KT = typename std::conditional<KEY, uint32_t, float>::type;
+  KT k0[kSegBatches], k1[kSegBatches], k2[kSegBatches], k3[kSegBatches];
+#pragma unroll
+  for (uint32_t B = 0; B < kSegBatches; ++B) {
+    const uint32_t tc = begin + B * 64u + lane;
+    const uint32_t cc = tc < end ? tc : end - 1;
+    u32x4 blk{0u, 0u, 0u, 0u};
+    if (B < nbatch) blk = draw<true>(a.key, ST_SEL, cc, 0);  // wave-uniform; batches past the end load entry 0
+    const uint4 ix = make_uint4(word_to_index(blk.x, S), word_to_index(blk.y, S), word_to_index(blk.z, S),
+                                word_to_index(blk.w, S));
+    ixs[B * 64u + lane] = ix;
+    const uint4 j = tourn ? ix : make_uint4(0, 0, 0, 0);
+    if (roul) {  // the two selection words, searched below for every batch at once
+      k0[B] = __builtin_bit_cast(KT, blk.x);
+      k1[B] = __builtin_bit_cast(KT, blk.y);
+    } else if (rank) {  // linear ranking: the two parents straight from the rank order
+      const u32x4 b1 = draw<true>(a.key, ST_SEL, cc, 1);
+      const uint32_t ra = rank_pick(blk.x, blk.y, blk.z, S, a.rank_thresh);
+      const uint32_t rb = rank_pick(blk.w, b1.x, b1.y, S, a.rank_thresh);
+      k0[B] = __builtin_bit_cast(KT, ld32<uint32_t>(a.rank_order, ra));
+      k1[B] = __builtin_bit_cast(KT, ld32<uint32_t>(a.rank_order, rb));
+    } else if constexpr (KEY) {
+      k0[B] = ld32<uint16_t>(a.key_cur, j.x);
+      k1[B] = ld32<uint16_t>(a.key_cur, j.y);
+      k2[B] = ld32<uint16_t>(a.key_cur, j.z);
+      k3[B] = ld32<uint16_t>(a.key_cur, j.w);
+    } else {
+      k0[B] = ld32<float>(a.score_cur, j.x);
+      k1[B] = ld32<float>(a.score_cur, j.y);
+      k2[B] = ld32<float>(a.score_cur, j.z);
+      k3[B] = ld32<float>(a.score_cur, j.w);
+    }
+  }
+  if (roul) {
+    // fitness-proportional: the 2 x kSegBatches binary searches of
+    // roulette_pick (smallest i with cumfit[i] >= u * total) advance in
+    // lock step, one load each per halving
+    constexpr uint32_t NS = 2 * kSegBatches;
+    const float total = a.cumfit[S - 1];
+    uint32_t lo[NS], hi[NS];
+    float tg[NS];
+#pragma unroll
+    for (uint32_t i = 0; i < NS; ++i) {
+      const uint32_t w = __builtin_bit_cast(uint32_t, (i & 1u) ? k1[i >> 1] : k0[i >> 1]);
+      tg[i] = word_to_unit(w) * total;
+      lo[i] = total > 0.f ? 0u : word_to_index(w, S);
+      hi[i] = total > 0.f ? S - 1 : lo[i];
+    }
+    for (uint32_t n = S; n > 1; n = (n + 1) >> 1) {  // wave-uniform trip count
+      float v[NS];
+#pragma unroll
+      for (uint32_t i = 0; i < NS; ++i) v[i] = ld32<float>(a.cumfit, (lo[i] + hi[i]) >> 1);
+#pragma unroll
+      for (uint32_t i = 0; i < NS; ++i) {
+        const uint32_t mid = (lo[i] + hi[i]) >> 1;
+        if (lo[i] < hi[i]) {
+          if (v[i] < tg[i]) lo[i] = mid + 1;
+          else hi[i] = mid;
+        }
+      }
+    }
+#pragma unroll
+    for (uint32_t B = 0; B < kSegBatches; ++B) {
+      k0[B] = __builtin_bit_cast(KT, lo[2 * B]);
+      k1[B] = __builtin_bit_cast(KT, lo[2 * B + 1]);
+    }
+  }
+#pragma unroll
+  for (uint32_t B = 0; B < kSegBatches; ++B) {
+    const uint4 ix = ixs[B * 64u + lane];
+    uint32_t pa = ix.x, pb = ix.y;
+    if (tourn) {
+      pa = k0[B] < k1[B] ? ix.y : ix.x;
+      pb = k2[B] < k3[B] ? ix.w : ix.z;
+    } else if (rank || roul) {
+      pa = __builtin_bit_cast(uint32_t, k0[B]);
+      pb = __builtin_bit_cast(uint32_t, k1[B]);
+    }
+    par[B * 64u + lane] = make_uint2(pa, pb);
+  }
+}
+
+// this wave's children [wbegin, wend): contiguous, a multiple of NG long
+__device__ __forceinline__ void tp_wave_range(uint32_t S, uint32_t NG, uint32_t& wbegin, uint32_t& wend) {
+  constexpr uint32_t NW = kBlock / 64;
+  const uint64_t W = (uint64_t)gridDim.x * NW, w = (uint64_t)blockIdx.x * NW + (threadIdx.x >> 6);
+  uint64_t per = (S + W - 1) / W;
+  per = (per + NG - 1) / NG * NG;
+  wbegin = (uint32_t)(w * per < S ? w * per : S);
+  wend = (uint32_t)(wbegin + per < S ? wbegin + per : S);
+}
+
+}  // namespace dev
+}  // namespace pga

@@ -155,14 +155,6 @@ __device__ __forceinline__ v4i expand16(uint32_t h) {  // 16 bits -> 16 int8 {0,
   return r;
 }
 
-// LDS written by other lanes of this wave is read after it (LDS ops of one
-// wave complete in order; this only stops the compiler moving them)
-__device__ __forceinline__ void wave_lds_sync() {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
-
 // chunk slot of lane 4m + h in the wave scratch: virtual row m, lane group h,
 // XOR-swizzled so that both the lane-order store and the (h, n) fragment
 // read touch 8 distinct 16-byte bank groups per 8 lanes
@@ -207,53 +199,6 @@ __device__ __forceinline__ float knap_mfma(const GenArgs& a, uint4 v, uint32_t l
   }
   const float vv = (float)(int)group_sum_u<GS>(V), ww = (float)(int)group_sum_u<GS>(W);
   return ww <= a.obj_f0 ? vv : a.obj_f0 - ww;
-}
-
-// Parents of `child` from the ST_SEL words; group-uniform (every lane of the
-// group computes the same).  Mirrors cpu_ops.cpp bin_select_parents.
-__device__ __forceinline__ void bin_select(const GenArgs& a, uint64_t child, uint32_t& pa, uint32_t& pb) {
-  const uint32_t S = (uint32_t)a.S;
-  u32x4 blk = draw(a.key, ST_SEL, child, 0);
-  if (a.selection == SEL_TOURNAMENT && a.tour_k == 2) {
-    const uint32_t i0 = word_to_index(blk.x, S), i1 = word_to_index(blk.y, S);
-    const uint32_t i2 = word_to_index(blk.z, S), i3 = word_to_index(blk.w, S);
-    const float s0 = a.score_cur[i0], s1 = a.score_cur[i1], s2 = a.score_cur[i2], s3 = a.score_cur[i3];
-    pa = (s0 < s1) ? i1 : i0;
-    pb = (s2 < s3) ? i3 : i2;
-  } else if (a.selection == SEL_TOURNAMENT) {
-    const uint32_t k = a.tour_k;
-    uint32_t cb = 0, best[2];
-    for (uint32_t p = 0; p < 2; ++p) {
-      uint32_t b = 0;
-      float bs = 0.f;
-      for (uint32_t j = 0; j < k; ++j) {
-        const uint32_t t = p * k + j;
-        if ((t >> 2) != cb) {
-          cb = t >> 2;
-          blk = draw(a.key, ST_SEL, child, cb);
-        }
-        const uint32_t c = word_to_index(sel4(blk, t & 3u), S);
-        const float cs = a.score_cur[c];
-        if (j == 0 || bs < cs) {
-          bs = cs;
-          b = c;
-        }
-      }
-      best[p] = b;
-    }
-    pa = best[0];
-    pb = best[1];
-  } else if (a.selection == SEL_ROULETTE) {
-    pa = roulette_pick(a.cumfit, S, blk.x);
-    pb = roulette_pick(a.cumfit, S, blk.y);
-  } else if (a.selection == SEL_RANK) {
-    const u32x4 b1 = draw(a.key, ST_SEL, child, 1);
-    pa = a.rank_order[rank_pick(blk.x, blk.y, blk.z, S, a.rank_thresh)];
-    pb = a.rank_order[rank_pick(blk.w, b1.x, b1.y, S, a.rank_thresh)];
-  } else {
-    pa = word_to_index(blk.x, S);
-    pb = word_to_index(blk.y, S);
-  }
 }
 
 // Sparse bit-flip sampler, group-cooperative form: continue the sequence of
@@ -359,7 +304,7 @@ __global__ __launch_bounds__(kBlock) void binary_kernel(GenArgs a, unsigned long
       if (elite) {
         pa = pb = a.elite_idx ? a.elite_idx[child] : lds_elite;
       } else if (MODE == MODE_GEN || MODE == MODE_CROSS) {
-        bin_select(a, child, pa, pb);
+        st_select_parents(a, child, pa, pb);
         xo = a.crossover != XO_NONE && do_crossover(a, misc.x);
         if (a.crossover == XO_ONE_POINT) {
           blo = word_to_index(misc.y, L);

@@ -63,7 +63,7 @@ __device__ __forceinline__ void ld8(const uint16_t* p, uint32_t e[8]) {
 template <int GS, int MODE, int OBJ, int BLK = kBlock>
 __global__ __launch_bounds__(BLK) void perm_kernel(GenArgs a, unsigned long long* best_parts) {
   resolve_gen(a);
-  extern __shared__ __attribute__((aligned(16))) float smem[];
+  float* smem = (float*)pga_dyn_lds;
   unsigned long long* lds_red = (unsigned long long*)smem;
   uint32_t* lds_elite = (uint32_t*)(smem + 8);
   const uint32_t L = a.L, nch = a.chunks, lp = 8 * nch;
@@ -310,7 +310,7 @@ __device__ __forceinline__ uint4 set16(uint4 v, uint32_t e, uint32_t x) {
 template <int GS, int OBJ>
 __global__ __launch_bounds__(kBlock) void perm_gen_fast(GenArgs a, unsigned long long* best_parts) {
   resolve_gen(a);
-  extern __shared__ __attribute__((aligned(16))) float smem[];
+  float* smem = (float*)pga_dyn_lds;
   unsigned long long* lds_red = (unsigned long long*)smem;
   uint32_t* lds_elite = (uint32_t*)(smem + 8);
   const uint32_t L = a.L, nch = a.chunks, lp = 8 * nch;

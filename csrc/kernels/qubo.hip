@@ -55,7 +55,7 @@ __global__ __launch_bounds__(kBlock, 2) void qubo_eval_kernel(const uint32_t* __
   constexpr uint32_t QROW = Lp + 16u;         // LDS row stride of the Q^T block (bytes)
   constexpr uint32_t BROW = Lp / 8u + 8u;     // LDS row stride of a child's bits (bytes)
   constexpr uint32_t TILE = 4u * 16u * MT;    // children per workgroup tile
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  unsigned char* smem = pga_dyn_lds;
   unsigned char* qb = smem;                   // [64][QROW]
   unsigned char* bits = smem + 64u * QROW;    // [TILE][BROW]
   __shared__ unsigned long long lds_red[kBlock / 64];

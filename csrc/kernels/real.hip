@@ -3,30 +3,33 @@
 //
 // Geometry: one individual = `chunks` 16-byte chunks of 4 genes; a group of
 // GS = group_size(chunks) lanes owns one individual (lane q holds genes
-// 4q..4q+3), GPB = 256/GS individuals per block iteration, for genomes up to
-// 256 genes (GS <= 64); longer genomes use real_long_kernel (a chunk-segment
-// loop, one wave per individual).  Per iteration every child's genes are also staged in an
-// LDS tile X[GPB][TW] (TW = max(4 GS, 16) + 1: the +1 breaks the 16-way bank
-// conflict of the MFMA A-operand column reads).
+// 4q..4q+3), for genomes up to 256 genes (GS <= 64); longer genomes use
+// real_long_kernel (a chunk-segment loop, one wave per individual).  The
+// randomness layout (real_ops.hpp) is the BINARY one: ST_SEL selection words,
+// one misc block per child, sparse mutation positions from ST_BMUT.
+//
+// Kernels:
+//   real_gen_tp<GS,OBJ,ROT>     the hot generation path (transposed tournaments,
+//                               per-child records, see below)
+//   real_kernel<GS,MODE,ROT,UFN> every mode / selection / objective, one child
+//                               per lane group at a time; rotated objectives
+//                               on MFMA 16x16x4 f32 tiles staged in LDS
+//   real_long_kernel<MODE>      genomes beyond 256 genes
 //
 // Rotated objectives (CEC-style f(M (x - o)), the "MFMA batched fitness" of
-// BASELINE config 3) multiply the whole child tile by M^T with
-// v_mfma_f32_16x16x4_f32: 16 children x 16 dims per wave tile, K = 4 per
-// instruction, exact f32 (bit-for-bit a k-ordered fma chain, so the CPU
-// reference reproduces it), M staged once per block in LDS (real_gen_fast,
-// L <= 128).  For L <= 32 (the 30-D Rastrigin config) the software-pipelined
-// kernel does the rotation wave-locally instead, with v_mfma_f32_4x4x1_16b_f32
-// (64/GS children x 4 GS dims = 16 blocks of 4x4 per wave, no empty rows),
-// the same exact fma chain, and no block barrier (real_gen_pipe, ROT).
+// BASELINE config 3) multiply child tiles by M^T on the matrix cores, exact
+// f32 (bit-for-bit a k-ordered fma chain, so the CPU reference reproduces it).
 //
 // Reference parity: float genes, user objective via device function pointer
 // (OBJ_USER_FNPTR, include/pga.h:46 obj_f), E1 sum / E2 knapsack / E3 random-key
-// TSP objectives (test*/test.cu) are built in.
+// TSP objectives (test*/test.cu) are built in; the reference's evaluate /
+// crossover / mutate kernels (src/pga.cu:250-347) become one launch.
 #include <hip/hip_runtime.h>
 
 #include "pga/device.hpp"
 #include "pga/ops.hpp"
 #include "pga/real_ops.hpp"
+#include "pga/tp.hpp"
 
 namespace pga {
 namespace {
@@ -40,6 +43,45 @@ __device__ __forceinline__ float group_prod(float v) {
 #pragma unroll
   for (int o = GS / 2; o > 0; o >>= 1) v *= __shfl_xor(v, o, 64);
   return v;
+}
+
+__device__ __forceinline__ float gene4(const float v[4], uint32_t b) {
+  return fsel(b == 0, v[0], fsel(b == 1, v[1], fsel(b == 2, v[2], v[3])));
+}
+__device__ __forceinline__ void set_gene4(float v[4], uint32_t b, float x) {
+  v[0] = fsel(b == 0, x, v[0]);
+  v[1] = fsel(b == 1, x, v[1]);
+  v[2] = fsel(b == 2, x, v[2]);
+  v[3] = fsel(b == 3, x, v[3]);
+}
+
+// Sparse per-gene mutation, group-cooperative form: continue the sequence of
+// mutation words at j with n distinct genes already mutated (mm = this lane's
+// mask of mutated genes of its chunk q), until K distinct genes are mutated.
+// A candidate is a repeat iff its owner lane already mutated it: one ballot
+// per candidate.  The owner applies the n-th value.  Same result as the
+// sequential definition (cpu_real.cpp).
+template <int GS, bool NH = false>
+__device__ __forceinline__ void real_sparse_group(const GenArgs& a, uint64_t child, uint32_t K, uint32_t n, uint32_t j,
+                                                  uint32_t& mm, uint32_t q, uint32_t gbase, float v[4]) {
+  u32x4 blk{0u, 0u, 0u, 0u};
+  if (j & 3u) blk = draw<NH>(a.key, ST_BMUT, child, j >> 2);
+  while (n < K) {  // group-uniform
+    if ((j & 3u) == 0u) blk = draw<NH>(a.key, ST_BMUT, child, j >> 2);
+    const uint32_t p = word_to_index(sel4(blk, j & 3u), a.L);
+    ++j;
+    const bool own = (p >> 2) == q;
+    const uint32_t b = p & 3u;
+    unsigned long long bal = __ballot(own && ((mm >> b) & 1u));
+    if (GS < 64) bal = (bal >> gbase) & ((1ull << GS) - 1ull);
+    if (bal == 0ull) {
+      if (own) {
+        set_gene4(v, b, real_mut_apply(a, real_mut_draw<NH>(a, child, n), gene4(v, b)));
+        mm |= 1u << b;
+      }
+      ++n;
+    }
+  }
 }
 
 struct RealGeom {
@@ -68,13 +110,16 @@ __host__ __device__ inline size_t real_lds_floats(uint32_t GS, uint32_t chunks, 
   return n;
 }
 
+// ---------------------------------------------------------------------------
+// Generic kernel: every mode, selection and objective, one child per group.
 // UFN: the user-objective instantiation is the only one that contains the
 // indirect call (an indirect call forces a scratch stack and a conservative
-// register allocation on every instantiation that can reach it)
+// register allocation on every instantiation that can reach it).
+// ---------------------------------------------------------------------------
 template <int GS, int MODE, bool ROT, bool UFN>
 __global__ __launch_bounds__(kBlock) void real_kernel(GenArgs a, unsigned long long* best_parts) {
   resolve_gen(a);
-  extern __shared__ __attribute__((aligned(16))) float smem[];
+  float* smem = (float*)pga_dyn_lds;
   uint32_t* lds_thr = (uint32_t*)smem;
   unsigned long long* lds_red = (unsigned long long*)(smem + 128);
   uint32_t* lds_elite = (uint32_t*)(smem + 136);
@@ -95,9 +140,11 @@ __global__ __launch_bounds__(kBlock) void real_kernel(GenArgs a, unsigned long l
   const bool have = q < a.chunks;
   const uint32_t clen = have ? (L - 4 * q >= 4 ? 4u : L - 4 * q) : 0u;
   constexpr bool MUTATES = MODE == MODE_GEN || MODE == MODE_MUTATE;
+  constexpr bool CROSSES = MODE == MODE_GEN || MODE == MODE_CROSS;
   constexpr bool EVALS = MODE == MODE_GEN || MODE == MODE_INIT || MODE == MODE_EVAL;
   const bool evals = EVALS && a.objective != OBJ_NONE;
-  const bool per_gene_mut = MUTATES && (a.mutation == MUT_GAUSSIAN || a.mutation == MUT_UNIFORM) && a.mut_rate > 0.f;
+  const bool per_gene = MUTATES && real_per_gene_mutation(a);
+  const bool sparse = per_gene && a.mut_sparse;
   const bool reset_one = MUTATES && a.mutation == MUT_RESET_ONE;
   const bool shift = (a.obj_i & 1) && a.obj_data2 && real_obj_rotatable(a.objective);
   const bool tile_needed = ROT || a.objective == OBJ_TSP_RANDOM_KEY || a.objective == OBJ_USER_FNPTR ||
@@ -108,7 +155,7 @@ __global__ __launch_bounds__(kBlock) void real_kernel(GenArgs a, unsigned long l
     unsigned long long b = block_reduce_parts(a.best_cur, a.n_best_cur, lds_red);
     if (threadIdx.x == 0) *lds_elite = (uint32_t)best_index(b);
   }
-  if (per_gene_mut)
+  if (per_gene)
     for (uint32_t i = threadIdx.x; i < kMutCap; i += kBlock) lds_thr[i] = a.mut_thr[i];
   for (uint32_t i = threadIdx.x; i < G.xr * G.tw; i += kBlock) X[i] = 0.f;
   if (ROT) {
@@ -126,17 +173,17 @@ __global__ __launch_bounds__(kBlock) void real_kernel(GenArgs a, unsigned long l
     const uint64_t child = base + g;
     const bool valid = child < a.S;  // group-uniform
     float v[4] = {0.f, 0.f, 0.f, 0.f};
-    bool elite = false;
     float score = 0.f;
     if (valid) {
-      if (MODE == MODE_GEN && child < a.n_elite) {
-        elite = true;
+      // elitism: child = copy of the elite row (no variation), re-evaluated like every child
+      const bool elite = MODE == MODE_GEN && child < a.n_elite;
+      const u32x4 misc = (CROSSES || MUTATES) ? real_misc(a.key, child) : u32x4{0, 0, 0, 0};
+      if (elite) {
         const uint32_t src = a.elite_idx ? a.elite_idx[child] : *lds_elite;
         if (have) {
           const float4 e = cur[(uint64_t)src * rs + q];
           v[0] = e.x; v[1] = e.y; v[2] = e.z; v[3] = e.w;
         }
-        score = a.score_cur[src];
       } else if (MODE == MODE_INIT) {
         if (have) real_init_chunk(a, child, q, v);
       } else if (MODE == MODE_EVAL || MODE == MODE_MUTATE) {
@@ -145,43 +192,25 @@ __global__ __launch_bounds__(kBlock) void real_kernel(GenArgs a, unsigned long l
           v[0] = e.x; v[1] = e.y; v[2] = e.z; v[3] = e.w;
         }
       }
-      if (!elite && (MODE == MODE_GEN || MODE == MODE_CROSS || MODE == MODE_MUTATE)) {
-        Pool<GS> pool{draw(a.key, ST_CHILD, child, q), gbase};
-        if (MODE == MODE_GEN || MODE == MODE_CROSS) {
-          uint32_t pa, pb;
-          select_parents<GS>(a, pool, child, pa, pb);
-          const bool xo = a.crossover != XO_NONE && do_crossover(a, pool.get(W_XOPROB, a.key, child));
-          uint32_t blo = 0, bhi = 0;
-          float ua = 0.f;
-          if (a.crossover == XO_ONE_POINT) {
-            blo = word_to_index(pool.get(W_CUT1, a.key, child), L);
-            bhi = L;
-          } else if (a.crossover == XO_TWO_POINT) {
-            const uint32_t c1 = word_to_index(pool.get(W_CUT1, a.key, child), L);
-            const uint32_t c2 = word_to_index(pool.get(W_CUT2, a.key, child), L);
-            blo = c1 < c2 ? c1 : c2;
-            bhi = c1 < c2 ? c2 : c1;
-          } else if (a.crossover == XO_ARITHMETIC) {
-            ua = word_to_unit(pool.get(W_CUT1, a.key, child));
-          }
-          if (have) {
-            const float4 A4 = cur[(uint64_t)pa * rs + q], B4 = cur[(uint64_t)pb * rs + q];
-            const float A[4] = {A4.x, A4.y, A4.z, A4.w}, B[4] = {B4.x, B4.y, B4.z, B4.w};
-            real_cross_chunk(a, child, q, A, B, xo, blo, bhi, ua, v);
-          }
+      if (CROSSES && !elite) {
+        uint32_t pa, pb;
+        st_select_parents(a, child, pa, pb);
+        const bool xo = a.crossover != XO_NONE && do_crossover(a, misc.x);
+        const uint32_t cut = real_cut_word(a, misc);
+        if (have) {
+          const float4 A4 = cur[(uint64_t)pa * rs + q], B4 = cur[(uint64_t)pb * rs + q];
+          const float A[4] = {A4.x, A4.y, A4.z, A4.w}, B[4] = {B4.x, B4.y, B4.z, B4.w};
+          const uint32_t ub = (xo && a.crossover == XO_UNIFORM) ? real_uniform_bits(a.key, child, q) : 0u;
+          real_cross_chunk(a, child, q, A, B, xo, cut, ub, v);
         }
-        if (per_gene_mut && have) {
-          real_mutate_chunk(a, child, q, clen, pool.w.w, lds_thr, v);
-        } else if (reset_one && pool.get(W_MUTIND, a.key, child) < a.mut_ind_thresh) {
-          const uint32_t pos = word_to_index(pool.get(W_MUTPOS, a.key, child), L);
-          const float x = real_reset_value(a, pool.get(W_SEL + sel_words(a), a.key, child));
-          if ((pos >> 2) == q) {
-            const uint32_t j = pos & 3u;
-            v[0] = j == 0 ? x : v[0];
-            v[1] = j == 1 ? x : v[1];
-            v[2] = j == 2 ? x : v[2];
-            v[3] = j == 3 ? x : v[3];
-          }
+      }
+      if (MUTATES && !elite) {
+        if (sparse || reset_one) {
+          const uint32_t K = sparse ? binom_count(misc.w, lds_thr) : (misc.w < a.mut_ind_thresh ? 1u : 0u);
+          uint32_t mm = 0;
+          real_sparse_group<GS>(a, child, K, 0, 0, mm, q, gbase, v);
+        } else if (per_gene && have) {
+          real_mutate_chunk(a, child, q, clen, bin_chunk_mut_word(a.key, child, q), lds_thr, v);
         }
       }
       // padding genes of the last chunk stay zero
@@ -226,7 +255,7 @@ __global__ __launch_bounds__(kBlock) void real_kernel(GenArgs a, unsigned long l
       } else if (tile_needed) {
         __syncthreads();
       }
-      if (valid && !elite) {
+      if (valid) {
         if (UFN) {
           // reference ABI: obj_f(gene*, unsigned) on the child's genome (LDS row)
           float s = 0.f;
@@ -285,13 +314,16 @@ __global__ __launch_bounds__(kBlock) void real_kernel(GenArgs a, unsigned long l
 // butterfly.  Element-wise objectives and Rosenbrock: the neighbour of a
 // segment's last gene is the next segment's first, so lane 63 defers that
 // term to the next segment (added before that segment's own terms: the CPU's
-// gene-order accumulation per lane).  Rotation (M is L x L), the reference-E3
-// random-key TSP (O(L^2)) and device function pointers stay <= 256 genes.
+// gene-order accumulation per lane).  Sparse mutation positions are listed
+// once per child in the wave's LDS (distinct by a wave-wide compare).
+// Rotation (M is L x L), the reference-E3 random-key TSP (O(L^2)) and device
+// function pointers stay <= 256 genes.
 // ---------------------------------------------------------------------------
 template <int MODE>
 __global__ __launch_bounds__(kBlock) void real_long_kernel(GenArgs a, unsigned long long* best_parts) {
   resolve_gen(a);
   __shared__ uint32_t lds_thr[kMutCap];
+  __shared__ uint32_t lds_mpos[kBlock / 64][kMutCap];
   __shared__ unsigned long long lds_red[kBlock / 64];
   __shared__ uint32_t lds_elite;
   constexpr uint32_t GS = 64, GPB = kBlock / 64;
@@ -301,18 +333,21 @@ __global__ __launch_bounds__(kBlock) void real_long_kernel(GenArgs a, unsigned l
   float4* nxt = (float4*)a.next;
   const uint32_t L = a.L, nchunks = a.chunks;
   constexpr bool MUTATES = MODE == MODE_GEN || MODE == MODE_MUTATE;
+  constexpr bool CROSSES = MODE == MODE_GEN || MODE == MODE_CROSS;
   constexpr bool EVALS = MODE == MODE_GEN || MODE == MODE_INIT || MODE == MODE_EVAL;
   const bool evals = EVALS && a.objective != OBJ_NONE;
-  const bool per_gene_mut = MUTATES && (a.mutation == MUT_GAUSSIAN || a.mutation == MUT_UNIFORM) && a.mut_rate > 0.f;
+  const bool per_gene = MUTATES && real_per_gene_mutation(a);
+  const bool sparse = per_gene && a.mut_sparse;
   const bool reset_one = MUTATES && a.mutation == MUT_RESET_ONE;
   const bool shift = (a.obj_i & 1) && a.obj_data2 && real_obj_rotatable(a.objective);
   const bool rosen = a.objective == OBJ_ROSENBROCK;
+  uint32_t* mpos = lds_mpos[g];
 
   if (MODE == MODE_GEN && a.n_elite > 0 && a.elite_idx == nullptr && blockIdx.x == 0) {
     unsigned long long b = block_reduce_parts(a.best_cur, a.n_best_cur, lds_red);
     if (threadIdx.x == 0) lds_elite = (uint32_t)best_index(b);
   }
-  if (per_gene_mut)
+  if (per_gene)
     for (uint32_t i = threadIdx.x; i < kMutCap; i += kBlock) lds_thr[i] = a.mut_thr[i];
   __syncthreads();
 
@@ -321,31 +356,28 @@ __global__ __launch_bounds__(kBlock) void real_long_kernel(GenArgs a, unsigned l
   for (uint64_t child = (uint64_t)blockIdx.x * GPB + g; child < a.S; child += (uint64_t)gridDim.x * GPB) {
     const bool elite = MODE == MODE_GEN && child < a.n_elite;  // wave-uniform
     const uint32_t src = elite ? (a.elite_idx ? a.elite_idx[child] : lds_elite) : 0u;
-    const bool breeds = !elite && (MODE == MODE_GEN || MODE == MODE_CROSS || MODE == MODE_MUTATE);
-    Pool<GS> pool{u32x4{0, 0, 0, 0}, 0u};
-    uint32_t pa = 0, pb = 0, blo = 0, bhi = 0, rpos = 0xFFFFFFFFu;
+    const u32x4 misc = (CROSSES || MUTATES) ? real_misc(a.key, child) : u32x4{0, 0, 0, 0};
+    uint32_t pa = 0, pb = 0, cut = 0, nm = 0;
     bool xo = false;
-    float ua = 0.f, rval = 0.f;
-    if (breeds) {
-      pool.w = draw(a.key, ST_CHILD, child, q);
-      if (MODE == MODE_GEN || MODE == MODE_CROSS) {
-        select_parents<GS>(a, pool, child, pa, pb);
-        xo = a.crossover != XO_NONE && do_crossover(a, pool.get(W_XOPROB, a.key, child));
-        if (a.crossover == XO_ONE_POINT) {
-          blo = word_to_index(pool.get(W_CUT1, a.key, child), L);
-          bhi = L;
-        } else if (a.crossover == XO_TWO_POINT) {
-          const uint32_t c1 = word_to_index(pool.get(W_CUT1, a.key, child), L);
-          const uint32_t c2 = word_to_index(pool.get(W_CUT2, a.key, child), L);
-          blo = c1 < c2 ? c1 : c2;
-          bhi = c1 < c2 ? c2 : c1;
-        } else if (a.crossover == XO_ARITHMETIC) {
-          ua = word_to_unit(pool.get(W_CUT1, a.key, child));
-        }
-      }
-      if (reset_one && pool.get(W_MUTIND, a.key, child) < a.mut_ind_thresh) {
-        rpos = word_to_index(pool.get(W_MUTPOS, a.key, child), L);
-        rval = real_reset_value(a, pool.get(W_SEL + sel_words(a), a.key, child));
+    if (CROSSES && !elite) {
+      st_select_parents(a, child, pa, pb);
+      xo = a.crossover != XO_NONE && do_crossover(a, misc.x);
+      cut = real_cut_word(a, misc);
+    }
+    if (MUTATES && !elite && (sparse || reset_one)) {
+      // the first K distinct positions (sequential definition), listed in LDS
+      nm = sparse ? binom_count(misc.w, lds_thr) : (misc.w < a.mut_ind_thresh ? 1u : 0u);
+      u32x4 blk{0u, 0u, 0u, 0u};
+      for (uint32_t n = 0, j = 0; n < nm;) {  // wave-uniform
+        if ((j & 3u) == 0u) blk = draw(a.key, ST_BMUT, child, j >> 2);
+        const uint32_t p = word_to_index(sel4(blk, j & 3u), L);
+        ++j;
+        bool dup = false;
+        for (uint32_t i = q; i < n; i += 64) dup |= mpos[i] == p;
+        if (__any(dup)) continue;
+        if (q == 0) mpos[n] = p;
+        wave_lds_sync();
+        ++n;
       }
     }
     RealAcc acc{0.f, 0.f, 1.f};
@@ -366,24 +398,26 @@ __global__ __launch_bounds__(kBlock) void real_long_kernel(GenArgs a, unsigned l
           const float4 e = cur[child * rs + c];
           v[0] = e.x; v[1] = e.y; v[2] = e.z; v[3] = e.w;
         }
-        if (breeds && (MODE == MODE_GEN || MODE == MODE_CROSS)) {
+        if (CROSSES && !elite) {
           const float4 A4 = cur[(uint64_t)pa * rs + c], B4 = cur[(uint64_t)pb * rs + c];
           const float A[4] = {A4.x, A4.y, A4.z, A4.w}, B[4] = {B4.x, B4.y, B4.z, B4.w};
-          real_cross_chunk(a, child, c, A, B, xo, blo, bhi, ua, v);
+          const uint32_t ub = (xo && a.crossover == XO_UNIFORM) ? real_uniform_bits(a.key, child, c) : 0u;
+          real_cross_chunk(a, child, c, A, B, xo, cut, ub, v);
         }
-        if (breeds && per_gene_mut) {
-          real_mutate_chunk(a, child, c, clen, c == q ? pool.w.w : chunk_mut_word(a.key, child, c), lds_thr, v);
-        } else if (breeds && (rpos >> 2) == c) {
-          const uint32_t j = rpos & 3u;
-          v[0] = j == 0 ? rval : v[0];
-          v[1] = j == 1 ? rval : v[1];
-          v[2] = j == 2 ? rval : v[2];
-          v[3] = j == 3 ? rval : v[3];
+        if (MUTATES && !elite) {
+          if (nm > 0) {
+            for (uint32_t i = 0; i < nm; ++i) {
+              const uint32_t p = mpos[i];
+              if ((p >> 2) == c) set_gene4(v, p & 3u, real_mut_apply(a, real_mut_draw(a, child, i), gene4(v, p & 3u)));
+            }
+          } else if (per_gene && !sparse) {
+            real_mutate_chunk(a, child, c, clen, bin_chunk_mut_word(a.key, child, c), lds_thr, v);
+          }
         }
         for (uint32_t j = 0; j < 4; ++j) v[j] = j < clen ? v[j] : 0.f;
         if (MODE != MODE_EVAL) nxt[child * rs + c] = make_float4(v[0], v[1], v[2], v[3]);
       }
-      if (evals && !elite) {
+      if (evals) {
         float x[4];
         for (uint32_t j = 0; j < 4; ++j) {
           const uint32_t d = 4 * c + j;
@@ -410,12 +444,13 @@ __global__ __launch_bounds__(kBlock) void real_long_kernel(GenArgs a, unsigned l
         }
       }
     }
+    if (MUTATES && nm > 0) wave_lds_sync();  // the list is rewritten for the next child
     float score = 0.f;
     if (evals) {
       acc.s0 = group_sum<GS>(acc.s0);
       acc.s1 = group_sum<GS>(acc.s1);
       acc.s2 = group_prod<GS>(acc.s2);
-      score = elite ? a.score_cur[src] : real_obj_finish(a, acc);
+      score = real_obj_finish(a, acc);
     }
     if (evals && q == 0) {
       a.score_next[child] = score;
@@ -461,274 +496,44 @@ uint32_t go(const GenArgs& a, unsigned long long* parts, hipStream_t s) {
   return launch_occ(real_kernel<GS, MODE, ROT, false>, kBlock / GS, lds, a, parts, s, c0);
 }
 
-
 // ---------------------------------------------------------------------------
-// Fast GEN path.  The generic kernel above walks one child per group per block
-// iteration through a strictly serial chain (pool draw -> 4 score loads ->
-// 2 parent-row loads -> crossover/mutation -> store -> objective), so with a
-// few waves per SIMD it is latency bound (rocprof: ~5.7 us per iteration,
-// 1.1 TB/s effective on Rastrigin-30D @ 1M).  Here every group carries U
-// children through each phase together: U x 4 tournament loads are in flight
-// at once, then U x 2 parent rows, then the U children are finished back to
-// back — U-fold memory-level parallelism per wave with no extra waves.
-// Semantics (RNG words, operators, elitism, MFMA order) are exactly the
-// generic kernel's, so rows stay bit-identical to the CPU reference.
-// Eligible: MODE_GEN, tournament-2 or random selection, built-in objectives
-// that need no neighbour dimension (not Rosenbrock without rotation, not
-// random-key TSP, not user fn-ptrs).
-template <int GS, int U, bool ROT>
-__global__ __launch_bounds__(kBlock) void real_gen_fast(GenArgs a, unsigned long long* best_parts) {
-  resolve_gen(a);
-  extern __shared__ __attribute__((aligned(16))) float smem[];
-  uint32_t* lds_thr = (uint32_t*)smem;
-  unsigned long long* lds_red = (unsigned long long*)(smem + 128);
-  uint32_t* lds_elite = (uint32_t*)(smem + 136);
-  constexpr uint32_t GPB = kBlock / GS;
-  constexpr uint32_t ROWS = GPB * U;
-  constexpr uint32_t XR = ROWS > 16 ? ROWS : 16;
-  constexpr uint32_t TW = (4 * GS > 16 ? 4 * GS : 16) + 1;
-  const uint32_t dp = ((4 * a.chunks + 15) / 16) * 16;
-  float* X = smem + kHdr;  // [XR][TW] shifted x (ROT)
-  float* Z = X + XR * TW;  // [XR][TW] rotated z (ROT)
-  float* MS = Z + XR * TW; // [dp][dp+1]
-
-  const uint32_t lane = lane_id();
-  const uint32_t q = lane & (GS - 1);
-  const uint32_t gbase = lane & ~(uint32_t)(GS - 1);
-  const uint32_t g = threadIdx.x / GS;
-  const uint64_t rs = a.row_words >> 2;
-  const float4* cur = (const float4*)a.cur;
-  float4* nxt = (float4*)a.next;
-  const uint32_t L = a.L;
-  const uint32_t S32 = (uint32_t)a.S;
-  const bool have = q < a.chunks;
-  const uint32_t qc = have ? q : a.chunks - 1;  // unconditional loads, clamped chunk
-  const uint32_t clen = have ? (L - 4 * q >= 4 ? 4u : L - 4 * q) : 0u;
-  const bool evals = a.objective != OBJ_NONE;
-  const bool tour2 = a.selection == SEL_TOURNAMENT;
-  const bool per_gene_mut = (a.mutation == MUT_GAUSSIAN || a.mutation == MUT_UNIFORM) && a.mut_rate > 0.f;
-  const bool reset_one = a.mutation == MUT_RESET_ONE;
-  const bool shift = (a.obj_i & 1) && a.obj_data2 && real_obj_rotatable(a.objective);
-
-  if (a.n_elite > 0 && a.elite_idx == nullptr && blockIdx.x == 0) {
-    unsigned long long b = block_reduce_parts(a.best_cur, a.n_best_cur, lds_red);
-    if (threadIdx.x == 0) *lds_elite = (uint32_t)best_index(b);
-  }
-  if (per_gene_mut)
-    for (uint32_t i = threadIdx.x; i < kMutCap; i += kBlock) lds_thr[i] = a.mut_thr[i];
-  if (ROT) {
-    for (uint32_t i = threadIdx.x; i < 2 * XR * TW; i += kBlock) X[i] = 0.f;
-    for (uint32_t i = threadIdx.x; i < dp * (dp + 1); i += kBlock) {
-      const uint32_t n = i / (dp + 1), k = i % (dp + 1);
-      MS[i] = (n < L && k < L) ? a.obj_data[n * L + k] : 0.f;
-    }
-  }
-  __syncthreads();
-
-  unsigned long long my_best = 0;
-  ScoreStats st;
-  for (uint64_t base = (uint64_t)blockIdx.x * ROWS; base < a.S; base += (uint64_t)gridDim.x * ROWS) {
-    uint64_t ch[U];
-    u32x4 pw[U];
-    uint32_t pa[U], pb[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      ch[u] = base + u * GPB + g;
-      pw[u] = draw(a.key, ST_CHILD, ch[u], q);
-    }
-    // ---- phase 1: selection (all U x 4 score loads in flight together) ----
-    if (tour2) {
-      uint32_t i0[U], i1[U], i2[U], i3[U];
-      float s0[U], s1[U], s2[U], s3[U];
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const Pool<GS> pool{pw[u], gbase};
-        i0[u] = word_to_index(pool.get(W_SEL + 0, a.key, ch[u]), S32);
-        i1[u] = word_to_index(pool.get(W_SEL + 1, a.key, ch[u]), S32);
-        i2[u] = word_to_index(pool.get(W_SEL + 2, a.key, ch[u]), S32);
-        i3[u] = word_to_index(pool.get(W_SEL + 3, a.key, ch[u]), S32);
-      }
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        s0[u] = a.score_cur[i0[u]];
-        s1[u] = a.score_cur[i1[u]];
-        s2[u] = a.score_cur[i2[u]];
-        s3[u] = a.score_cur[i3[u]];
-      }
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        pa[u] = (s0[u] < s1[u]) ? i1[u] : i0[u];
-        pb[u] = (s2[u] < s3[u]) ? i3[u] : i2[u];
-      }
-    } else {
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const Pool<GS> pool{pw[u], gbase};
-        pa[u] = word_to_index(pool.get(W_SEL + 0, a.key, ch[u]), S32);
-        pb[u] = word_to_index(pool.get(W_SEL + 1, a.key, ch[u]), S32);
-      }
-    }
-    bool el[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      el[u] = ch[u] < a.n_elite;
-      if (el[u]) {
-        pa[u] = a.elite_idx ? a.elite_idx[ch[u]] : *lds_elite;
-        pb[u] = pa[u];
-      }
-    }
-    // ---- phase 2: parent rows (U x 2 dwordx4 loads in flight) ----
-    float4 A4[U], B4[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      A4[u] = cur[(uint64_t)pa[u] * rs + qc];
-      B4[u] = cur[(uint64_t)pb[u] * rs + qc];
-    }
-    // ---- phase 3: variation + store ----
-    float v[U][4];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const float A[4] = {A4[u].x, A4[u].y, A4[u].z, A4[u].w}, B[4] = {B4[u].x, B4[u].y, B4[u].z, B4[u].w};
-      if (el[u]) {
-        for (int j = 0; j < 4; ++j) v[u][j] = A[j];
-      } else {
-        const Pool<GS> pool{pw[u], gbase};
-        const bool xo = a.crossover != XO_NONE && do_crossover(a, pool.get(W_XOPROB, a.key, ch[u]));
-        uint32_t blo = 0, bhi = 0;
-        float ua = 0.f;
-        if (a.crossover == XO_ONE_POINT) {
-          blo = word_to_index(pool.get(W_CUT1, a.key, ch[u]), L);
-          bhi = L;
-        } else if (a.crossover == XO_TWO_POINT) {
-          const uint32_t c1 = word_to_index(pool.get(W_CUT1, a.key, ch[u]), L);
-          const uint32_t c2 = word_to_index(pool.get(W_CUT2, a.key, ch[u]), L);
-          blo = c1 < c2 ? c1 : c2;
-          bhi = c1 < c2 ? c2 : c1;
-        } else if (a.crossover == XO_ARITHMETIC) {
-          ua = word_to_unit(pool.get(W_CUT1, a.key, ch[u]));
-        }
-        real_cross_chunk(a, ch[u], q, A, B, xo, blo, bhi, ua, v[u]);
-        if (per_gene_mut) {
-          if (have) real_mutate_chunk(a, ch[u], q, clen, pw[u].w, lds_thr, v[u]);
-        } else if (reset_one && pool.get(W_MUTIND, a.key, ch[u]) < a.mut_ind_thresh) {
-          const uint32_t pos = word_to_index(pool.get(W_MUTPOS, a.key, ch[u]), L);
-          const float x = real_reset_value(a, pool.get(W_SEL + sel_words(a), a.key, ch[u]));
-          if ((pos >> 2) == q) {
-            const uint32_t j = pos & 3u;
-            v[u][0] = j == 0 ? x : v[u][0];
-            v[u][1] = j == 1 ? x : v[u][1];
-            v[u][2] = j == 2 ? x : v[u][2];
-            v[u][3] = j == 3 ? x : v[u][3];
-          }
-        }
-      }
-      for (uint32_t j = 0; j < 4; ++j) v[u][j] = j < clen ? v[u][j] : 0.f;
-      if (ch[u] < a.S && have) nxt[ch[u] * rs + q] = make_float4(v[u][0], v[u][1], v[u][2], v[u][3]);
-    }
-    if (!evals) continue;
-    // ---- phase 4: objective (rotated: one MFMA pass over the U*GPB-row tile) ----
-    float z[U][4];
-#pragma unroll
-    for (int u = 0; u < U; ++u)
-      for (int j = 0; j < 4; ++j) {
-        const uint32_t d = 4 * q + j;
-        z[u][j] = d < L ? ((shift) ? v[u][j] - a.obj_data2[d] : v[u][j]) : 0.f;
-      }
-    if (ROT) {
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        float* row = X + (u * GPB + g) * TW + 4 * q;
-        row[0] = z[u][0]; row[1] = z[u][1]; row[2] = z[u][2]; row[3] = z[u][3];
-      }
-      __syncthreads();
-      const uint32_t w = threadIdx.x >> 6;
-      const uint32_t nct = dp / 16;
-      for (uint32_t t = w; t < (XR / 16) * nct; t += kBlock / 64) {
-        const uint32_t rt = t / nct, ct = t % nct;
-        floatx4 acc = {0.f, 0.f, 0.f, 0.f};
-        const float* xa = X + (rt * 16 + (lane & 15)) * TW + (lane >> 4);
-        const float* mb = MS + (ct * 16 + (lane & 15)) * (dp + 1) + (lane >> 4);
-        for (uint32_t k0 = 0; k0 < dp; k0 += 4) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(xa[k0], mb[k0], acc, 0, 0, 0);
-        float* zo = Z + (rt * 16 + (lane >> 4) * 4) * TW + ct * 16 + (lane & 15);
-        zo[0] = acc[0];
-        zo[TW] = acc[1];
-        zo[2 * TW] = acc[2];
-        zo[3 * TW] = acc[3];
-      }
-      __syncthreads();
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      float score;
-      if (el[u]) {
-        score = a.score_cur[pa[u]];
-      } else {
-        RealAcc acc{0.f, 0.f, 1.f};
-        const float* zrow = Z + (u * GPB + g) * TW + 4 * q;
-        for (uint32_t j = 0; j < 4; ++j) {
-          const uint32_t d = 4 * q + j;
-          if (d < L) {
-            const float zj = ROT ? zrow[j] : z[u][j];
-            const float zn = ROT ? zrow[j + 1] : 0.f;  // Rosenbrock only reaches here rotated
-            real_obj_term(a, d, zj, zn, v[u][j], acc);
-          }
-        }
-        acc.s0 = group_sum<GS>(acc.s0);
-        acc.s1 = group_sum<GS>(acc.s1);
-        acc.s2 = group_prod<GS>(acc.s2);
-        score = real_obj_finish(a, acc);
-      }
-      if (ch[u] < a.S && q == 0) {
-        a.score_next[ch[u]] = score;
-        const unsigned long long pb2 = pack_best(score, ch[u]);
-        my_best = pb2 > my_best ? pb2 : my_best;
-        st.add(score);
-      }
-    }
-    if (ROT) __syncthreads();  // X/Z are rewritten next iteration
-  }
-  if (evals && best_parts) {
-    unsigned long long b = block_max_u64(my_best, lds_red);
-    if (threadIdx.x == 0) best_parts[blockIdx.x] = b;
-    if (a.stats_parts) block_stats_store(st, a.stats_parts);
-  }
-}
-
-
-// ---------------------------------------------------------------------------
-// Software-pipelined GEN kernel, the REAL analogue of
-// binary_gen_pipe: three children per lane group in flight — contestant score
-// loads of c+2, parent-row loads of c+1 and the variation / objective of c in
-// one loop body, three static register sets rotating X -> Y -> Z so hipcc's
-// vmcnt waits stay exact (every load is issued unconditionally; tail children
-// are clamped, lanes without a chunk re-read the last chunk).  Tournament-2 or
-// random selection, any crossover / mutation, objectives that need no
-// neighbouring dimension.  Same semantics as real_kernel (bit-exact).
+// The hot generation kernel: transposed tournaments (the binary_gen_tp design,
+// binary.hip).  A wave owns a contiguous range of children and breeds
+// NG = 64/GS of them per STEP; steps come in BATCHES of GS steps = 64
+// children.  The range is cut into SEGMENTS of up to kSegBatches batches:
+//   TOURNAMENTS  tp_select_segment (tp.hpp): one lane per child, every f32
+//                score load of the segment in flight together
+//   BREED        per batch, RESOLVE (one lane per child): the misc block
+//                (crossover test, cut points / arithmetic u, mutation count
+//                K), the first min(K, 3) distinct mutation positions and
+//                their values (gaussian z by gauss_z) -> a 32-byte child
+//                RECORD in the wave's LDS ring (2 batches); per step: parent
+//                rows loaded one step ahead, crossover (BLX: one Philox block
+//                per lane), the record's mutations (K > 3: the group
+//                continues the sequence), objective, group butterfly, stores.
+// So a child costs 2 Philox blocks of child-level words computed once (not
+// one pool block per lane) plus BLX's per-gene uniforms, and the per-gene
+// mutation test is a K-position loop instead of a per-lane geometric search.
+// Every vector memory operation is unconditional (hipcc's s_waitcnt vmcnt
+// accounting otherwise assumes the fewest outstanding loads over all paths).
 //
-// ROT (GS 4 or 8, i.e. L <= 16 / 32): rotated objective f(M (x - o)) with the
-// rotation on the matrix cores, wave-local — no block barrier in the loop.
-// Per stage 3 the wave's 64/GS children are transposed through a private
-// 16 x 36 LDS tile, multiplied by M^T (rot_tile4), and the outputs go back
-// through the same tile to the lanes' own 4-gene chunks.  Same k-ordered
-// accumulation as real_gen_fast (bit-exact).  The loop condition is
-// wave-uniform here: every lane of the wave takes part in the tile even when
-// its own child is past S.  4 waves/SIMD (launch bounds; 3 without them:
-// rastrigin30_rot 211 -> 193 us/gen).
+// Record: [0] = {parent A, parent B, crossover plan word, meta}
+//         [1] = {3 positions (u8), mutation draws 0..2 (f32 bits)}
+// meta: K (8 bits) | next mutation word j (16 bits) << 8 | xo << 30 | elite << 31
+//
+// ROT (GS 4 or 8, L <= 32): rotated objective f(M (x - o)) on the matrix
+// cores, wave-local: the wave's 64/GS children are transposed through a
+// private 16 x 36 LDS tile and multiplied by M^T with v_mfma_f32_4x4x1_16b_f32
+// (rot_tile4: 16 independent 4x4 blocks = 64/GS children x 4 GS dims, no
+// wasted rows), the same k-ordered fma chain as the CPU reference.
+// ---------------------------------------------------------------------------
 constexpr uint32_t kRotTW = 36;  // tile row stride (floats): conflict-free column reads, 16-byte rows
 
-__device__ __forceinline__ void rot_wave_sync() {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
+__device__ __forceinline__ void rot_tile4_sync() { wave_lds_sync(); }
 
-// z (4 genes of this lane's chunk, shifted) -> rotated z, in place, with
-// v_mfma_f32_4x4x1_16b_f32 (16 independent 4x4 blocks, K = 1): the wave's
-// C = 64/GS children x DP = 4 GS dims are exactly 16 blocks (C/4 row groups x
-// GS column groups), so no tile row is wasted — a 16x16x4 tile leaves half its
-// rows empty at GS 8 and measured 4% slower (rastrigin30_rot 201 vs 193 us/gen).
-// One k per instruction: each output is the same sequential fma chain as the
-// CPU reference.  A = X[child][k] and B = M[n][k] come from LDS as dwordx4 runs
+// z (4 genes of this lane's chunk, shifted) -> rotated z, in place.  One k
+// per instruction: each output is the same sequential fma chain as the CPU
+// reference.  A = X[child][k] and B = M[n][k] come from LDS as dwordx4 runs
 // of 4 k (xw: this wave's tile, ms: the block's M tile, row stride kRotTW).
 template <int GS>
 __device__ __forceinline__ void rot_tile4(float* xw, const float* ms, float z[4]) {
@@ -739,7 +544,7 @@ __device__ __forceinline__ void rot_tile4(float* xw, const float* ms, float z[4]
   const uint32_t ca = 4 * rg + (lane & 3);   // A row (child) of this lane
   const uint32_t nb = 4 * cg + (lane & 3);   // B column (output dim) of this lane
   *(float4*)(xw + row * kRotTW + 4 * q) = make_float4(z[0], z[1], z[2], z[3]);
-  rot_wave_sync();
+  rot_tile4_sync();
   floatx4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int k4 = 0; k4 < DP / 4; ++k4) {
@@ -750,47 +555,54 @@ __device__ __forceinline__ void rot_tile4(float* xw, const float* ms, float z[4]
     acc = __builtin_amdgcn_mfma_f32_4x4x1f32(xa.z, mb.z, acc, 0, 0, 0);
     acc = __builtin_amdgcn_mfma_f32_4x4x1f32(xa.w, mb.w, acc, 0, 0, 0);
   }
-  rot_wave_sync();
+  rot_tile4_sync();
 #pragma unroll
   for (int i = 0; i < 4; ++i) xw[(4 * rg + i) * kRotTW + nb] = acc[i];
-  rot_wave_sync();
+  rot_tile4_sync();
   const float4 r = *(const float4*)(xw + row * kRotTW + 4 * q);
   z[0] = r.x;
   z[1] = r.y;
   z[2] = r.z;
   z[3] = r.w;
-  rot_wave_sync();
+  rot_tile4_sync();
 }
 
-template <int GS, int OBJ, bool ROT = false>
-__global__ __launch_bounds__(kBlock, ROT ? 4 : 1) void real_gen_pipe(GenArgs a, unsigned long long* best_parts) {
+#ifndef PGA_RTP_WAVES
+#define PGA_RTP_WAVES 4
+#endif
+
+template <int GS, int OBJ, bool ROT>
+__global__ __launch_bounds__(kBlock, PGA_RTP_WAVES) void real_gen_tp(GenArgs a, unsigned long long* best_parts) {
   static_assert(!ROT || GS == 4 || GS == 8, "wave-local rotation: 16 or 32 padded dims");
   resolve_gen(a);
   a.objective = OBJ;  // compile-time objective: the term switches fold away
-  __shared__ unsigned long long lds_red[kBlock / 64];
-  __shared__ uint32_t lds_elite;
+  constexpr uint32_t NW = kBlock / 64;
+  constexpr uint32_t NG = 64 / GS;  // children per wave per step
+  constexpr bool EVALS = OBJ != OBJ_NONE;
+  __shared__ uint4 lds_rec[NW][2][64][2];           // per wave: 2 batches x 64 records x 32 B
+  __shared__ uint2 lds_par[NW][kSegBatches * 64];  // per wave: the segment's (parent A, parent B)
   __shared__ uint32_t lds_thr[kMutCap];
-  __shared__ __attribute__((aligned(16))) float lds_rot[ROT ? (kBlock / 64 + 2) * 16 * kRotTW : 1];  // 4 wave tiles + M
+  __shared__ uint32_t lds_el[kTpMaxElite];  // elite sources
+  __shared__ unsigned long long lds_red[NW];
+  __shared__ __attribute__((aligned(16))) float lds_rot[ROT ? (NW + 2) * 16 * kRotTW : 1];  // wave tiles + M
 
-  const uint32_t lane = lane_id();
-  const uint32_t q = lane & (GS - 1);
-  const uint32_t gbase = lane & ~(uint32_t)(GS - 1);
-  constexpr uint32_t GPB = kBlock / GS;
-  const uint64_t rs = a.row_words >> 2;
+  const uint32_t lane = lane_id(), wid = threadIdx.x >> 6;
+  const uint32_t q = lane & (GS - 1), gbase = lane & ~(uint32_t)(GS - 1), g = lane / GS;
   const float4* cur = (const float4*)a.cur;
   float4* nxt = (float4*)a.next;
-  const uint32_t L = a.L;
-  const uint32_t S32 = (uint32_t)a.S;
+  const uint32_t L = a.L, S = (uint32_t)a.S;
   const bool have = q < a.chunks;
-  const uint32_t qc = have ? q : a.chunks - 1;
+  const uint32_t qq = have ? q : 0u;
   const uint32_t clen = have ? (L - 4 * q >= 4 ? 4u : L - 4 * q) : 0u;
-  const bool tour2 = a.selection == SEL_TOURNAMENT;
   const bool xo_on = a.crossover != XO_NONE;
-  const bool per_gene_mut = (a.mutation == MUT_GAUSSIAN || a.mutation == MUT_UNIFORM) && a.mut_rate > 0.f;
+  const bool uniform_xo = a.crossover == XO_UNIFORM;
+  const bool u_word0 = uniform_xo && L <= 32u;  // the record carries every chunk's mask bits
+  const bool per_gene = real_per_gene_mutation(a);
+  const bool dense = per_gene && !a.mut_sparse;
+  const bool sparse = per_gene && a.mut_sparse;
   const bool reset_one = a.mutation == MUT_RESET_ONE;
-  const bool evals = a.objective != OBJ_NONE;
-  const bool shift = (a.obj_i & 1) && a.obj_data2 && real_obj_rotatable(a.objective);
-  // loop-invariant per-lane problem data (no conditional loads inside the pipeline)
+  const bool shift = (a.obj_i & 1) && a.obj_data2 && real_obj_rotatable(OBJ);
+  // loop-invariant per-lane problem data
   float sh[4], w0[4], w1[4];
 #pragma unroll
   for (uint32_t j = 0; j < 4; ++j) {
@@ -798,257 +610,249 @@ __global__ __launch_bounds__(kBlock, ROT ? 4 : 1) void real_gen_pipe(GenArgs a, 
     sh[j] = (shift && d < L) ? a.obj_data2[d] : 0.f;
     w0[j] = 1.f;
     w1[j] = 0.f;
-    if (evals && d < L) real_obj_data(a, d, w0[j], w1[j]);
+    if (EVALS && d < L) real_obj_data(a, d, w0[j], w1[j]);
   }
-  float* xw = lds_rot + (ROT ? (threadIdx.x >> 6) * 16 * kRotTW : 0);  // this wave's X/Z tile
-  float* ms = lds_rot + (ROT ? (kBlock / 64) * 16 * kRotTW : 0);        // M[n][k], block-shared
+  // 32-bit offsets (the launcher checks (S + pad) rows < 4 GiB)
+  const uint32_t rb = a.row_words * 4u;
+#define RROW(base, row, ch) (*(float4*)((char*)(base) + ((uint32_t)(row) * rb + (uint32_t)(ch) * 16u)))
+#define RELEM(T, base, i) (*(T*)((char*)(base) + (uint32_t)(i) * (uint32_t)sizeof(T)))
+
+  uint32_t wbegin, wend;
+  tp_wave_range(S, NG, wbegin, wend);
+
+  float* xw = lds_rot + (ROT ? wid * 16 * kRotTW : 0);  // this wave's X/Z tile
+  float* ms = lds_rot + (ROT ? NW * 16 * kRotTW : 0);   // M[n][k], block-shared
   if (ROT)
     for (uint32_t i = threadIdx.x; i < 32 * kRotTW; i += kBlock) {
       const uint32_t n = i / kRotTW, k = i % kRotTW;
       ms[i] = (n < L && k < L) ? a.obj_data[n * L + k] : 0.f;
     }
-
-  if (a.n_elite > 0 && a.elite_idx == nullptr && blockIdx.x == 0) {
-    unsigned long long b = block_reduce_parts(a.best_cur, a.n_best_cur, lds_red);
-    if (threadIdx.x == 0) lds_elite = (uint32_t)best_index(b);
+  // elite sources of children [0, n_elite) for the blocks that hold any of them
+  {
+    uint32_t per = (uint32_t)((S + (uint64_t)gridDim.x * NW - 1) / ((uint64_t)gridDim.x * NW));
+    per = (per + NG - 1) / NG * NG;
+    if (a.n_elite > 0 && (uint64_t)blockIdx.x * NW * per < a.n_elite) {
+      if (a.elite_idx) {
+        for (uint32_t i = threadIdx.x; i < a.n_elite; i += kBlock) lds_el[i] = a.elite_idx[i];
+      } else {
+        unsigned long long b = block_reduce_parts(a.best_cur, a.n_best_cur, lds_red);
+        if (threadIdx.x == 0) lds_el[0] = (uint32_t)best_index(b);
+      }
+    }
   }
-  if (per_gene_mut)
+  if (per_gene)
     for (uint32_t i = threadIdx.x; i < kMutCap; i += kBlock) lds_thr[i] = a.mut_thr[i];
   __syncthreads();
 
   unsigned long long my_best = 0;
   ScoreStats st;
-  const uint64_t stride = (uint64_t)gridDim.x * GPB;
-  uint64_t c0 = (uint64_t)blockIdx.x * GPB + threadIdx.x / GS;
-  while (c0 < a.n_elite && c0 < a.S) {  // elites: copy row and score
-    const uint32_t src = a.elite_idx ? a.elite_idx[c0] : lds_elite;
-    if (have) nxt[c0 * rs + q] = cur[(uint64_t)src * rs + q];
-    const float sc = a.score_cur[src];
-    if (q == 0) {
-      a.score_next[c0] = sc;
-      const unsigned long long pb = pack_best(sc, c0);
-      my_best = pb > my_best ? pb : my_best;
-      st.add(sc);
+  uint4(*rec)[64][2] = lds_rec[wid];
+  uint2* par = lds_par[wid];
+  static_assert(sizeof(lds_rec[0]) >= kSegBatches * 64 * sizeof(uint4), "contestant staging");
+  for (uint32_t begin = wbegin; begin < wend; begin += kSegBatches * 64u) {  // wave-uniform
+    const uint32_t end = begin + kSegBatches * 64u < wend ? begin + kSegBatches * 64u : wend;
+    const uint32_t nsteps = (end - begin + NG - 1) / NG;
+    const uint32_t nbatch = (end - begin + 63) / 64;
+
+    // TOURNAMENTS of the whole segment (contestants wait in the record ring)
+    tp_select_segment<false>(a, begin, end, lane, &rec[0][0][0], par);
+
+    // RESOLVE: parents, crossover plan, mutation positions and draws of batch B -> records
+#define PGA_RTP_RESOLVE(B)                                                                                   \
+  {                                                                                                          \
+    const uint32_t tc = begin + (B) * 64u + lane;                                                            \
+    const uint32_t cc = tc < end ? tc : end - 1;                                                             \
+    const uint2 pp = par[(B) * 64u + lane];                                                                  \
+    uint32_t pa = pp.x;                                                                                      \
+    const u32x4 misc = real_misc<true>(a.key, cc);                                                           \
+    const bool elite = tc < a.n_elite;                                                                       \
+    const bool xo = !elite && xo_on && do_crossover(a, misc.x);                                              \
+    if (elite) pa = lds_el[tc];                                                                              \
+    const uint32_t pb = xo ? pp.y : pa;                                                                      \
+    uint32_t cut = real_cut_word(a, misc);                                                                   \
+    if (u_word0 && xo) cut = real_uniform_word0<true>(a.key, cc);                                            \
+    uint32_t K = 0;                                                                                          \
+    if (!elite && sparse) K = binom_count(misc.w, lds_thr);                                                  \
+    if (!elite && reset_one) K = misc.w < a.mut_ind_thresh ? 1u : 0u;                                        \
+    uint32_t posw = 0, jn = 0, d0 = 0, d1 = 0, d2 = 0;                                                       \
+    if (K > 0u) {                                                                                            \
+      const uint32_t kk = K < 3u ? K : 3u;                                                                   \
+      const u32x4 m0 = draw<true>(a.key, ST_BMUT, cc, 0);                                                    \
+      const uint32_t c0 = word_to_index(m0.x, L), c1 = word_to_index(m0.y, L), c2 = word_to_index(m0.z, L);  \
+      /* common case: the first kk candidates are distinct, hence the positions */                          \
+      const bool slow = (kk > 1u && c0 == c1) || (kk > 2u && (c2 == c0 || c2 == c1));                        \
+      posw = c0 | (c1 << 8) | (c2 << 16);                                                                    \
+      jn = kk;                                                                                               \
+      if (slow) {                                                                                            \
+        posw = c0;                                                                                           \
+        uint32_t n = 1, j = 1;                                                                               \
+        u32x4 blk = m0;                                                                                      \
+        while (n < kk) {                                                                                     \
+          if ((j & 3u) == 0u) blk = draw<true>(a.key, ST_BMUT, cc, j >> 2);                                  \
+          const uint32_t p = word_to_index(sel4(blk, j & 3u), L);                                            \
+          ++j;                                                                                               \
+          if (p == (posw & 0xFFu) || (n > 1u && p == ((posw >> 8) & 0xFFu))) continue;                       \
+          posw |= p << (8u * n);                                                                             \
+          ++n;                                                                                               \
+        }                                                                                                    \
+        jn = j;                                                                                              \
+      }                                                                                                      \
+      d0 = f2u(real_mut_draw<true>(a, cc, 0));                                                               \
+      if (kk > 1u) d1 = f2u(real_mut_draw<true>(a, cc, 1));                                                  \
+      if (kk > 2u) d2 = f2u(real_mut_draw<true>(a, cc, 2));                                                  \
+    }                                                                                                        \
+    const uint32_t meta =                                                                                    \
+        (K > 255u ? 255u : K) | ((jn > 0xFFFFu ? 0xFFFFu : jn) << 8) | (xo ? 1u << 30 : 0u) | (elite ? 1u << 31 : 0u); \
+    uint4(*r)[2] = rec[(B) & 1u];                                                                            \
+    r[lane][0] = make_uint4(pa, pb, cut, meta);                                                              \
+    r[lane][1] = make_uint4(posw, d0, d1, d2);                                                               \
+  }
+
+    // prologue: batch 0 resolved, rows of step 0 in flight
+    PGA_RTP_RESOLVE(0u)
+    float4 A0, B0, A1, B1;
+    {
+      const uint4 r = rec[0][g][0];
+      A0 = RROW(cur, r.x, qq);
+      B0 = RROW(cur, r.y, qq);
     }
-    c0 += stride;
+
+    // one STEP: every vector-memory operation is unconditional (the tail of
+    // the last wave writes the padding rows past S)
+#define PGA_RTP_STEP(t, XA, XB, YA, YB)                                                                     \
+  {                                                                                                         \
+    const uint32_t b = (t) / GS, i = (t) & (GS - 1);                                                        \
+    if ((((t) + 1) & (GS - 1)) == 0u && b + 1 < nbatch) PGA_RTP_RESOLVE(b + 1)                              \
+    {                                                                                                       \
+      /* parent rows of step t+1 (the last step re-reads its own) */                                        \
+      const uint32_t tn = (t) + 1 < nsteps ? (t) + 1 : (t);                                                 \
+      const uint4 r = rec[(tn / GS) & 1u][(tn & (GS - 1)) * NG + g][0];                                     \
+      YA = RROW(cur, r.x, qq);                                                                              \
+      YB = RROW(cur, r.y, qq);                                                                              \
+    }                                                                                                       \
+    const uint32_t c = begin + (t) * NG + g;                                                                \
+    const uint4 r0 = rec[b & 1u][i * NG + g][0];                                                            \
+    const uint32_t meta = r0.w;                                                                             \
+    const float A_[4] = {XA.x, XA.y, XA.z, XA.w}, B_[4] = {XB.x, XB.y, XB.z, XB.w};                         \
+    float v[4];                                                                                             \
+    {                                                                                                       \
+      uint32_t ub = 0;                                                                                      \
+      if (uniform_xo) ub = u_word0 ? (r0.z >> ((4u * q) & 31u)) & 0xFu : real_uniform_bits<true>(a.key, c, q); \
+      real_cross_chunk<true>(a, c, q, A_, B_, (meta >> 30) & 1u, r0.z, ub, v);                             \
+    }                                                                                                       \
+    const uint32_t K = meta & 0xFFu;                                                                        \
+    if (K > 0u) { /* group-uniform */                                                                       \
+      const uint4 r1 = rec[b & 1u][i * NG + g][1];                                                          \
+      uint32_t mm = 0;                                                                                      \
+      _Pragma("unroll") for (uint32_t k = 0; k < 3; ++k) {                                                  \
+        const uint32_t p = (r1.x >> (8u * k)) & 0xFFu;                                                      \
+        const uint32_t dk = k == 0 ? r1.y : (k == 1 ? r1.z : r1.w);                                         \
+        if (k < K && (p >> 2) == q) {                                                                       \
+          set_gene4(v, p & 3u, real_mut_apply(a, u2f(dk), gene4(v, p & 3u)));                               \
+          mm |= 1u << (p & 3u);                                                                             \
+        }                                                                                                   \
+      }                                                                                                     \
+      if (K > 3u) real_sparse_group<GS, true>(a, c, K, 3, (meta >> 8) & 0xFFFFu, mm, q, gbase, v);          \
+    } else if (dense && !(meta >> 31)) { /* elites are not mutated */                                       \
+      real_mutate_chunk(a, c, q, clen, bin_chunk_mut_word<true>(a.key, c, q), lds_thr, v);                  \
+    }                                                                                                       \
+    _Pragma("unroll") for (uint32_t j = 0; j < 4; ++j) v[j] = j < clen ? v[j] : 0.f;                        \
+    if (have) RROW(nxt, c, q) = make_float4(v[0], v[1], v[2], v[3]);                                        \
+    if constexpr (EVALS) {                                                                                  \
+      float z[4], zn[4];                                                                                    \
+      _Pragma("unroll") for (uint32_t j = 0; j < 4; ++j) z[j] = 4 * q + j < L ? v[j] - sh[j] : 0.f;         \
+      if constexpr (ROT) rot_tile4<GS>(xw, ms, z);                                                          \
+      zn[0] = z[1];                                                                                         \
+      zn[1] = z[2];                                                                                         \
+      zn[2] = z[3];                                                                                         \
+      zn[3] = OBJ == OBJ_ROSENBROCK ? __shfl(z[0], (int)lane + 1, 64) : 0.f;                                \
+      RealAcc acc{0.f, 0.f, 1.f};                                                                           \
+      _Pragma("unroll") for (uint32_t j = 0; j < 4; ++j) {                                                  \
+        if (j < clen) real_obj_term_w(a, 4 * q + j, z[j], zn[j], v[j], w0[j], w1[j], acc);                  \
+      }                                                                                                     \
+      acc.s0 = group_sum<GS>(acc.s0);                                                                       \
+      acc.s1 = group_sum<GS>(acc.s1);                                                                       \
+      acc.s2 = group_prod<GS>(acc.s2);                                                                      \
+      const float sc = real_obj_finish(a, acc);                                                             \
+      RELEM(float, a.score_next, c) = sc; /* every lane of the group stores the same score */              \
+      const unsigned long long pk = c < S ? pack_best(sc, c) : 0ull;                                        \
+      my_best = pk > my_best ? pk : my_best;                                                                \
+      st.add_if(q == 0u && c < S, sc);                                                                      \
+    }                                                                                                       \
   }
 
-#define R_SET(P)                                                      \
-  u32x4 P##w{0, 0, 0, 0};                                             \
-  uint32_t P##i0 = 0, P##i1 = 0, P##i2 = 0, P##i3 = 0;                \
-  float P##t0 = 0.f, P##t1 = 0.f, P##t2 = 0.f, P##t3 = 0.f;           \
-  float4 P##A = make_float4(0.f, 0.f, 0.f, 0.f), P##B = P##A;         \
-  bool P##xo = false;
-  R_SET(X)
-  R_SET(Y)
-  R_SET(Z)
-#undef R_SET
-
-#define R_STAGE1(c, P)                                                 \
-  {                                                                    \
-    const uint64_t cc_ = (c) < a.S ? (c) : a.S - 1;                    \
-    P##w = draw(a.key, ST_CHILD, cc_, q);                              \
-    const Pool<GS> pool_{P##w, gbase};                                 \
-    P##i0 = word_to_index(pool_.get(W_SEL + 0, a.key, cc_), S32);      \
-    P##i1 = word_to_index(pool_.get(W_SEL + 1, a.key, cc_), S32);      \
-    P##i2 = word_to_index(pool_.get(W_SEL + 2, a.key, cc_), S32);      \
-    P##i3 = word_to_index(pool_.get(W_SEL + 3, a.key, cc_), S32);      \
-    P##t0 = a.score_cur[P##i0];                                        \
-    P##t1 = a.score_cur[P##i1];                                        \
-    P##t2 = a.score_cur[P##i2];                                        \
-    P##t3 = a.score_cur[P##i3];                                        \
+    uint32_t t = 0;
+    for (; t + 1 < nsteps; t += 2) {  // static row-register rotation
+      PGA_RTP_STEP(t, A0, B0, A1, B1)
+      PGA_RTP_STEP(t + 1, A1, B1, A0, B0)
+    }
+    if (t < nsteps) PGA_RTP_STEP(t, A0, B0, A1, B1)
+#undef PGA_RTP_RESOLVE
+#undef PGA_RTP_STEP
   }
-
-#define R_STAGE2(c, P)                                                                          \
-  {                                                                                             \
-    const uint64_t cc_ = (c) < a.S ? (c) : a.S - 1;                                             \
-    uint32_t pa_, pb_;                                                                          \
-    if (tour2) {                                                                                \
-      pa_ = P##i0 ^ ((P##i0 ^ P##i1) & (0u - (uint32_t)(P##t0 < P##t1)));                       \
-      pb_ = P##i2 ^ ((P##i2 ^ P##i3) & (0u - (uint32_t)(P##t2 < P##t3)));                       \
-    } else {                                                                                    \
-      pa_ = P##i0;                                                                              \
-      pb_ = P##i1;                                                                              \
-    }                                                                                           \
-    const Pool<GS> pool_{P##w, gbase};                                                          \
-    P##xo = xo_on && do_crossover(a, pool_.get(W_XOPROB, a.key, cc_));                          \
-    P##A = cur[(uint64_t)pa_ * rs + qc];                                                        \
-    P##B = cur[(uint64_t)pb_ * rs + qc];                                                        \
-  }
-
-#define R_VARY(c, P)                                                                            \
-  const Pool<GS> pool_{P##w, gbase};                                                            \
-  uint32_t lo_ = 0, hi_ = 0;                                                                    \
-  float ua_ = 0.f;                                                                              \
-  if (a.crossover == XO_ONE_POINT) {                                                            \
-    lo_ = word_to_index(pool_.get(W_CUT1, a.key, (c)), L);                                      \
-    hi_ = L;                                                                                    \
-  } else if (a.crossover == XO_TWO_POINT) {                                                     \
-    const uint32_t x1_ = word_to_index(pool_.get(W_CUT1, a.key, (c)), L);                       \
-    const uint32_t x2_ = word_to_index(pool_.get(W_CUT2, a.key, (c)), L);                       \
-    lo_ = x1_ < x2_ ? x1_ : x2_;                                                                \
-    hi_ = x1_ < x2_ ? x2_ : x1_;                                                                \
-  } else if (a.crossover == XO_ARITHMETIC) {                                                    \
-    ua_ = word_to_unit(pool_.get(W_CUT1, a.key, (c)));                                          \
-  }                                                                                             \
-  const float A_[4] = {P##A.x, P##A.y, P##A.z, P##A.w};                                         \
-  const float B_[4] = {P##B.x, P##B.y, P##B.z, P##B.w};                                         \
-  real_cross_chunk(a, (c), q, A_, B_, P##xo, lo_, hi_, ua_, v_);                                \
-  if (per_gene_mut) {                                                                           \
-    if (have) real_mutate_chunk(a, (c), q, clen, P##w.w, lds_thr, v_);                          \
-  } else if (reset_one && pool_.get(W_MUTIND, a.key, (c)) < a.mut_ind_thresh) {                 \
-    const uint32_t pos_ = word_to_index(pool_.get(W_MUTPOS, a.key, (c)), L);                    \
-    const float x_ = real_reset_value(a, pool_.get(W_SEL + sel_words(a), a.key, (c)));          \
-    if ((pos_ >> 2) == q) {                                                                     \
-      v_[0] = fsel(pos_ == 4 * q + 0, x_, v_[0]);                                               \
-      v_[1] = fsel(pos_ == 4 * q + 1, x_, v_[1]);                                               \
-      v_[2] = fsel(pos_ == 4 * q + 2, x_, v_[2]);                                               \
-      v_[3] = fsel(pos_ == 4 * q + 3, x_, v_[3]);                                               \
-    }                                                                                           \
-  }                                                                                             \
-  for (uint32_t j = 0; j < 4; ++j) v_[j] = j < clen ? v_[j] : 0.f;                              \
-  if (have) nxt[(c) * rs + q] = make_float4(v_[0], v_[1], v_[2], v_[3]);
-
-#define R_EVAL(c, ZE, ZN)                                                                       \
-  {                                                                                             \
-    RealAcc acc_{0.f, 0.f, 1.f};                                                                \
-    _Pragma("unroll") for (uint32_t j = 0; j < 4; ++j) {                                        \
-      const uint32_t d_ = 4 * q + j;                                                            \
-      if (d_ < L) real_obj_term_w(a, d_, ZE, ZN, v_[j], w0[j], w1[j], acc_);                    \
-    }                                                                                           \
-    acc_.s0 = group_sum<GS>(acc_.s0);                                                           \
-    acc_.s1 = group_sum<GS>(acc_.s1);                                                           \
-    acc_.s2 = group_prod<GS>(acc_.s2);                                                          \
-    const float sc_ = real_obj_finish(a, acc_);                                                 \
-    if (q == 0) {                                                                               \
-      a.score_next[(c)] = sc_;                                                                  \
-      const unsigned long long pb_ = pack_best(sc_, (c));                                       \
-      my_best = pb_ > my_best ? pb_ : my_best;                                                  \
-      st.add(sc_);                                                                              \
-    }                                                                                           \
-  }
-
-#define R_STAGE3(c, P)                                                                               \
-  if constexpr (!ROT) {                                                                              \
-    if ((c) < a.S) {                                                                                 \
-      float v_[4];                                                                                   \
-      R_VARY(c, P)                                                                                   \
-      if (evals) R_EVAL(c, v_[j] - sh[j], 0.f)                                                       \
-    }                                                                                                \
-  } else { /* wave-uniform: every lane joins the rotation tile */                                    \
-    float v_[4] = {0.f, 0.f, 0.f, 0.f};                                                              \
-    const bool live_ = (c) < a.S;                                                                    \
-    if (live_) {                                                                                     \
-      R_VARY(c, P)                                                                                   \
-    }                                                                                                \
-    float z_[4], zn_[4];                                                                             \
-    _Pragma("unroll") for (uint32_t j = 0; j < 4; ++j) z_[j] = 4 * q + j < L ? v_[j] - sh[j] : 0.f;  \
-    rot_tile4<GS>(xw, ms, z_);                                                                       \
-    zn_[0] = z_[1];                                                                                  \
-    zn_[1] = z_[2];                                                                                  \
-    zn_[2] = z_[3];                                                                                  \
-    zn_[3] = OBJ == OBJ_ROSENBROCK ? __shfl(z_[0], (int)lane + 1, 64) : 0.f;                         \
-    if (live_) R_EVAL(c, z_[j], zn_[j])                                                              \
-  }
-
-  // ROT: a wave stays in the loop while any of its groups has a child left
-#define R_MORE(c) (ROT ? __any((c) < a.S) != 0 : (c) < a.S)
-  R_STAGE1(c0, X)
-  R_STAGE2(c0, X)
-  R_STAGE1(c0 + stride, Y)
-  while (R_MORE(c0)) {  // group-uniform (ROT: wave-uniform)
-    R_STAGE1(c0 + 2 * stride, Z)
-    R_STAGE2(c0 + stride, Y)
-    R_STAGE3(c0, X)
-    c0 += stride;
-    if (!R_MORE(c0)) break;
-    R_STAGE1(c0 + 2 * stride, X)
-    R_STAGE2(c0 + stride, Z)
-    R_STAGE3(c0, Y)
-    c0 += stride;
-    if (!R_MORE(c0)) break;
-    R_STAGE1(c0 + 2 * stride, Y)
-    R_STAGE2(c0 + stride, X)
-    R_STAGE3(c0, Z)
-    c0 += stride;
-  }
-#undef R_STAGE1
-#undef R_MORE
-#undef R_STAGE2
-#undef R_STAGE3
-#undef R_VARY
-#undef R_EVAL
-
-  if (evals && best_parts) {
-    unsigned long long b = block_max_u64(my_best, lds_red);
-    if (threadIdx.x == 0) best_parts[blockIdx.x] = b;
-    if (a.stats_parts) block_stats_store(st, a.stats_parts);
+#undef RROW
+#undef RELEM
+  if constexpr (EVALS) {
+    unsigned long long bb = block_max_u64(my_best, lds_red);
+    if (threadIdx.x == 0 && best_parts) best_parts[blockIdx.x] = bb;
+    if (best_parts && a.stats_parts) block_stats_store(st, a.stats_parts);
   }
 }
 
-template <int GS, int U, bool ROT>
-uint32_t go_fast(const GenArgs& a, unsigned long long* parts, hipStream_t s) {
-  constexpr uint32_t ROWS = (kBlock / GS) * U;
-  constexpr uint32_t XR = ROWS > 16 ? ROWS : 16;
-  constexpr uint32_t TW = (4 * GS > 16 ? 4 * GS : 16) + 1;
-  const uint32_t dp = ((4 * a.chunks + 15) / 16) * 16;
-  const size_t lds = (kHdr + (ROT ? 2 * XR * TW + (size_t)dp * (dp + 1) : 0)) * sizeof(float);
-  static bool c = false;
-  return launch_occ(real_gen_fast<GS, U, ROT>, ROWS, lds, a, parts, s, c);
+template <typename K>
+uint32_t go_tp(K kernel, const GenArgs& a, unsigned long long* parts, hipStream_t s) {
+  const uint32_t grid = launch_grid_occ(a.S, kBlock, (const void*)kernel);
+  hipLaunchKernelGGL(kernel, grid, kBlock, 0, s, a, parts);
+  return grid;
 }
 
-bool real_fast_eligible(int mode, const GenArgs& a, bool rot) {
-  if (mode != MODE_GEN || force_generic_kernels()) return false;
+bool real_tp_eligible(const GenArgs& a, uint32_t GS, bool rot) {
+  if (force_generic_kernels()) return false;
   if (a.objective == OBJ_USER_FNPTR || a.objective == OBJ_TSP_RANDOM_KEY) return false;
-  if (a.objective == OBJ_ROSENBROCK && !rot) return false;
-  if (!(a.selection == SEL_RANDOM || (a.selection == SEL_TOURNAMENT && a.tour_k == 2))) return false;
-  if (a.n_elite > 1 && a.elite_idx == nullptr) return false;
-  return true;
+  if (rot && GS != 4 && GS != 8) return false;
+  const bool sel_ok = (a.selection == SEL_TOURNAMENT && a.tour_k == 2) || a.selection == SEL_RANDOM ||
+                      (a.selection == SEL_RANK && a.rank_order != nullptr) ||
+                      (a.selection == SEL_ROULETTE && a.cumfit != nullptr);
+  if (!sel_ok) return false;
+  if (a.n_elite > kTpMaxElite || (a.n_elite > 1 && a.elite_idx == nullptr)) return false;
+  // 32-bit offsets: the (S + kRowPad)-row buffers must stay below 4 GiB
+  return (a.S + kRowPad) * (uint64_t)a.row_words * 4u <= 0xFFFFFFFFull;
 }
 
 template <int GS, bool ROT>
-uint32_t launch_fast(const GenArgs& a, unsigned long long* parts, hipStream_t s) {
-  if constexpr (ROT && (GS == 4 || GS == 8)) {
-    {
-      static bool c[6] = {false, false, false, false, false, false};
+uint32_t launch_tp(const GenArgs& a, unsigned long long* parts, hipStream_t s) {
+  if constexpr (ROT) {
+    if constexpr (GS == 4 || GS == 8) {
       switch (a.objective) {
-        case OBJ_SPHERE: return launch_occ(real_gen_pipe<GS, OBJ_SPHERE, true>, kBlock / GS, 0, a, parts, s, c[0]);
-        case OBJ_RASTRIGIN:
-          return launch_occ(real_gen_pipe<GS, OBJ_RASTRIGIN, true>, kBlock / GS, 0, a, parts, s, c[1]);
-        case OBJ_ROSENBROCK:
-          return launch_occ(real_gen_pipe<GS, OBJ_ROSENBROCK, true>, kBlock / GS, 0, a, parts, s, c[2]);
-        case OBJ_ACKLEY: return launch_occ(real_gen_pipe<GS, OBJ_ACKLEY, true>, kBlock / GS, 0, a, parts, s, c[3]);
-        case OBJ_GRIEWANK:
-          return launch_occ(real_gen_pipe<GS, OBJ_GRIEWANK, true>, kBlock / GS, 0, a, parts, s, c[4]);
-        case OBJ_SCHWEFEL:
-          return launch_occ(real_gen_pipe<GS, OBJ_SCHWEFEL, true>, kBlock / GS, 0, a, parts, s, c[5]);
-        default: break;
+        case OBJ_SPHERE: return go_tp(real_gen_tp<GS, OBJ_SPHERE, true>, a, parts, s);
+        case OBJ_RASTRIGIN: return go_tp(real_gen_tp<GS, OBJ_RASTRIGIN, true>, a, parts, s);
+        case OBJ_ROSENBROCK: return go_tp(real_gen_tp<GS, OBJ_ROSENBROCK, true>, a, parts, s);
+        case OBJ_ACKLEY: return go_tp(real_gen_tp<GS, OBJ_ACKLEY, true>, a, parts, s);
+        case OBJ_GRIEWANK: return go_tp(real_gen_tp<GS, OBJ_GRIEWANK, true>, a, parts, s);
+        default: return go_tp(real_gen_tp<GS, OBJ_SCHWEFEL, true>, a, parts, s);
       }
     }
-  }
-  if (!ROT) {
-    static bool c[8] = {false, false, false, false, false, false, false, false};
+    return 0;
+  } else {
     switch (a.objective) {
-      case OBJ_SPHERE: return launch_occ(real_gen_pipe<GS, OBJ_SPHERE>, kBlock / GS, 0, a, parts, s, c[0]);
-      case OBJ_RASTRIGIN: return launch_occ(real_gen_pipe<GS, OBJ_RASTRIGIN>, kBlock / GS, 0, a, parts, s, c[1]);
-      case OBJ_ACKLEY: return launch_occ(real_gen_pipe<GS, OBJ_ACKLEY>, kBlock / GS, 0, a, parts, s, c[2]);
-      case OBJ_GRIEWANK: return launch_occ(real_gen_pipe<GS, OBJ_GRIEWANK>, kBlock / GS, 0, a, parts, s, c[3]);
-      case OBJ_SCHWEFEL: return launch_occ(real_gen_pipe<GS, OBJ_SCHWEFEL>, kBlock / GS, 0, a, parts, s, c[4]);
-      case OBJ_LINEAR: return launch_occ(real_gen_pipe<GS, OBJ_LINEAR>, kBlock / GS, 0, a, parts, s, c[5]);
-      case OBJ_KNAPSACK_REAL:
-        return launch_occ(real_gen_pipe<GS, OBJ_KNAPSACK_REAL>, kBlock / GS, 0, a, parts, s, c[6]);
-      case OBJ_NONE: return launch_occ(real_gen_pipe<GS, OBJ_NONE>, kBlock / GS, 0, a, parts, s, c[7]);
-      default: break;  // Rosenbrock needs the neighbouring dimension: fast path below
+      case OBJ_SPHERE: return go_tp(real_gen_tp<GS, OBJ_SPHERE, false>, a, parts, s);
+      case OBJ_RASTRIGIN: return go_tp(real_gen_tp<GS, OBJ_RASTRIGIN, false>, a, parts, s);
+      case OBJ_ROSENBROCK: return go_tp(real_gen_tp<GS, OBJ_ROSENBROCK, false>, a, parts, s);
+      case OBJ_ACKLEY: return go_tp(real_gen_tp<GS, OBJ_ACKLEY, false>, a, parts, s);
+      case OBJ_GRIEWANK: return go_tp(real_gen_tp<GS, OBJ_GRIEWANK, false>, a, parts, s);
+      case OBJ_SCHWEFEL: return go_tp(real_gen_tp<GS, OBJ_SCHWEFEL, false>, a, parts, s);
+      case OBJ_LINEAR: return go_tp(real_gen_tp<GS, OBJ_LINEAR, false>, a, parts, s);
+      case OBJ_KNAPSACK_REAL: return go_tp(real_gen_tp<GS, OBJ_KNAPSACK_REAL, false>, a, parts, s);
+      default: return go_tp(real_gen_tp<GS, OBJ_NONE, false>, a, parts, s);
     }
   }
-  return go_fast<GS, 1, ROT>(a, parts, s);
 }
 
 template <int GS, bool ROT>
 uint32_t launch_mode(int mode, const GenArgs& a, unsigned long long* parts, hipStream_t s) {
   switch (mode) {
     case MODE_GEN:
-      if (real_fast_eligible(mode, a, ROT)) return launch_fast<GS, ROT>(a, parts, s);
+      if (real_tp_eligible(a, GS, ROT)) return launch_tp<GS, ROT>(a, parts, s);
       return go<GS, MODE_GEN, ROT>(a, parts, s);
     case MODE_INIT: return go<GS, MODE_INIT, ROT>(a, parts, s);
     case MODE_EVAL: return go<GS, MODE_EVAL, ROT>(a, parts, s);

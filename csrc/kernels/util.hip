@@ -411,7 +411,7 @@ __device__ __forceinline__ void topk_emit(const TopkMove& mv, uint32_t* idx_out,
 
 __global__ __launch_bounds__(kBlock) void topk16_hist_kernel(const uint16_t* k16, uint64_t S, uint32_t R, bool largest,
                                                              uint32_t* G, uint64_t* status, uint32_t n_status) {
-  extern __shared__ uint32_t hr[];
+  uint32_t* hr = (uint32_t*)pga_dyn_lds;
   // aggregate words and ticket counters of the topk16_select_kernel that follows
   for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < n_status; i += gridDim.x * kBlock) status[i] = 0;
   if (status && blockIdx.x == 0 && threadIdx.x < 2) ((uint32_t*)(status + n_status))[threadIdx.x] = 0;

@@ -15,6 +15,7 @@
 #include "pga/island.hpp"
 #include "pga/trace.hpp"
 #include "pga/ops.hpp"
+#include "pga/real_ops.hpp"
 
 namespace py = pybind11;
 using pga::Island;
@@ -109,10 +110,31 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   });
   m.def("perm_crossover", [](int op, const std::vector<uint16_t>& A, const std::vector<uint16_t>& B, uint32_t lo,
                              uint32_t hi) {
-    if (A.size() != B.size() || hi > A.size() || lo > hi) throw std::invalid_argument("perm_crossover: bad arguments");
+    if (A.empty() || A.size() != B.size() || hi > A.size() || lo > hi)
+      throw std::invalid_argument("perm_crossover: bad arguments");
+    // both parents must be permutations of [0, L): the operators index position
+    // maps by gene value
+    for (const auto* P : {&A, &B}) {
+      std::vector<char> seen(A.size(), 0);
+      for (uint16_t x : *P) {
+        if (x >= A.size() || seen[x]) throw std::invalid_argument("perm_crossover: parents must be permutations of [0, L)");
+        seen[x] = 1;
+      }
+    }
     std::vector<uint16_t> C(A.size());
     pga::cpu::perm_crossover(op, A.data(), B.data(), (uint32_t)A.size(), lo, hi, C.data());
     return C;
+  });
+  // the deterministic Box-Muller of the REAL gaussian mutation (real_ops.hpp)
+  m.def("gauss_z", [](uint32_t w1, uint32_t w2) { return pga::gauss_z(w1, w2); });
+  m.def("gauss_z_batch", [](torch::Tensor w) {
+    auto wc = w.to(torch::kInt64).contiguous();
+    TORCH_CHECK(wc.dim() == 2 && wc.size(1) == 2, "gauss_z_batch: [n, 2] words");
+    auto out = torch::empty({wc.size(0)}, torch::dtype(torch::kFloat32));
+    const int64_t* p = wc.data_ptr<int64_t>();
+    float* o = out.data_ptr<float>();
+    for (int64_t i = 0; i < wc.size(0); ++i) o[i] = pga::gauss_z((uint32_t)p[2 * i], (uint32_t)p[2 * i + 1]);
+    return out;
   });
   m.def("mut_table", [](float p, uint32_t L) {
     auto t = torch::empty({(int64_t)L}, torch::dtype(torch::kInt64));

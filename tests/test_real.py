@@ -92,6 +92,12 @@ def test_sum_genes_improves():
     assert ga.best_score() > s0 + 10
 
 
+# transcendental objectives: the device's v_cos_f32 / libm differ from the
+# host's by ulps, so scores agree to rounding; every other objective is exact
+TRANSCENDENTAL = {"rastrigin", "rastrigin_rot", "ackley", "griewank", "schwefel", "rastrigin_rot16", "rastrigin_rot11",
+                  "ackley_rot20", "griewank_rot32", "rastrigin_1024", "ackley_777_shift", "tsp_rk"}
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("name", list(PROBLEMS))
 def test_gpu_matches_cpu(name):
@@ -102,15 +108,103 @@ def test_gpu_matches_cpu(name):
     assert torch.equal(g.rows.cpu(), c.rows), "init rows differ"
     assert close(g.scores.cpu(), c.scores)
     assert close(p.reference_fitness(g.genomes().cpu()), g.scores.cpu())
-    # one generation from the SAME population: selection identical unless two
-    # scores are within an ulp; compare children gene-wise with tolerance
     g.run(1)
     c.run(1)
     torch.cuda.synchronize()
-    gg, cg = g.genomes().cpu(), c.genomes()
-    same_rows = torch.isclose(gg, cg, rtol=1e-4, atol=1e-4).all(-1).float().mean().item()
-    assert same_rows > 0.99
-    assert close(p.reference_fitness(gg), g.scores.cpu())
+    if name in TRANSCENDENTAL:
+        # selection is identical unless two contestants' scores lie within an ulp
+        same_rows = (g.rows.cpu() == c.rows).all(-1).float().mean().item()
+        assert same_rows > 0.995
+        assert close(g.scores.cpu(), c.scores) or same_rows < 1.0
+    else:
+        assert torch.equal(g.rows.cpu(), c.rows)
+        assert torch.equal(g.scores.cpu(), c.scores)
+    assert close(p.reference_fitness(g.genomes().cpu()), g.scores.cpu())
+
+
+# polynomial objectives through the transposed kernel (real_gen_tp): rows AND
+# scores equal the CPU backend's bit for bit, generation after generation
+EXACT = {
+    "sphere30": lambda: M.Sphere(30),          # GS 8, the Rastrigin-30D geometry
+    "rosen30": lambda: M.Rosenbrock(30),       # neighbour gene across lanes
+    "sum30": lambda: M.SumGenes(30),
+    "sphere30_rot": lambda: M.Sphere(30, rotate=True, shift=True, seed=2),  # wave-local MFMA rotation
+    "rosen13_rot": lambda: M.Rosenbrock(13, rotate=True, seed=3),          # GS 4 rotation
+    "sphere100": lambda: M.Sphere(100),        # GS 32
+    "sphere256": lambda: M.Sphere(256),        # GS 64, every lane a chunk
+    "sphere3": lambda: M.Sphere(3),            # GS 1
+    "knap": lambda: M.ReferenceKnapsack(),     # GS 2, reference E2
+}
+
+
+def _exact_pair(p, S, gens, **kw):
+    g = pga.GeneticAlgorithm(p, S, device="cuda:0", **kw)
+    c = pga.GeneticAlgorithm(p, S, device="cpu", **kw)
+    for k in range(gens):
+        g.run(1)
+        c.run(1)
+        torch.cuda.synchronize()
+        assert torch.equal(g.rows.cpu(), c.rows), f"rows differ after generation {k + 1}"
+        assert torch.equal(g.scores.cpu(), c.scores), f"scores differ after generation {k + 1}"
+    assert close(p.reference_fitness(g.genomes().cpu()), g.scores.cpu())
+    return g, c
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("xo", ["uniform", "blend", "arithmetic", "one_point", "two_point", "none"])
+@pytest.mark.parametrize("mut", ["gaussian", "uniform", "reset_one", "none"])
+def test_gpu_tp_bitexact_operators(xo, mut):
+    """Sphere-30 (the BASELINE config 3 geometry): every crossover x mutation,
+    3 generations, children and scores bit for bit vs the CPU backend."""
+    _exact_pair(M.Sphere(30), 3000, 3, seed=21, elitism=1, crossover=xo, mutation=mut)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", list(EXACT))
+def test_gpu_tp_bitexact_geometries(name):
+    p = EXACT[name]()
+    for mut in ("gaussian", "reset_one"):
+        _exact_pair(p, 2500, 3, seed=5, elitism=3, crossover="blend", mutation=mut)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("sel", ["random", "rank", "tournament3", "roulette"])
+def test_gpu_real_selections_bitexact(sel):
+    """rank / random through the transposed kernel, tournament-3 through the
+    generic one; roulette on integer scores (exact prefix sums)."""
+    kw = dict(seed=8, elitism=1, crossover="two_point", mutation="gaussian")
+    if sel == "tournament3":
+        kw.update(selection="tournament", tournament_k=3)
+    else:
+        kw.update(selection=sel)
+    p = M.ReferenceKnapsack() if sel == "roulette" else M.Rosenbrock(30)
+    _exact_pair(p, 3000, 3, **kw)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("rate", [0.2, 0.06])
+def test_gpu_real_dense_and_many_flips_bitexact(rate):
+    """rate 0.2 (L p = 6): the dense per-chunk sampler; rate 0.06 (L p = 1.8
+    > 1.5 too) and, below, 1.4/30: sparse with K > 3 continuing in the group."""
+    _exact_pair(M.Sphere(30), 3000, 3, seed=3, elitism=1, crossover="blend", mutation="gaussian", mutation_rate=rate)
+    _exact_pair(M.Sphere(30), 3000, 3, seed=4, elitism=1, crossover="uniform", mutation="uniform",
+                mutation_rate=1.4 / 30)
+
+
+@pytest.mark.gpu
+def test_gpu_rastrigin30_tp_1m():
+    """BASELINE config 3 (plain): pop 1M through real_gen_tp; rows from a
+    shared population equal the CPU's, scores match the torch fp32 oracle."""
+    p = M.Rastrigin(30)
+    ga = pga.GeneticAlgorithm(p, 1 << 20, seed=1, device="cuda:0", elitism=1)
+    b0 = ga.best_score()
+    ga.run(20)
+    torch.cuda.synchronize()
+    idx = torch.randint(0, 1 << 20, (8192,), device="cuda:0")
+    assert close(p.reference_fitness(ga.genomes()[idx]), ga.scores[idx], rel=1e-4, abs_=5e-3)
+    assert ga.best_score() > b0
+    s = ga.stats()
+    assert s["min"] <= s["mean"] <= s["max"] == ga.best_score()
 
 
 @pytest.mark.gpu
@@ -131,9 +225,8 @@ def test_gpu_rastrigin30_rotated_mfma_1m():
 @pytest.mark.parametrize("xo", ["uniform", "one_point", "blend"])
 @pytest.mark.parametrize("mut", ["gaussian", "uniform", "reset_one"])
 def test_gpu_long_genome_bitexact_rows(xo, mut):
-    """Sphere-1000 / sum-1024: the long-genome kernel's children equal the
-    CPU backend's bit for bit over several generations (gaussian mutation:
-    to libm tolerance), scores to float rounding."""
+    """Sphere-1000 / sum-1024: the long-genome kernel's children and scores
+    equal the CPU backend's bit for bit over several generations."""
     for p in (M.Sphere(1000), M.SumGenes(1024)):
         kw = dict(seed=13, elitism=1, crossover=xo, mutation=mut)
         g = pga.GeneticAlgorithm(p, 512, device="cuda:0", **kw)
@@ -141,10 +234,40 @@ def test_gpu_long_genome_bitexact_rows(xo, mut):
         g.run(3)
         c.run(3)
         torch.cuda.synchronize()
-        if mut == "gaussian":  # Box-Muller: device and host libm differ by ulps
-            same = torch.isclose(g.genomes().cpu(), c.genomes(), rtol=1e-4, atol=1e-4).all(-1).float().mean()
-            assert same.item() > 0.99
-            assert close(p.reference_fitness(g.genomes().cpu()), g.scores.cpu())
-        else:  # children bit for bit; scores to rounding (the device contracts a*b+c into fma)
-            assert torch.equal(g.rows.cpu(), c.rows)
-            assert close(g.scores.cpu(), c.scores, rel=1e-5, abs_=1e-2)
+        # children bit for bit (gaussian too: real_ops.hpp gauss_z), scores too
+        assert torch.equal(g.rows.cpu(), c.rows)
+        assert torch.equal(g.scores.cpu(), c.scores)
+
+
+def test_gauss_z_deterministic_normal():
+    """The REAL gaussian mutation's Box-Muller (integer range reduction +
+    fma polynomials, identical on host and device): close to the float64
+    transform of the same words and N(0, 1) in distribution."""
+    from libpga_amd._ext import C
+    g = torch.Generator().manual_seed(0)
+    w = torch.randint(0, 1 << 32, (200000, 2), generator=g, dtype=torch.int64)
+    z = C.gauss_z_batch(w).double()
+    u1 = ((w[:, 0] >> 8) + 1).double() / 16777216.0
+    u2 = ((w[:, 1] >> 8) + 1).double() / 16777216.0
+    ref = torch.sqrt(-2.0 * torch.log(u1)) * torch.cos(2.0 * torch.pi * u2)
+    assert float((z - ref).abs().max()) < 2e-5
+    assert abs(float(z.mean())) < 0.01 and abs(float(z.std()) - 1.0) < 0.01
+    k = float(((z - z.mean()) ** 4).mean() / z.var() ** 2)
+    assert abs(k - 3.0) < 0.05  # kurtosis of a normal
+    assert C.gauss_z(0xFFFFFFFF, 0) == 0.0 or abs(C.gauss_z(0xFFFFFFFF, 0)) < 1e-6  # u1 = 1: radius 0
+
+
+def test_cpu_sparse_mutation_rate():
+    """Sparse per-gene uniform mutation: mutated genes per child ~ Binomial(L, p)."""
+    p = M.Sphere(30)
+    ga = pga.GeneticAlgorithm(p, 4000, seed=11, device="cpu", crossover="none", mutation="uniform",
+                              selection="random", mutation_rate=1.0 / 30)
+    before = ga.genomes().clone()
+    ga.run(1)
+    after = ga.genomes()
+    # with crossover none and random selection every child is a copy of some
+    # parent plus its mutations: count genes that match no parent gene value
+    vals = set(before.flatten().tolist())
+    changed = sum(1 for x in after.flatten().tolist() if x not in vals)
+    mean = changed / 4000
+    assert 0.9 < mean < 1.1  # E[K] = L p = 1
