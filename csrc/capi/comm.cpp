@@ -107,17 +107,35 @@ class LoopbackComm final : public Comm {
 
   bool wait(std::vector<LocalRank>&, double) override { return !failed_; }
 
-  std::vector<float> allgather(const std::vector<LocalRank>& local, const std::vector<float>& mine) override {
-    std::vector<float> all(n_, 0.f);
-    for (size_t i = 0; i < local.size(); ++i) all[local[i].rank] = mine[i];
-    return all;
+  bool allgather(const std::vector<LocalRank>& local, const std::vector<uint32_t>& mine, uint32_t count,
+                 std::vector<uint32_t>& all, double) override {
+    if (count == 0 || count > kGatherMaxWords) throw std::invalid_argument("allgather: bad word count");
+    all.assign((size_t)n_ * count, 0u);
+    for (size_t i = 0; i < local.size(); ++i)
+      std::memcpy(&all[(size_t)local[i].rank * count], &mine[i * count], 4ull * count);
+    return true;
+  }
+
+  bool broadcast(const std::vector<LocalRank>& local, const std::vector<void*>& bufs, size_t bytes, int root,
+                 double) override {
+    size_t r = local.size();
+    for (size_t i = 0; i < local.size(); ++i)
+      if (local[i].rank == root) r = i;
+    if (r == local.size()) throw std::runtime_error("loopback broadcast: root not driven by this call");
+    for (const LocalRank& l : local)
+      if (l.device >= 0) PGA_COMM_HIP(hipStreamSynchronize(l.stream));
+    for (size_t i = 0; i < local.size(); ++i) {
+      if (i == r) continue;
+      if (local[i].device < 0 && local[r].device < 0) std::memcpy(bufs[i], bufs[r], bytes);
+      else PGA_COMM_HIP(hipMemcpy(bufs[i], bufs[r], bytes, hipMemcpyDefault));
+    }
+    return true;
   }
 
   void set_fault(int every, int mode) override {
     if (mode < 0 || mode > 2) throw std::invalid_argument("loopback fault mode must be 0 (none), 1 (drop) or 2 (corrupt)");
     every_ = every;
     mode_ = mode;
-    self_exchange = true;
   }
 
  private:

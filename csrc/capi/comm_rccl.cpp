@@ -46,12 +46,19 @@ class RcclComm final : public Comm {
       : comms_(std::move(comms)), ranks_(std::move(ranks)), n_(nranks), all_(all) {
     ready_.resize(comms_.size(), nullptr);
     done_.resize(comms_.size(), nullptr);
+    ag_done_.resize(comms_.size(), nullptr);
     streams_.resize(comms_.size(), nullptr);
+    ag_dev_.resize(comms_.size(), nullptr);
+    ag_host_.resize(comms_.size(), nullptr);
   }
   ~RcclComm() override {
-    for (auto* v : {&ready_, &done_})
+    for (auto* v : {&ready_, &done_, &ag_done_})
       for (hipEvent_t e : *v)
         if (e) (void)hipEventDestroy(e);
+    for (uint32_t* b : ag_dev_)
+      if (b) (void)hipFree(b);
+    for (uint32_t* b : ag_host_)
+      if (b) (void)hipHostFree(b);
     if (!aborted_)
       for (ncclComm_t c : comms_)
         if (c) (void)ncclCommDestroy(c);
@@ -66,10 +73,10 @@ class RcclComm final : public Comm {
   bool drives_all_ranks() const override { return all_; }
 
   void set_fault(int every, int mode) override {
-    if (mode != 0 && mode != 3) throw std::invalid_argument("RCCL fault mode must be 0 (none) or 3 (withhold sends)");
+    if (mode != 0 && mode != 3 && mode != 4)
+      throw std::invalid_argument("RCCL fault mode must be 0 (none), 3 (withhold sends) or 4 (stall all-gathers)");
     every_ = every;
     mode_ = mode;
-    self_exchange = true;
   }
 
   // The emigrants are packed on each rank's compute stream; the transfers
@@ -80,13 +87,7 @@ class RcclComm final : public Comm {
     ++count_;
     const bool withhold = mode_ == 3 && every_ > 0 && count_ % (uint64_t)every_ == 0;
     for (LocalRank& l : local) {
-      const size_t j = slot_of(l.rank);
-      PGA_COMM_HIP(hipSetDevice(l.device));
-      if (!streams_[j]) {
-        PGA_COMM_HIP(hipStreamCreateWithFlags(&streams_[j], hipStreamNonBlocking));
-        PGA_COMM_HIP(hipEventCreateWithFlags(&ready_[j], hipEventDisableTiming));
-        PGA_COMM_HIP(hipEventCreateWithFlags(&done_[j], hipEventDisableTiming));
-      }
+      const size_t j = ensure_stream(l);
       PGA_COMM_HIP(hipEventRecord(ready_[j], l.stream));
       PGA_COMM_HIP(hipStreamWaitEvent(streams_[j], ready_[j], 0));
     }
@@ -127,20 +128,7 @@ class RcclComm final : public Comm {
   bool wait(std::vector<LocalRank>& local, double timeout_s) override {
     if (aborted_) return false;
     if (timeout_s > 0) {
-      const auto t0 = std::chrono::steady_clock::now();
-      for (;;) {
-        bool done = true;
-        for (const LocalRank& l : local) {
-          const hipError_t q = hipEventQuery(done_[slot_of(l.rank)]);
-          if (q == hipErrorNotReady) done = false;
-          else if (q != hipSuccess) return abort_all();
-        }
-        if (async_error()) return abort_all();
-        if (done) break;
-        const double dt = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-        if (dt > timeout_s) return abort_all();
-        std::this_thread::sleep_for(std::chrono::microseconds(50));
-      }
+      if (!poll(local, done_, timeout_s)) return abort_all();
     } else if (async_error()) {
       return abort_all();
     }
@@ -151,30 +139,121 @@ class RcclComm final : public Comm {
     return true;
   }
 
-  std::vector<float> allgather(const std::vector<LocalRank>& local, const std::vector<float>& mine) override {
-    std::vector<float> all(n_, 0.f);
-    std::vector<float*> dbuf(local.size(), nullptr);
+  // The words travel host -> pinned staging -> device -> ncclAllGather ->
+  // device -> pinned staging, all on the rank's communication stream (nothing
+  // waits for the compute stream, so a gather never queues behind the
+  // generation kernels), then the host polls the completion like wait().
+  bool allgather(const std::vector<LocalRank>& local, const std::vector<uint32_t>& mine, uint32_t count,
+                 std::vector<uint32_t>& all, double timeout_s) override {
+    if (count == 0 || count > kGatherMaxWords) throw std::invalid_argument("allgather: bad word count");
+    if (aborted_) return false;
+    const size_t words = (size_t)n_ * count;
+    ++ag_count_;
+    const bool stall = mode_ == 4 && every_ > 0 && ag_count_ % (uint64_t)every_ == 0;
     for (size_t i = 0; i < local.size(); ++i) {
-      PGA_COMM_HIP(hipSetDevice(local[i].device));
-      PGA_COMM_HIP(hipMalloc(&dbuf[i], sizeof(float) * (n_ + 1)));
-      PGA_COMM_HIP(hipMemcpyAsync(dbuf[i] + n_, &mine[i], sizeof(float), hipMemcpyHostToDevice, local[i].stream));
+      const size_t j = ensure_stream(local[i]);
+      if (!ag_dev_[j]) {
+        PGA_COMM_HIP(hipMalloc(&ag_dev_[j], 4ull * (n_ + 2) * kGatherMaxWords));
+        PGA_COMM_HIP(hipHostMalloc(&ag_host_[j], 4ull * (n_ + 1) * kGatherMaxWords, hipHostMallocDefault));
+      }
+      std::memcpy(ag_host_[j] + words, &mine[i * count], 4ull * count);
+      PGA_COMM_HIP(hipMemcpyAsync(ag_dev_[j] + words, ag_host_[j] + words, 4ull * count, hipMemcpyHostToDevice,
+                                  streams_[j]));
+    }
+    if (stall) {
+      // test fault: a receive nobody sends, ahead of the all-gather on the
+      // communication stream -- a peer that died between two check points
+      Group g;
+      for (const LocalRank& l : local) {
+        const size_t j = slot_of(l.rank);
+        nccl_check(ncclRecv(ag_dev_[j] + (n_ + 1) * kGatherMaxWords, 1, ncclUint32, ranks_[j], comms_[j], streams_[j]),
+                   "ncclRecv");
+      }
     }
     {
       Group g;
-      for (size_t i = 0; i < local.size(); ++i)
-        nccl_check(ncclAllGather(dbuf[i] + n_, dbuf[i], 1, ncclFloat32, comm_of(local[i].rank), local[i].stream),
+      for (const LocalRank& l : local) {
+        const size_t j = slot_of(l.rank);
+        nccl_check(ncclAllGather(ag_dev_[j] + words, ag_dev_[j], count, ncclUint32, comms_[j], streams_[j]),
                    "ncclAllGather");
+      }
     }
-    for (size_t i = 0; i < local.size(); ++i) {
-      PGA_COMM_HIP(hipSetDevice(local[i].device));
-      PGA_COMM_HIP(hipMemcpyAsync(all.data(), dbuf[i], sizeof(float) * n_, hipMemcpyDeviceToHost, local[i].stream));
-      PGA_COMM_HIP(hipStreamSynchronize(local[i].stream));
-      PGA_COMM_HIP(hipFree(dbuf[i]));
+    for (const LocalRank& l : local) {
+      const size_t j = slot_of(l.rank);
+      PGA_COMM_HIP(hipSetDevice(l.device));
+      PGA_COMM_HIP(hipMemcpyAsync(ag_host_[j], ag_dev_[j], 4ull * words, hipMemcpyDeviceToHost, streams_[j]));
+      PGA_COMM_HIP(hipEventRecord(ag_done_[j], streams_[j]));
     }
-    return all;
+    if (!poll(local, ag_done_, timeout_s)) return abort_all();
+    all.assign(ag_host_[slot_of(local[0].rank)], ag_host_[slot_of(local[0].rank)] + words);
+    return true;
+  }
+
+  bool broadcast(const std::vector<LocalRank>& local, const std::vector<void*>& bufs, size_t bytes, int root,
+                 double timeout_s) override {
+    if (aborted_) return false;
+    for (const LocalRank& l : local) {
+      const size_t j = ensure_stream(l);
+      PGA_COMM_HIP(hipEventRecord(ready_[j], l.stream));
+      PGA_COMM_HIP(hipStreamWaitEvent(streams_[j], ready_[j], 0));
+    }
+    {
+      Group g;
+      for (size_t i = 0; i < local.size(); ++i) {
+        const size_t j = slot_of(local[i].rank);
+        nccl_check(ncclBroadcast(bufs[i], bufs[i], bytes, ncclUint8, root, comms_[j], streams_[j]), "ncclBroadcast");
+      }
+    }
+    for (const LocalRank& l : local) {
+      const size_t j = slot_of(l.rank);
+      PGA_COMM_HIP(hipSetDevice(l.device));
+      PGA_COMM_HIP(hipEventRecord(done_[j], streams_[j]));
+    }
+    if (!poll(local, done_, timeout_s)) return abort_all();
+    for (const LocalRank& l : local) {
+      PGA_COMM_HIP(hipSetDevice(l.device));
+      PGA_COMM_HIP(hipStreamWaitEvent(l.stream, done_[slot_of(l.rank)], 0));
+    }
+    return true;
   }
 
  private:
+  // the local rank's communication stream and events (created on first use)
+  size_t ensure_stream(const LocalRank& l) {
+    const size_t j = slot_of(l.rank);
+    PGA_COMM_HIP(hipSetDevice(l.device));
+    if (!streams_[j]) {
+      PGA_COMM_HIP(hipStreamCreateWithFlags(&streams_[j], hipStreamNonBlocking));
+      PGA_COMM_HIP(hipEventCreateWithFlags(&ready_[j], hipEventDisableTiming));
+      PGA_COMM_HIP(hipEventCreateWithFlags(&done_[j], hipEventDisableTiming));
+      PGA_COMM_HIP(hipEventCreateWithFlags(&ag_done_[j], hipEventDisableTiming));
+    }
+    return j;
+  }
+  // completion of ev[slot] for every local rank.  timeout_s > 0: host poll
+  // with the deadline, RCCL's asynchronous error state checked every round;
+  // otherwise a blocking wait.  false: failed or expired (caller aborts).
+  bool poll(const std::vector<LocalRank>& local, const std::vector<hipEvent_t>& ev, double timeout_s) {
+    if (timeout_s <= 0) {
+      for (const LocalRank& l : local)
+        if (hipEventSynchronize(ev[slot_of(l.rank)]) != hipSuccess) return false;
+      return !async_error();
+    }
+    const auto t0 = std::chrono::steady_clock::now();
+    for (;;) {
+      bool done = true;
+      for (const LocalRank& l : local) {
+        const hipError_t q = hipEventQuery(ev[slot_of(l.rank)]);
+        if (q == hipErrorNotReady) done = false;
+        else if (q != hipSuccess) return false;
+      }
+      if (async_error()) return false;
+      if (done) return true;
+      const double dt = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+      if (dt > timeout_s) return false;
+      std::this_thread::sleep_for(std::chrono::microseconds(50));
+    }
+  }
   size_t slot_of(int rank) const {
     for (size_t i = 0; i < ranks_.size(); ++i)
       if (ranks_[i] == rank) return i;
@@ -198,12 +277,13 @@ class RcclComm final : public Comm {
 
   std::vector<ncclComm_t> comms_;
   std::vector<int> ranks_;
-  std::vector<hipEvent_t> ready_, done_;
+  std::vector<hipEvent_t> ready_, done_, ag_done_;
   std::vector<hipStream_t> streams_;  // one communication stream per local rank
+  std::vector<uint32_t*> ag_dev_, ag_host_;  // all-gather staging: (n + 1) x kGatherMaxWords words
   int n_;
   bool all_;
   bool aborted_ = false;
-  uint64_t count_ = 0;
+  uint64_t count_ = 0, ag_count_ = 0;
   int every_ = 0, mode_ = 0;
 };
 

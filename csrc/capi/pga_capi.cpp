@@ -90,6 +90,12 @@ struct pga_solver {
   float* mig_send_scores = nullptr;
   float* mig_recv_scores = nullptr;
   uint32_t mig_cap = 0;
+  // an exchange posted and not yet received (run_islands overlaps it with
+  // the next generation), of mig_k migrants
+  bool mig_pending = false;
+  uint32_t mig_k = 0;
+  // one row of device staging for the cross-rank best genome (broadcast)
+  void* best_row = nullptr;
 };
 
 namespace {
@@ -294,9 +300,11 @@ void pga_deinit(pga_t* p) {
   if (!p) return;
   if (!p->pops.empty() && p->mig_cap) {
     pga::Island& isl = *p->pops[0]->isl;
+    if (isl.on_gpu()) (void)hipStreamSynchronize(p->stream);  // a posted exchange may still read the staging
     for (void* b : {p->mig_send_rows, p->mig_recv_rows, (void*)p->mig_send_scores, (void*)p->mig_recv_scores})
       dev_free(isl, b);
   }
+  if (!p->pops.empty() && p->best_row) dev_free(*p->pops[0]->isl, p->best_row);
   for (population_t* pop : p->pops) delete pop;
   p->pops.clear();
   if (p->comm_members) {
@@ -527,27 +535,40 @@ gene* pga_get_best_all(pga_t* p) {
 gene** pga_get_best_top_all(pga_t* p, unsigned length) {
   if (!p || p->pops.empty() || length == 0) return nullptr;
   return guard_r<gene**>(p, nullptr, [&]() -> gene** {
+    // per population: top-k on the device, the k winners' rows and scores
+    // gathered there, ONE copy of k rows + k scores to the host
     struct Cand {
       float score;
       size_t pop;
-      uint32_t idx;
+      uint32_t slot;
     };
     std::vector<Cand> all;
+    std::vector<std::vector<uint32_t>> rows(p->pops.size());
     for (size_t i = 0; i < p->pops.size(); ++i) {
       pga::Island& isl = *p->pops[i]->isl;
       isl.stream = p->stream;
       const uint32_t k = (uint32_t)std::min<uint64_t>(length, isl.config().S);
-      std::vector<uint32_t> idx = isl.topk_host(k, true);
-      std::vector<float> sc(isl.config().S);
-      isl.copy_to_host(sc.data(), isl.scores(0), 4ull * sc.size());
-      for (uint32_t j : idx) all.push_back({sc[j], i, j});
+      const size_t rb = isl.row_bytes();
+      char* buf = (char*)isl.scratch(4ull * k + rb * k + 4ull * k);
+      uint32_t* idx = (uint32_t*)buf;
+      void* rdev = buf + 4ull * k;
+      float* sdev = (float*)(buf + 4ull * k + rb * k);
+      isl.topk(k, true, idx, /*sorted=*/true);
+      isl.gather(idx, k, rdev, sdev);
+      rows[i].resize(rb / 4 * k);
+      std::vector<float> sc(k);
+      isl.copy_to_host(rows[i].data(), rdev, rb * k);
+      isl.copy_to_host(sc.data(), sdev, 4ull * k);
+      for (uint32_t j = 0; j < k; ++j) all.push_back({sc[j], i, j});
     }
     std::stable_sort(all.begin(), all.end(), [](const Cand& a, const Cand& b) { return a.score > b.score; });
     gene** out = (gene**)std::calloc(length, sizeof(gene*));
     if (!out) throw std::bad_alloc();
     for (size_t i = 0; i < std::min<size_t>(length, all.size()); ++i) {
-      pga::Island& isl = *p->pops[all[i].pop]->isl;
-      out[i] = decode_row(isl, isl.row_host(all[i].idx));
+      const pga::Island& isl = *p->pops[all[i].pop]->isl;
+      const size_t rw = isl.row_bytes() / 4;
+      std::vector<uint32_t> r(rows[all[i].pop].begin() + rw * all[i].slot, rows[all[i].pop].begin() + rw * (all[i].slot + 1));
+      out[i] = decode_row(isl, r);
     }
     return out;
   });
@@ -620,32 +641,38 @@ void ensure_staging(pga_t* p, pga::Island& isl, uint32_t k) {
 
 // Inter-rank migration of population 0 of every solver in `solvers` (all the
 // ranks this call drives: one per process with ncclCommInitRank, all of them
-// with InitAll / loopback).  Per rank: top-k emigrants (device radix select)
-// -> packed send buffers -> the epoch's plan over the transport ->
-// [optional host check with timeout] -> re-score the received rows with the
-// LOCAL objective (a forged score never enters) -> replace the bottom-k.
-// Everything is stream-ordered; with no timeout nothing waits on the host,
-// so the exchange overlaps whatever the GPUs run next.
-void migrate_ranks(const std::vector<pga_t*>& solvers, float pct) {
-  pga_t* p0 = solvers.front();
-  // a 1-rank communicator exchanges only in fault-injection (test) mode
-  if (!p0->comm || (p0->comm->size() == 1 && !p0->comm->self_exchange) || p0->degraded) return;
-  pga::Comm& comm = *p0->comm;
-  const uint64_t S = p0->pops[0]->isl->config().S;
-  const uint32_t k0 = migrants(S, S, pct);
-  const uint32_t k = pga::plan_migrants(p0->topology, comm.size(), k0);
-  if (!k) return;
-  if (k > S / 2) throw std::invalid_argument("migration: too many migrants for the population size");
-  const std::vector<pga::Xfer> plan = pga::migration_plan(p0->topology, comm.size(), k0, p0->seed, p0->comm_epoch);
+// with InitAll / loopback), in two phases so the transfer overlaps compute:
+//   post_ranks    per rank: emigrants (island policy: exact top-k by default)
+//                 packed on the compute stream -> the epoch's plan posted on
+//                 the transport (RCCL: the rank's communication stream, which
+//                 waits only for the packed emigrants)
+//   finish_ranks  [host poll against the deadline, after whatever the caller
+//                 enqueued meanwhile] -> compute stream ordered after the
+//                 transfer -> received rows re-scored with the LOCAL
+//                 objective (a forged score never enters) -> bottom-k
+//                 replaced
+// run_islands posts at a migration point, enqueues the next generation, then
+// finishes: the exchange runs beside that generation and the host waits (if
+// at all) only once it is queued.  A failure or expiry aborts the
+// communicator and leaves every rank of the call degraded.
+void degrade(const std::vector<pga_t*>& solvers, const char* what) {
+  for (pga_t* p : solvers) {
+    if (!p->degraded) ++p->comm_failures;
+    p->degraded = true;
+    p->mig_pending = false;
+  }
+  std::fprintf(stderr, "pga: %s over %s failed (%s); islands continue without migration\n", what,
+               solvers.front()->comm ? solvers.front()->comm->name() : "?", g_last_error.c_str());
+}
+
+bool comm_active(const pga_t* p0) {
+  return p0->comm && !(p0->comm->size() == 1 && !p0->comm->self_exchange) && !p0->degraded;
+}
+
+std::vector<pga::LocalRank> local_ranks(const std::vector<pga_t*>& solvers) {
   std::vector<pga::LocalRank> local;
   for (pga_t* p : solvers) {
-    use_device(p);
     pga::Island& isl = *p->pops[0]->isl;
-    if (isl.config().S != S || isl.row_bytes() != p0->pops[0]->isl->row_bytes())
-      throw std::invalid_argument("migration: ranks need populations of the same size and genome length");
-    isl.stream = p->stream;
-    ensure_staging(p, isl, k);
-    isl.emigrate(k, p->mig_send_rows, p->mig_send_scores);
     pga::LocalRank l;
     l.rank = p->comm_rank;
     l.device = p->device;
@@ -657,32 +684,80 @@ void migrate_ranks(const std::vector<pga_t*>& solvers, float pct) {
     l.recv_scores = p->mig_recv_scores;
     local.push_back(l);
   }
-  bool ok = true;
+  return local;
+}
+
+bool post_ranks(const std::vector<pga_t*>& solvers, float pct) {
+  pga_t* p0 = solvers.front();
+  // a 1-rank communicator exchanges only in self-exchange (test) mode
+  if (!comm_active(p0) || p0->mig_pending) return false;
+  pga::Comm& comm = *p0->comm;
+  const uint64_t S = p0->pops[0]->isl->config().S;
+  const uint32_t k0 = migrants(S, S, pct);
+  const uint32_t k = pga::plan_migrants(p0->topology, comm.size(), k0);
+  if (!k) return false;
+  if (k > S / 2) throw std::invalid_argument("migration: too many migrants for the population size");
+  const std::vector<pga::Xfer> plan = pga::migration_plan(p0->topology, comm.size(), k0, p0->seed, p0->comm_epoch);
+  for (pga_t* p : solvers) {
+    use_device(p);
+    pga::Island& isl = *p->pops[0]->isl;
+    if (isl.config().S != S || isl.row_bytes() != p0->pops[0]->isl->row_bytes())
+      throw std::invalid_argument("migration: ranks need populations of the same size and genome length");
+    isl.stream = p->stream;
+    ensure_staging(p, isl, k);
+    isl.emigrate(k, p->mig_send_rows, p->mig_send_scores);
+  }
+  std::vector<pga::LocalRank> local = local_ranks(solvers);
   try {
     comm.exchange(plan, local);
+  } catch (const std::exception& e) {
+    g_last_error = e.what();
+    for (pga_t* p : solvers) ++p->comm_epoch;
+    degrade(solvers, "migration");
+    return false;
+  }
+  for (pga_t* p : solvers) {
+    p->mig_pending = true;
+    p->mig_k = k;
+  }
+  return true;
+}
+
+void finish_ranks(const std::vector<pga_t*>& solvers) {
+  pga_t* p0 = solvers.front();
+  if (!p0->mig_pending) return;
+  pga::Comm& comm = *p0->comm;
+  const uint32_t k = p0->mig_k;
+  std::vector<pga::LocalRank> local = local_ranks(solvers);
+  bool ok = true;
+  try {
     ok = comm.wait(local, p0->comm_timeout);
   } catch (const std::exception& e) {
     g_last_error = e.what();
     ok = false;
   }
-  for (pga_t* p : solvers) ++p->comm_epoch;
+  for (pga_t* p : solvers) {
+    ++p->comm_epoch;
+    p->mig_pending = false;
+  }
   if (!ok) {
-    // islands are loosely coupled: each keeps evolving alone (degraded mode)
-    for (pga_t* p : solvers) {
-      p->degraded = true;
-      ++p->comm_failures;
-    }
-    std::fprintf(stderr, "pga: migration over %s failed (%s); islands continue without migration\n", comm.name(),
-                 g_last_error.c_str());
+    if (g_last_error.empty()) g_last_error = "transfer failed or timed out";
+    degrade(solvers, "migration");
     return;
   }
   for (pga_t* p : solvers) {
     use_device(p);
     pga::Island& isl = *p->pops[0]->isl;
+    isl.stream = p->stream;
     if (p->validate_migrants) isl.evaluate_rows(p->mig_recv_rows, p->mig_recv_scores, k);
     isl.immigrate(k, p->mig_recv_rows, p->mig_recv_scores);
     p->migrants_received += k;
   }
+}
+
+// the serial form (pga_comm_exchange): post and receive at once
+void migrate_ranks(const std::vector<pga_t*>& solvers, float pct) {
+  if (post_ranks(solvers, pct)) finish_ranks(solvers);
 }
 }  // namespace
 
@@ -747,8 +822,7 @@ namespace {
 // best score over every population of `solvers` and, with a communicator that
 // is still healthy, over every rank (the same value on all of them)
 float global_best(const std::vector<pga_t*>& solvers) {
-  std::vector<pga::LocalRank> local;
-  std::vector<float> mine;
+  std::vector<uint32_t> mine;
   float all_best = -INFINITY;
   for (pga_t* q : solvers) {
     use_device(q);
@@ -757,17 +831,30 @@ float global_best(const std::vector<pga_t*>& solvers) {
       pop->isl->stream = q->stream;
       b = std::max(b, pop->isl->best_score());
     }
-    mine.push_back(b);
+    uint32_t w;
+    std::memcpy(&w, &b, 4);
+    mine.push_back(w);
     all_best = std::max(all_best, b);
-    pga::LocalRank l;
-    l.rank = q->comm_rank;
-    l.device = q->device;
-    l.stream = q->stream;
-    local.push_back(l);
   }
   pga_t* p0 = solvers.front();
-  if (!p0->comm || p0->degraded || (p0->comm->size() == 1 && !p0->comm->self_exchange)) return all_best;
-  for (float v : p0->comm->allgather(local, mine)) all_best = std::max(all_best, v);
+  if (!comm_active(p0)) return all_best;
+  std::vector<uint32_t> all;
+  bool ok = false;
+  try {
+    ok = p0->comm->allgather(local_ranks(solvers), mine, 1, all, p0->comm_timeout);
+  } catch (const std::exception& e) {
+    g_last_error = e.what();
+  }
+  if (!ok) {  // a dead or withheld peer: every local rank continues alone on its own best
+    if (g_last_error.empty()) g_last_error = "all-gather failed or timed out";
+    degrade(solvers, "global best all-gather");
+    return all_best;
+  }
+  for (uint32_t w : all) {
+    float v;
+    std::memcpy(&v, &w, 4);
+    all_best = std::max(all_best, v);
+  }
   return all_best;
 }
 
@@ -787,6 +874,15 @@ unsigned run_islands_until(const std::vector<pga_t*>& solvers, unsigned n, unsig
   const bool until = !std::isnan(target);
   const unsigned every = m > 0 ? m : 10u;  // check points of a target run
   if (until && global_best(solvers) >= target) return 0;
+  auto generations = [&](unsigned k) {
+    for (pga_t* p : solvers) {
+      use_device(p);
+      const bool gpu = p->device >= 0;
+      if (gpu) fork_islands(p);
+      for (population_t* pop : p->pops) pop->isl->run(k);
+      if (gpu) join_islands(p);
+    }
+  };
   unsigned g = 0;
   while (g < n) {
     // generations until the next migration / check point (or the end)
@@ -796,13 +892,15 @@ unsigned run_islands_until(const std::vector<pga_t*>& solvers, unsigned n, unsig
       const unsigned next = (g / period + 1) * period;
       if (next < n) step = next - g;
     }
-    for (pga_t* p : solvers) {
-      use_device(p);
-      const bool gpu = p->device >= 0;
-      if (gpu) fork_islands(p);
-      for (population_t* pop : p->pops) pop->isl->run(step);
-      if (gpu) join_islands(p);
+    if (solvers.front()->mig_pending) {
+      // the exchange posted at the last migration point runs beside this
+      // generation; its migrants enter the population that generation made
+      generations(1);
+      finish_ranks(solvers);
+      ++g;
+      --step;
     }
+    if (step > 0) generations(step);
     g += step;
     if (until && global_best(solvers) >= target) break;
     if (m > 0 && g % m == 0 && g < n) {
@@ -810,9 +908,10 @@ unsigned run_islands_until(const std::vector<pga_t*>& solvers, unsigned n, unsig
         use_device(p);
         pga_migrate(p, pct);
       }
-      migrate_ranks(solvers, pct);
+      post_ranks(solvers, pct);
     }
   }
+  finish_ranks(solvers);  // nothing is left in flight (a no-op unless a check point ended the run)
   return g;
 }
 }  // namespace
@@ -1080,32 +1179,132 @@ int pga_comm_exchange(pga_t** solvers, int count, float pct) {
   });
 }
 
+namespace {
+// the solvers this process drives for p's communicator (all ranks of an
+// InitAll / loopback group, else p alone)
+std::vector<pga_t*> comm_solvers(pga_t* p) {
+  std::vector<pga_t*> solvers{p};
+  if (p->comm && p->comm->drives_all_ranks() && p->comm_members) solvers = *p->comm_members;
+  std::sort(solvers.begin(), solvers.end(), [](pga_t* a, pga_t* b) { return a->comm_rank < b->comm_rank; });
+  return solvers;
+}
+
+// (score, index) of every local rank's population-0 best, all-gathered: the
+// global best = the highest score, ties to the lowest rank.  false: the
+// all-gather failed or timed out (the group is degraded, *score / *rank / *idx
+// describe the local best).
+bool comm_best_of(pga_t* p, const std::vector<pga_t*>& solvers, float* score, int* rank, uint32_t* idx) {
+  std::vector<uint32_t> mine;
+  for (pga_t* q : solvers) {
+    use_device(q);
+    pga::Island& isl = *q->pops[0]->isl;
+    isl.stream = q->stream;
+    const unsigned long long b = isl.best_packed();
+    const float s = pga::best_score(b);
+    uint32_t w;
+    std::memcpy(&w, &s, 4);
+    mine.push_back(w);
+    mine.push_back((uint32_t)pga::best_index(b));
+  }
+  std::vector<uint32_t> all = mine;
+  bool ok = true;
+  if (comm_active(p)) {
+    try {
+      ok = p->comm->allgather(local_ranks(solvers), mine, 2, all, p->comm_timeout);
+    } catch (const std::exception& e) {
+      g_last_error = e.what();
+      ok = false;
+    }
+    if (!ok) {
+      degrade(solvers, "global best all-gather");
+      all = mine;
+    }
+  }
+  const int nr = ok && comm_active(p) ? p->comm->size() : (int)solvers.size();
+  int br = 0;
+  float bs = -INFINITY;
+  for (int i = 0; i < nr; ++i) {
+    float v;
+    std::memcpy(&v, &all[2 * i], 4);
+    if (i == 0 || v > bs) {
+      bs = v;
+      br = i;
+    }
+  }
+  if (score) *score = bs;
+  if (rank) *rank = ok && comm_active(p) ? br : solvers[br]->comm_rank;
+  if (idx) *idx = all[2 * br + 1];
+  return ok;
+}
+}  // namespace
+
 int pga_comm_best(pga_t* p, float* score, int* rank) {
   if (!p || p->pops.empty()) return -1;
   return guard_r<int>(p, -1, [&]() {
-    std::vector<pga_t*> solvers{p};
-    if (p->comm && p->comm->drives_all_ranks() && p->comm_members) solvers = *p->comm_members;
-    std::vector<pga::LocalRank> local;
-    std::vector<float> mine;
+    (void)comm_best_of(p, comm_solvers(p), score, rank, nullptr);
+    return 0;
+  });
+}
+
+int pga_comm_get_best(pga_t* p, float* score, int* rank, void* row_out) {
+  if (!p || p->pops.empty()) return -1;
+  return guard_r<int>(p, -1, [&]() {
+    const std::vector<pga_t*> solvers = comm_solvers(p);
+    float bs = 0.f;
+    int br = 0;
+    uint32_t bi = 0;
+    const bool ok = comm_best_of(p, solvers, &bs, &br, &bi);
+    if (score) *score = bs;
+    if (rank) *rank = br;
+    if (!row_out) return 0;
+    pga_t* self = p;
+    if (!ok || !comm_active(p)) {  // local only: the winner is one of our own solvers
+      for (pga_t* q : solvers)
+        if (q->comm_rank == br) self = q;
+      pga::Island& isl = *self->pops[0]->isl;
+      std::vector<uint32_t> r = isl.row_host(bi);
+      std::memcpy(row_out, r.data(), isl.row_bytes());
+      return 0;
+    }
+    // the winning rank copies its row into the staging, the communicator
+    // broadcasts it, every rank reads it back
+    std::vector<void*> bufs;
     for (pga_t* q : solvers) {
       use_device(q);
       pga::Island& isl = *q->pops[0]->isl;
-      isl.stream = q->stream;
-      mine.push_back(isl.best_score());
-      pga::LocalRank l;
-      l.rank = q->comm_rank;
-      l.device = q->device;
-      l.stream = q->stream;
-      local.push_back(l);
+      if (!q->best_row) q->best_row = dev_alloc(isl, isl.row_bytes());
+      if (q->comm_rank == br) {
+        const char* src = (const char*)isl.rows(0) + (size_t)bi * isl.row_bytes();
+        if (isl.on_gpu())
+          PGA_HIP_CHECK(hipMemcpyAsync(q->best_row, src, isl.row_bytes(), hipMemcpyDeviceToDevice, q->stream));
+        else
+          std::memcpy(q->best_row, src, isl.row_bytes());
+      }
+      bufs.push_back(q->best_row);
     }
-    std::vector<float> all = p->comm ? p->comm->allgather(local, mine) : mine;
-    int br = 0;
-    for (int i = 1; i < (int)all.size(); ++i)
-      if (all[i] > all[br]) br = i;
-    if (score) *score = all[br];
-    if (rank) *rank = br;
+    std::vector<pga::LocalRank> local = local_ranks(solvers);
+    const size_t rb = p->pops[0]->isl->row_bytes();
+    bool bok = false;
+    try {
+      bok = p->comm->broadcast(local, bufs, rb, br, p->comm_timeout);
+    } catch (const std::exception& e) {
+      g_last_error = e.what();
+    }
+    if (!bok) {
+      degrade(solvers, "best-genome broadcast");
+      return -1;
+    }
+    pga::Island& isl = *p->pops[0]->isl;
+    isl.stream = p->stream;
+    isl.copy_to_host(row_out, p->best_row, rb);
     return 0;
   });
+}
+
+int pga_comm_set_self_exchange(pga_t* p, int on) {
+  if (!p || !p->comm) return -1;
+  p->comm->self_exchange = on != 0;
+  return 0;
 }
 
 }  // extern "C"

@@ -79,13 +79,31 @@ class Comm {
   // host-side completion check of the last exchange; false: failed or timed
   // out (the communicator is then unusable and the islands run on alone)
   virtual bool wait(std::vector<LocalRank>& local, double timeout_s) = 0;
-  // one float per rank; `local[i]` contributes mine[i]; returns all ranks' values
-  virtual std::vector<float> allgather(const std::vector<LocalRank>& local, const std::vector<float>& mine) = 0;
+  // All-gather of `count` 32-bit words per rank (count <= kGatherMaxWords):
+  // local[i] contributes mine[i * count ..]; `all` receives every rank's words
+  // in rank order.  Bounded like wait(): with timeout_s > 0 the host polls the
+  // completion against the deadline and on expiry or an asynchronous error
+  // aborts the communicator and returns false (the caller degrades); with
+  // timeout_s <= 0 it blocks until the collective completes.  Persistent
+  // staging: no allocation or free per call.
+  static constexpr uint32_t kGatherMaxWords = 16;
+  virtual bool allgather(const std::vector<LocalRank>& local, const std::vector<uint32_t>& mine, uint32_t count,
+                         std::vector<uint32_t>& all, double timeout_s) = 0;
+  // `bytes` of rank `root`'s bufs[i] (the local rank's buffer: device memory
+  // for GPU ranks, host for CPU ones) copied to every rank's buffer; the
+  // buffers are written on the local ranks' compute streams beforehand and
+  // read there afterwards.  Same deadline semantics as allgather.
+  virtual bool broadcast(const std::vector<LocalRank>& local, const std::vector<void*>& bufs, size_t bytes, int root,
+                         double timeout_s) = 0;
   // test-only fault injection (pga_comm_set_fault): loopback drops (1) or
   // corrupts (2) every `every`-th exchange; RCCL withholds this process's
   // sends (3) of every `every`-th exchange, so its receives can never
-  // complete.  Arming it also lets a 1-rank communicator exchange with itself.
+  // complete, or stalls (4) every `every`-th all-gather behind a receive
+  // that never completes.  Mode 0 disarms it.
   virtual void set_fault(int every, int mode) = 0;
+  // test-only (pga_comm_set_self_exchange): a 1-rank communicator normally
+  // skips migration; with this set it exchanges with itself, which runs the
+  // real transport (and the fault injection) on one GPU
   bool self_exchange = false;
   uint64_t bytes_sent = 0;
 };

@@ -127,7 +127,7 @@ class Island {
   // do each in ONE selection kernel with the row moves fused in; otherwise
   // topk + gather / scatter.  `idx_scratch` (k words, device) may be null.
   void emigrate(uint32_t k, void* out_rows, float* out_scores);
-  // MIG_STRIPE (default) or MIG_TOPK, see core.hpp MigrationPolicy
+  // MIG_TOPK (default: the reference's "top pct%") or MIG_STRIPE, see core.hpp MigrationPolicy
   void set_migration_policy(int p);
   int migration_policy() const { return mig_policy_; }
   void immigrate(uint32_t k, const void* in_rows, const float* in_scores);
@@ -206,7 +206,7 @@ class Island {
   std::vector<float> hist_host_;  // CPU backend
   uint64_t hist_n_ = 0;
   bool hist_on_ = false;
-  int mig_policy_ = MIG_STRIPE;
+  int mig_policy_ = MIG_TOPK;
   float mut_inv_ = 0.f;
   bool mut_sparse_ = false;  // BINARY bit-flip uses the sparse (Binomial) sampler
   float mut_rate_eff_ = 0.f;

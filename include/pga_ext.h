@@ -117,17 +117,22 @@ int pga_comm_rank(const pga_t *p);
 int pga_comm_size(const pga_t *p);
 int pga_comm_set_topology(pga_t *p, enum pga_topology t); /* applies to the whole local group */
 /* Emigrant / victim choice of every migration of `pop` (pga_migrate*,
- * pga_run_islands*, inter-rank epochs).  STRIPE (default): the population is
- * cut into k contiguous stripes; stripe i's best emigrates and its worst is
- * replaced by immigrant i — one pass over the scores each way, so the global
- * best always emigrates.  TOPK: the exact top-k emigrate and the bottom-k are
- * replaced (two radix selections). */
+ * pga_run_islands*, inter-rank epochs).  TOPK (default, the "top pct%" of
+ * the reference's pga_migrate / pga_run_islands, include/pga.h): the exact
+ * top-k emigrate and the bottom-k are replaced.  STRIPE (opt-in, cheaper):
+ * the population is cut into k contiguous stripes; stripe i's best emigrates
+ * and its worst is replaced by immigrant i — one pass over the scores each
+ * way, and the global best still always emigrates. */
 enum pga_migration_policy { PGA_MIGRATE_TOPK = 0, PGA_MIGRATE_STRIPE = 1 };
 int pga_set_migration_policy(pga_t *p, population_t *pop, enum pga_migration_policy policy);
-/* > 0: after each exchange wait at most `seconds` on the host (RCCL: event
- * polling + async error check); a failed or late exchange aborts the
- * communicator and the islands continue alone (degraded).  0 (default):
- * fully asynchronous, errors are only checked. */
+/* > 0: every collective of the island model is bounded by `seconds` on the
+ * host (RCCL: event polling + async error check): the migration exchange
+ * (polled only after the next generation is queued, so it still overlaps
+ * compute), the all-gathers of the global best / target checks and the
+ * best-genome broadcast.  A failed or late collective aborts the
+ * communicator at once; the islands continue alone (degraded) and queries
+ * fall back to the local best.  0 (default): exchanges fully asynchronous
+ * (errors are only checked), collectives block until done. */
 int pga_comm_set_timeout(pga_t *p, double seconds);
 int pga_comm_set_validation(pga_t *p, int on);             /* re-score received migrants (default 1) */
 int pga_comm_degraded(const pga_t *p);
@@ -135,14 +140,25 @@ int pga_comm_info(const pga_t *p, struct pga_comm_stats *out);
 /* tests: every `every`-th exchange is dropped (mode 1, loopback), arrives
  * with forged scores (mode 2, loopback) or has this rank's sends withheld so
  * its receives never complete (mode 3, RCCL: exercises the timeout + abort
- * path).  Also lets a 1-rank communicator exchange with itself. */
+ * path); mode 4 (RCCL) stalls every `every`-th all-gather behind a receive
+ * that never completes (a peer lost between two check points); mode 0
+ * disarms it. */
 int pga_comm_set_fault(pga_t *p, int every, int mode);
-/* global best over ranks (score, owning rank) */
-/* one inter-rank migration epoch now (the step pga_run_islands takes every
- * m generations), for callers driving their own generation loop; pass every
- * rank of an InitAll / loopback group, or the one solver of an InitRank rank */
+/* tests: let a 1-rank communicator exchange with itself (normally migration
+ * is skipped at one rank), so the real transport runs on one GPU */
+int pga_comm_set_self_exchange(pga_t *p, int on);
+/* one inter-rank migration epoch now, serially (exchange, wait, immigrate;
+ * pga_run_islands overlaps it with the next generation instead), for callers
+ * driving their own generation loop; pass every rank of an InitAll /
+ * loopback group, or the one solver of an InitRank rank */
 int pga_comm_exchange(pga_t **solvers, int count, float pct);
+/* global best over ranks: score and owning rank (ties: the lowest rank), an
+ * all-gather of (score, index) of every rank's population 0 */
 int pga_comm_best(pga_t *p, float *score, int *rank);
+/* the same plus the winning genome: its raw row (pga_row_bytes bytes,
+ * pga_get_genome layout) is broadcast from the owning rank and copied to
+ * row_out on every rank (row_out may be NULL).  Every rank must call it. */
+int pga_comm_get_best(pga_t *p, float *score, int *rank, void *row_out);
 /* pga_run_islands over every rank of an InitAll / loopback group at once */
 int pga_run_islands_multi(pga_t **solvers, int n, unsigned generations, unsigned m, float pct);
 

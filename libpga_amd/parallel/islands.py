@@ -7,8 +7,8 @@ its peer(s), replacing its worst individuals.
 
 Data path per migration (all on-device, no host synchronisation):
   emigrant selection with the row gather fused in (Island.emigrate; policy
-  "stripe": the best of each of k population stripes, one pass; "topk": the
-  exact top-k, u16-key histogram + one ticketed select kernel) writing
+  "topk", the default: the exact top-k; "stripe": the best of each of k
+  population stripes, one pass) writing
   rows+scores into ONE packed send buffer -> RCCL send/recv on torch's NCCL
   stream -> [next generation kernel runs concurrently on the compute stream]
   -> stream wait on the NCCL work -> re-score -> victims replaced with the
@@ -100,7 +100,7 @@ class IslandModel:
         validate: bool = True,
         timeout_s: Optional[float] = None,
         fault_hook: Optional[Callable[[torch.Tensor, int], bool]] = None,
-        policy: str = "stripe",
+        policy: str = "topk",
     ):
         if topology not in TOPOLOGIES:
             raise ValueError(f"topology must be one of {TOPOLOGIES}")
@@ -150,6 +150,11 @@ class IslandModel:
         if topology == "all_to_all" and self.world > 1:
             others = [p for p in range(self.world) if p != self.rank]
             self._peer_idx = torch.tensor(others, dtype=torch.long, device=dev)
+            # persistent [peer][rows | scores] send / receive packing (the self
+            # slice stays empty): no allocation or memset per epoch
+            per = self.k // (self.world - 1)
+            self._a2a_send = torch.zeros(self.world * per * (self.rw + 1), dtype=torch.int32, device=dev)
+            self._a2a_recv = torch.empty_like(self._a2a_send)
         self._epoch = 0
         self.migrations = 0
         self.bytes_sent = 0
@@ -209,12 +214,10 @@ class IslandModel:
         # per-peer loop); the self slice is empty
         w, per = self.world, self.k // (self.world - 1)
         srows, sscores = self._views(self.send)
-        packed = torch.zeros(w * per * (self.rw + 1), dtype=torch.int32, device=self.send.device)
-        pv = packed.view(w, per * (self.rw + 1))
+        pv = self._a2a_send.view(w, per * (self.rw + 1))
         pv[self._peer_idx, : per * self.rw] = srows.view(w - 1, per * self.rw)
         pv[self._peer_idx, per * self.rw:] = sscores.view(torch.int32).view(w - 1, per)
-        self._a2a_recv = torch.empty_like(packed)
-        return [dist.all_to_all_single(self._a2a_recv, packed, group=self.group, async_op=True)]
+        return [dist.all_to_all_single(self._a2a_recv, self._a2a_send, group=self.group, async_op=True)]
 
     def _await(self, works) -> None:
         """Complete the exchange.  Without a timeout: stream-ordered waits
@@ -335,27 +338,46 @@ class IslandModel:
             self.finish_migration()
 
     # -------------------------------------------------------------- queries --
+    def _bounded(self, work) -> bool:
+        """Complete an async collective under the migration deadline (the
+        same host poll + abort as an exchange); False: failed or expired, the
+        model is now degraded."""
+        try:
+            self._await([work])
+        except Exception as e:  # noqa: BLE001 — a dead peer must never hang a query
+            self._fail(e)
+            return False
+        return True
+
     def global_best(self) -> Tuple[float, int, torch.Tensor]:
-        """(score, owning rank, decoded genome) of the best individual of all islands."""
+        """(score, owning rank, decoded genome) of the best individual of all
+        islands; ties go to the lowest rank.  Bounded by ``timeout_s``: on a
+        dead peer the model degrades and this returns the local best."""
         score, genome = self.ga.best()
         if self.world == 1 or self.degraded:
             return score, self.rank, genome
         dev = self.send.device
         t = torch.tensor([score, float(self.rank)], dtype=torch.float64, device=dev)
         allt = [torch.empty_like(t) for _ in range(self.world)]
-        dist.all_gather(allt, t, group=self.group)
+        if not self._bounded(dist.all_gather(allt, t, group=self.group, async_op=True)):
+            return score, self.rank, genome
         vals = torch.stack(allt).cpu()
         best_rank = int(vals[:, 0].argmax().item())
         row = self.ga.island.row(self.ga.best_index()).to(dev)
-        dist.broadcast(row, src=best_rank, group=self.group)
+        if not self._bounded(dist.broadcast(row, src=best_rank, group=self.group, async_op=True)):
+            return score, self.rank, genome
         return float(vals[best_rank, 0]), best_rank, self.ga.problem.decode(row.unsqueeze(0).cpu())[0]
 
     def global_reduce_best(self) -> float:
+        """Max of every island's best (the target check).  Bounded by
+        ``timeout_s``: on a dead peer the model degrades and this returns the
+        local best."""
         s = self.ga.best_score()
         if self.world == 1 or self.degraded:  # an aborted group cannot reduce: the local best
             return s
         t = torch.tensor([s], dtype=torch.float32, device=self.send.device)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
+        if not self._bounded(dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group, async_op=True)):
+            return s
         return float(t.item())
 
 

@@ -38,7 +38,7 @@ def migration_policy(name: str) -> int:
 class LocalIslands:
     def __init__(self, problem: Problem, n_islands: int, pop_size: int, *, seed: Optional[int] = None,
                  device=None, migrate_every: int = 10, migrate_pct: float = 0.01, topology: str = "ring",
-                 first_island: int = 0, policy: str = "stripe", **op_overrides):
+                 first_island: int = 0, policy: str = "topk", **op_overrides):
         if n_islands < 1:
             raise ValueError("n_islands must be >= 1")
         if topology not in ("ring", "random"):

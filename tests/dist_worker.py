@@ -24,13 +24,9 @@ def run(rank: int, world: int, port: int, topology: str, out_dir: str) -> None:
     ga.run(5)
     send_scores = ga.scores.clone()
     k = model.k
-    # the default stripe policy: the best of each of k stripes (ties: lowest index)
+    # the default policy (the reference's "top pct%"): the exact top-k, ties to the lower index
     S = send_scores.numel()
-    top_idx = []
-    for i in range(k):
-        lo, hi = i * S // k, (i + 1) * S // k
-        seg = send_scores[lo:hi]
-        top_idx.append(lo + int(torch.nonzero(seg == seg.max())[0]))
+    top_idx = sorted(range(S), key=lambda i: (-float(send_scores[i]), i))[:k]
     emigrants = ga.rows.clone()[torch.tensor(top_idx)]
     model.start_migration()
     model.finish_migration()

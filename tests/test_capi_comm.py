@@ -65,6 +65,16 @@ def lib():
     L.pga_comm_degraded.argtypes = [vp]
     L.pga_comm_info.argtypes = [vp, C.POINTER(Stats)]
     L.pga_comm_best.argtypes = [vp, C.POINTER(C.c_float), C.POINTER(C.c_int)]
+    L.pga_comm_get_best.argtypes = [vp, C.POINTER(C.c_float), C.POINTER(C.c_int), vp]
+    L.pga_comm_set_self_exchange.argtypes = [vp, C.c_int]
+    L.pga_get_genome.argtypes = [vp, vp, C.c_ulong, vp]
+    L.pga_best_index.restype = C.c_ulong
+    L.pga_best_index.argtypes = [vp, vp]
+    L.pga_row_bytes.restype = C.c_size_t
+    L.pga_row_bytes.argtypes = [vp]
+    L.pga_migrate_between.argtypes = [vp, vp, vp, C.c_float]
+    L.pga_run_islands_until.restype = C.c_int
+    L.pga_run_islands_until.argtypes = [vp, C.c_uint, C.c_uint, C.c_float, C.c_float]
     L.pga_comm_exchange.argtypes = [C.POINTER(vp), C.c_int, C.c_float]
     L.pga_comm_unique_id.argtypes = [C.c_char_p]
     L.pga_comm_init.argtypes = [vp, C.c_int, C.c_int, C.c_char_p]
@@ -215,6 +225,62 @@ def test_forged_scores_are_rescored(lib, validate):
         lib.pga_deinit(p)
 
 
+def test_get_best_broadcasts_the_winning_genome(lib):
+    """pga_comm_get_best: (score, index) all-gathered, the owner's row
+    broadcast to every rank -- equal to the owner's own genome."""
+    solvers, pops, arr = make_group(lib, 3, seed=31)
+    assert lib.pga_comm_init_loopback(arr, 3) == 0
+    lib.pga_run(solvers[2], 40)  # rank 2 ahead
+    rb = lib.pga_row_bytes(pops[0])
+    want = C.create_string_buffer(rb)
+    assert lib.pga_get_genome(solvers[2], pops[2], lib.pga_best_index(solvers[2], pops[2]), want) == 0
+    for p in solvers:  # every rank sees the same winner and row
+        score, rank, row = C.c_float(), C.c_int(), C.create_string_buffer(rb)
+        assert lib.pga_comm_get_best(p, C.byref(score), C.byref(rank), row) == 0, lib.pga_last_error()
+        assert rank.value == 2 and score.value == lib.pga_best_score(solvers[2], pops[2])
+        assert row.raw == want.raw
+    for p in solvers:
+        lib.pga_deinit(p)
+
+
+def test_migrate_between_moves_exactly_the_top_k(lib):
+    """The pga.h contract (include/pga.h:108-115): pga_migrate_between copies
+    the top pct% of `from` over the worst of `to` (exact top-k by default)."""
+    p = lib.pga_init_device(-1)
+    lib.pga_set_seed(p, 77)
+    lib.pga_set_quiet(p, 1)
+    a = lib.pga_create_population_ext(p, S, LEN, PGA_BINARY)
+    b = lib.pga_create_population_ext(p, S, LEN, PGA_BINARY)
+    for q in (a, b):
+        assert lib.pga_set_objective_builtin(p, q, OBJ_ONEMAX, None, 0, None, 0, 0, 0.0, 0.0) == 0
+    lib.pga_run(p, 25)  # population 0 evolves: its top rows differ from b's
+    rb = lib.pga_row_bytes(a)
+
+    def snapshot(q):
+        sc = (C.c_float * S)()
+        lib.pga_get_scores(p, q, sc)
+        rows = []
+        for i in range(S):
+            r = C.create_string_buffer(rb)
+            lib.pga_get_genome(p, q, i, r)
+            rows.append(r.raw)
+        return list(sc), rows
+
+    sa, ra = snapshot(a)
+    sb, rbs = snapshot(b)
+    k = round(0.05 * S)
+    lib.pga_migrate_between(p, a, b, 0.05)
+    sb2, rb2 = snapshot(b)
+    # the k lowest-scored slots of b (ties: lower index first) were replaced ...
+    worst = sorted(range(S), key=lambda i: (sb[i], i))[:k]
+    kept = [i for i in range(S) if i not in set(worst)]
+    assert all(rb2[i] == rbs[i] for i in kept)
+    # ... by exactly a's top-k rows (as a multiset of (score, row))
+    top = sorted(range(S), key=lambda i: (-sa[i], i))[:k]
+    assert sorted((sb2[i], rb2[i]) for i in worst) == sorted((sa[i], ra[i]) for i in top)
+    lib.pga_deinit(p)
+
+
 def test_group_needs_the_multi_driver(lib):
     solvers, pops, arr = make_group(lib, 2)
     lib.pga_comm_init_loopback(arr, 2)
@@ -289,18 +355,20 @@ def rccl_rank0(lib, n=1):
 
 @pytest.mark.gpu
 def test_rccl_initrank_self_exchange_gpu(lib):
-    """InitRank with one rank; the fault hook (no fault, mode 0) arms the
-    self-exchange, so every epoch runs grouped ncclSend/ncclRecv on the
-    communication stream and the compute stream waits for it."""
+    """InitRank with one rank; the self-exchange test hook makes every epoch
+    run grouped ncclSend/ncclRecv on the communication stream, overlapped
+    with the next generation, before the compute stream consumes it."""
     p, pop = rccl_rank0(lib)
     assert lib.pga_comm_size(p) == 1 and lib.pga_comm_rank(p) == 0
-    assert lib.pga_comm_set_fault(p, 0, 0) == 0
+    lib.pga_run_islands(p, 10, 5, 0.05)
+    assert info(lib, p).epochs == 0  # one rank: no migration ...
+    assert lib.pga_comm_set_self_exchange(p, 1) == 0  # ... unless the test hook asks for it
     lib.pga_run_islands(p, 30, 5, 0.05)
     st = info(lib, p)
     k = round(0.05 * S)
     assert st.epochs == 5 and st.failures == 0 and not st.degraded
     assert st.migrants_received == 5 * k and st.bytes_sent == 5 * k * (16 + 4)
-    assert lib.pga_generation(pop) == 30 and lib.pga_best_score(p, pop) >= 50
+    assert lib.pga_generation(pop) == 40 and lib.pga_best_score(p, pop) >= 50
     lib.pga_deinit(p)
 
 
@@ -311,6 +379,7 @@ def test_rccl_withheld_send_degrades_gpu(lib):
     scatter is dropped and the generations continue on the compute stream,
     which never waited for the dead transfer."""
     p, pop = rccl_rank0(lib)
+    assert lib.pga_comm_set_self_exchange(p, 1) == 0
     assert lib.pga_comm_set_timeout(p, 2.0) == 0
     assert lib.pga_comm_set_fault(p, 2, 3) == 0
     t0 = time.monotonic()
@@ -334,3 +403,39 @@ def test_islands_multiproc_example_gpu(tmp_path):
                        timeout=120)
     assert r.returncode == 0, r.stderr
     assert "rank 0/1 generations 30" in r.stdout
+
+
+@pytest.mark.gpu
+def test_rccl_stalled_allgather_degrades_gpu(lib):
+    """A target run whose 2nd check-point all-gather stalls (a peer lost
+    between epochs): the deadline expires, the communicator is aborted, the
+    run goes on with the local best and returns within the timeout."""
+    p, pop = rccl_rank0(lib)
+    assert lib.pga_comm_set_self_exchange(p, 1) == 0
+    assert lib.pga_comm_set_timeout(p, 2.0) == 0
+    assert lib.pga_comm_set_fault(p, 2, 4) == 0
+    t0 = time.monotonic()
+    g = lib.pga_run_islands_until(p, 60, 10, 0.05, float(LEN + 1))  # unreachable target
+    dt = time.monotonic() - t0
+    st = info(lib, p)
+    assert g == 60, lib.pga_last_error()
+    assert st.degraded == 1 and st.failures == 1
+    assert dt < 30, dt
+    score, rank = C.c_float(), C.c_int()
+    assert lib.pga_comm_best(p, C.byref(score), C.byref(rank)) == 0  # degraded: the local best, no hang
+    assert score.value == lib.pga_best_score(p, pop)
+    lib.pga_deinit(p)
+
+
+@pytest.mark.gpu
+def test_rccl_get_best_genome_single_rank_gpu(lib):
+    p, pop = rccl_rank0(lib)
+    lib.pga_run(p, 20)
+    rb = lib.pga_row_bytes(pop)
+    want, row = C.create_string_buffer(rb), C.create_string_buffer(rb)
+    assert lib.pga_get_genome(p, pop, lib.pga_best_index(p, pop), want) == 0
+    score, rank = C.c_float(), C.c_int()
+    assert lib.pga_comm_set_self_exchange(p, 1) == 0  # the RCCL all-gather + broadcast path
+    assert lib.pga_comm_get_best(p, C.byref(score), C.byref(rank), row) == 0, lib.pga_last_error()
+    assert rank.value == 0 and row.raw == want.raw and score.value == lib.pga_best_score(p, pop)
+    lib.pga_deinit(p)
