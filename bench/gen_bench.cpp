@@ -14,6 +14,9 @@
 #include "pga/island.hpp"
 #include "pga/ops.hpp"
 
+// phase clocks of the headline kernel (experiment builds with -DPGA_TP_TIMING)
+extern "C" __attribute__((weak)) void pga_tp_timing_dump(uint32_t nwaves);
+
 
 int main(int argc, char** argv) {
   pga::Config c;
@@ -31,10 +34,22 @@ int main(int argc, char** argv) {
     else if (k == "--warmup") warm = std::atoi(v.c_str());
     else if (k == "--elitism") c.n_elite = (uint32_t)std::atoi(v.c_str());
     else if (k == "--objective") c.objective = std::atoi(v.c_str());
-    else if (k == "--xo") c.crossover = v == "one" ? pga::XO_ONE_POINT : (v == "two" ? pga::XO_TWO_POINT : pga::XO_UNIFORM);
+    else if (k == "--xo")
+      c.crossover = v == "one" ? pga::XO_ONE_POINT
+                    : v == "two" ? pga::XO_TWO_POINT
+                    : v == "blend" ? pga::XO_BLEND
+                    : v == "arith" ? pga::XO_ARITHMETIC : pga::XO_UNIFORM;
     else if (k == "--encoding") {
       c.encoding = v == "real" ? pga::ENC_REAL : (v == "perm" ? pga::ENC_PERMUTATION : pga::ENC_BINARY);
-      if (c.encoding == pga::ENC_REAL) { c.mutation = pga::MUT_GAUSSIAN; c.lo = -5.12f; c.hi = 5.12f; }
+      if (c.encoding == pga::ENC_REAL) {  // the Rastrigin-30D config of bench_configs.py
+        c.mutation = pga::MUT_GAUSSIAN;
+        c.lo = -5.12f;
+        c.hi = 5.12f;
+        c.crossover = pga::XO_BLEND;
+        c.blend_alpha = 0.3f;
+        c.sigma = 0.512f;  // Rastrigin default_operators: 0.05 (hi - lo)
+        c.objective = pga::OBJ_RASTRIGIN;
+      }
       if (c.encoding == pga::ENC_PERMUTATION) { c.mutation = pga::MUT_SWAP; c.crossover = pga::XO_OX; }
     }
   }
@@ -55,5 +70,6 @@ int main(int argc, char** argv) {
   std::printf("{\"pop\": %llu, \"length\": %u, \"gens\": %d, \"us_per_gen\": %.2f, \"gens_per_sec\": %.1f, "
               "\"evals_per_sec\": %.4e, \"best\": %.1f}\n",
               (unsigned long long)c.S, c.L, gens, us, 1e6 / us, 1e6 / us * (double)c.S, isl.best_score());
+  if (pga_tp_timing_dump) pga_tp_timing_dump(8192 * 4);
   return 0;
 }

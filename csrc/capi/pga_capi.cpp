@@ -620,6 +620,7 @@ void pga_migrate(pga_t* p, float pct) {
   });
 }
 
+extern "C++" {
 namespace {
 void use_device(pga_t* p) {
   if (p->device >= 0) PGA_HIP_CHECK(hipSetDevice(p->device));
@@ -760,6 +761,7 @@ void migrate_ranks(const std::vector<pga_t*>& solvers, float pct) {
   if (post_ranks(solvers, pct)) finish_ranks(solvers);
 }
 }  // namespace
+}  // extern "C++"
 
 void pga_run(pga_t* p, unsigned n) {
   if (!p || p->pops.empty()) return;
@@ -1179,6 +1181,7 @@ int pga_comm_exchange(pga_t** solvers, int count, float pct) {
   });
 }
 
+extern "C++" {
 namespace {
 // the solvers this process drives for p's communicator (all ranks of an
 // InitAll / loopback group, else p alone)
@@ -1237,6 +1240,7 @@ bool comm_best_of(pga_t* p, const std::vector<pga_t*>& solvers, float* score, in
   return ok;
 }
 }  // namespace
+}  // extern "C++"
 
 int pga_comm_best(pga_t* p, float* score, int* rank) {
   if (!p || p->pops.empty()) return -1;

@@ -67,9 +67,9 @@ Island::Island(const Config& cfg, int device) : cfg_(cfg), device_(device) {
 
 Island::~Island() {
   Buffer* all[] = {&rows_[0],   &rows_[1],     &scores_[0],   &scores_[1],  &best_[0],  &best_[1],   &mut_thr_,
-                   &obj_data_[0], &obj_data_[1], &keys_[0], &keys_[1], &elite_idx_, &cumfit_, &cum_ws_, &topk_ws_, &stats_,
+                   &obj_data_[0], &obj_data_[1], &keys_[0], &keys_[1], &elite_idx_, &cumfit_, &cum_ws_, &roul_guide_, &topk_ws_, &stats_,
                    &out_best_,  &scratch_, &compat_rand_, &ev_parts_, &gen_dev_, &rank_order_, &rank_ws_, &qubo_qt_,
-                   &knap_tab_, &stats_parts_[0], &stats_parts_[1], &hist_};
+                   &knap_tab_, &stats_parts_[0], &stats_parts_[1], &hist_, &qk_ws_};
   drop_graph();
   if (cap_stream_) (void)hipStreamDestroy(cap_stream_);
   for (Buffer* b : all) {
@@ -170,7 +170,10 @@ void Island::set_operators(const Config& c) {
   }
   if (cfg_.selection == SEL_ROULETTE && !cumfit_.ptr) {
     cumfit_ = alloc(4ull * cfg_.S);
-    cum_ws_ = alloc(4ull * (4 + 3 * 1024 + 1024));
+    if (on_gpu()) {
+      cum_ws_ = alloc(4ull * roulette_workspace_floats(cfg_.S));
+      roul_guide_ = alloc(4ull * (cfg_.S + 1));
+    }
   }
   if (cfg_.selection == SEL_RANK && !rank_order_.ptr) {
     rank_order_ = alloc(4ull * cfg_.S);
@@ -262,6 +265,8 @@ GenArgs Island::make_args(int mode) {
   a.selection = cfg_.selection;
   a.tour_k = cfg_.tour_k;
   a.cumfit = (const float*)cumfit_.ptr;
+  a.roul_guide = (const uint32_t*)roul_guide_.ptr;
+  a.roul_scale = cum_ws_.ptr ? (const float*)cum_ws_.ptr + kRoulScale : nullptr;
   a.rank_order = (const uint32_t*)rank_order_.ptr;
   a.rank_thresh = rank_thresh_of(cfg_.rank_pressure);
   a.crossover = cfg_.crossover;
@@ -301,6 +306,10 @@ GenArgs Island::make_args(int mode) {
     a.key_cur = (const uint16_t*)keys_[cur_].ptr;
     a.key_next = (uint16_t*)keys_[nx].ptr;
     if (mode == MODE_INIT || mode == MODE_EVAL) a.key_next = (uint16_t*)keys_[cur_].ptr;
+  } else if (mode == MODE_GEN && real_qk() && qk_valid_[cur_] && qk_ws_.ptr) {
+    a.key_cur = (const uint16_t*)keys_[cur_].ptr;
+    a.key_next = (uint16_t*)keys_[nx].ptr;
+    a.qk = (const float*)qk_ws_.ptr;
   }
   return a;
 }
@@ -312,6 +321,7 @@ uint32_t Island::launch(int mode, const GenArgs& a, unsigned long long* parts) {
 
 void Island::initialize() {
   TraceRange tr("pga.initialize");
+  invalidate_qk();
   GenArgs a = make_args(MODE_INIT);
   n_best_[cur_] = launch(MODE_INIT, a, (unsigned long long*)best_[cur_].ptr);
   stats_ok_[cur_] = a.stats_parts != nullptr;
@@ -325,6 +335,7 @@ void Island::initialize() {
 
 void Island::evaluate() {
   TraceRange tr("pga.evaluate");
+  invalidate_qk();
   if (jit_) {
     n_best_[cur_] = jit_eval(rows_[cur_].ptr, (float*)scores_[cur_].ptr, cfg_.S, (unsigned long long*)best_[cur_].ptr);
     stats_ok_[cur_] = false;
@@ -337,6 +348,7 @@ void Island::evaluate() {
 
 void Island::rebest() {
   stats_ok_[cur_] = false;
+  invalidate_qk();
   const float* sc = (const float*)scores_[cur_].ptr;
   if (on_gpu()) {
     uint16_t* keys = integer_objective(cfg_.objective, cfg_.L) ? (uint16_t*)keys_[cur_].ptr : nullptr;
@@ -347,11 +359,34 @@ void Island::rebest() {
   }
 }
 
+bool Island::real_qk() const {
+  return on_gpu() && cfg_.encoding == ENC_REAL && cfg_.objective != OBJ_NONE && !jit_;
+}
+
 void Island::prepare_generation() {
+  if (real_qk()) {
+    // the current generation's score range (fused partials when its kernel
+    // stored them), and its quantized keys if anything rewrote the scores
+    if (!qk_ws_.ptr) qk_ws_ = alloc(4ull * (4 + 3 * 1024));
+    const float* sc = (const float*)scores_[cur_].ptr;
+    if (stats_ok_[cur_])
+      stats_from_parts_launch((const float*)stats_parts_[cur_].ptr, (const unsigned long long*)best_[cur_].ptr,
+                              n_best_[cur_], cfg_.S, (float*)qk_ws_.ptr, stream);
+    else
+      score_stats_launch(sc, cfg_.S, (float*)qk_ws_.ptr, stream);
+    if (!qk_valid_[cur_]) {
+      scores_to_qkeys_launch(sc, cfg_.S, (const float*)qk_ws_.ptr, (uint16_t*)keys_[cur_].ptr, stream);
+      qk_valid_[cur_] = true;
+    }
+  }
   if (cfg_.selection == SEL_ROULETTE) {
     const float* sc = (const float*)scores_[cur_].ptr;
-    if (on_gpu()) roulette_prefix_launch(sc, cfg_.S, (float*)cumfit_.ptr, (float*)cum_ws_.ptr, stream);
-    else cpu::roulette_prefix(sc, cfg_.S, (float*)cumfit_.ptr);
+    if (on_gpu()) {
+      roulette_prefix_launch(sc, cfg_.S, (float*)cumfit_.ptr, (float*)cum_ws_.ptr, stream);
+      roulette_guide_launch((const float*)cumfit_.ptr, cfg_.S, (uint32_t*)roul_guide_.ptr, (float*)cum_ws_.ptr, stream);
+    } else {
+      cpu::roulette_prefix(sc, cfg_.S, (float*)cumfit_.ptr);
+    }
   }
   if (cfg_.selection == SEL_RANK) {
     const float* sc = (const float*)scores_[cur_].ptr;
@@ -387,6 +422,7 @@ void Island::run_plain(uint32_t n) {
     GenArgs a = make_args(MODE_GEN);
     n_best_[cur_ ^ 1] = launch(MODE_GEN, a, (unsigned long long*)best_[cur_ ^ 1].ptr);
     stats_ok_[cur_ ^ 1] = a.stats_parts != nullptr;
+    qk_valid_[cur_ ^ 1] = a.qk != nullptr && !jit_;  // every REAL GEN kernel writes the keys it is given
     if (jit_) {
       n_best_[cur_ ^ 1] = jit_eval(rows_[cur_ ^ 1].ptr, (float*)scores_[cur_ ^ 1].ptr, cfg_.S,
                                    (unsigned long long*)best_[cur_ ^ 1].ptr);
@@ -600,6 +636,7 @@ void Island::emigrate(uint32_t k, void* out_rows, float* out_scores) {
 void Island::immigrate(uint32_t k, const void* in_rows, const float* in_scores) {
   TraceRange tr("pga.migrate.immigrate");
   if (k == 0) return;
+  invalidate_qk();
   if (k > cfg_.S) throw std::invalid_argument("k exceeds population size");
   uint16_t* k16 = integer_objective(cfg_.objective, cfg_.L) ? (uint16_t*)keys_[cur_].ptr : nullptr;
   if (mig_policy_ == MIG_STRIPE) {

@@ -272,6 +272,11 @@ struct GenArgs {
   int32_t selection;
   uint32_t tour_k;
   const float* cumfit;  // roulette: inclusive prefix sums of shifted scores (S)
+  // roulette guide table (util.hip roulette_guide_launch): roul_guide[b] = the
+  // first individual whose cumfit bucket is >= b, bucket(t) =
+  // roulette_bucket(t, *roul_scale, S); nullptr: binary search only
+  const uint32_t* roul_guide;
+  const float* roul_scale;
   const uint32_t* rank_order;  // rank: individuals by ascending (score_key, index)
   uint32_t rank_thresh;        // rank: uniform-branch threshold (2 - sp) * 2^32
 
@@ -314,6 +319,10 @@ struct GenArgs {
   // unchanged because the key is exact.  nullptr when disabled.
   const uint16_t* key_cur;
   uint16_t* key_next;
+  // float objectives on the GPU (REAL): key_cur / key_next hold QUANTIZED
+  // keys (qkey) and qk -> {min, max} of the current generation's scores, the
+  // range the kernel quantizes the next generation's keys over
+  const float* qk;
 
   // derived objective data built by the runtime (QUBO: int8 Q^T padded to
   // qubo_padded_length(L) square); nullptr when unused
@@ -394,6 +403,15 @@ PGA_HD u32x4 chunk_flip_mask(const GenArgs& a, uint64_t child, uint32_t c, uint3
 }
 
 PGA_HD bool do_crossover(const GenArgs& a, uint32_t w0) { return a.xo_always || w0 < a.xo_thresh_hi; }
+
+// Roulette guide-table bucket of a cumulative weight t (Chen & Asau's
+// indexed search): any monotone non-decreasing map into [0, B] works, since
+// the pick then scans forward from guide[bucket(target)] to the first
+// cumfit >= target -- the same individual as the binary search.
+PGA_HD uint32_t roulette_bucket(float t, float scale, uint32_t B) {
+  const float x = t * scale;
+  return x >= (float)B ? B : (x > 0.f ? (uint32_t)x : 0u);
+}
 
 // ------------------------------------------------- BINARY randomness layout ---
 // The BINARY encoding draws per child (REAL / PERMUTATION keep the ST_CHILD
@@ -481,6 +499,26 @@ PGA_HD int32_t qubo_coef(float q) {
   float r = q < 0.f ? -__builtin_floorf(-q + 0.5f) : __builtin_floorf(q + 0.5f);
   r = r < -128.f ? -128.f : (r > 127.f ? 127.f : r);
   return (int32_t)r;
+}
+
+// ---- quantized tournament keys (GPU tournaments on float scores) ----
+// A 16-bit key per individual, monotone non-decreasing in its score: q(a) <
+// q(b) implies a < b, so a tournament decides on the 2-byte keys (an array
+// that stays L2-resident, where the f32 scores do not) and only equal keys
+// fall back to comparing the f32 scores -- the exact result either way.
+// lo / scale come from the population's score range; NaN maps to kQkNan,
+// which always falls back.
+constexpr uint32_t kQkNan = 0xFFFFu;
+PGA_HD void qkey_params(float mn, float mx, float& lo, float& scale) {
+  const float d = mx - mn;
+  const bool ok = d > 0.f && d < 3.0e38f && mn > -3.0e38f;
+  lo = ok ? mn : 0.f;
+  scale = ok ? 65534.f / d : 0.f;
+}
+PGA_HD uint32_t qkey(float s, float lo, float scale) {
+  const float x = (s - lo) * scale;
+  if (!(x == x)) return kQkNan;
+  return x <= 0.f ? 0u : (x >= 65534.f ? 65534u : (uint32_t)x);
 }
 
 // orderable encoding of a float score (monotone, -NaN < -inf < ... < +inf)

@@ -189,6 +189,15 @@ class Island {
   uint32_t n_best_[2] = {0, 0};
   Buffer mut_thr_, obj_data_[2], elite_idx_, cumfit_, cum_ws_, topk_ws_, stats_, out_best_, scratch_;
   Buffer rank_order_, rank_ws_;
+  Buffer roul_guide_;  // roulette guide table (GPU), S + 1 entries
+  // REAL on the GPU: quantized u16 tournament keys in keys_[p] (qkey), valid
+  // when qk_valid_[p]; qk_ws_ = {min, max, sum, count} of the current
+  // generation (+ score_stats workspace), the range the GEN kernel quantizes
+  // the next generation's keys over
+  bool real_qk() const;
+  void invalidate_qk() { qk_valid_[cur_] = false; }
+  Buffer qk_ws_;
+  bool qk_valid_[2] = {false, false};
   Buffer qubo_qt_;               // QUBO: int8 Q^T packed from objective data slot 0 (GPU)
   uint32_t obj_version_ = 0, qubo_version_ = ~0u;
   void prepare_objective();      // derived objective data (QUBO packing)

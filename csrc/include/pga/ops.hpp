@@ -99,6 +99,9 @@ uint32_t best_of_scores_launch(const float* scores, uint64_t S, unsigned long lo
                                uint16_t* keys = nullptr);  // keys: also refresh u16 tournament keys
 // keys[i] = (uint16)scores[i] (integer objectives' tournament keys)
 void scores_to_keys_launch(const float* scores, uint64_t S, uint16_t* keys, hipStream_t s);
+// keys[i] = qkey(scores[i]) over the range {min, max} = mm[0..1] (device):
+// the quantized tournament keys of a float objective (core.hpp qkey)
+void scores_to_qkeys_launch(const float* scores, uint64_t S, const float* mm, uint16_t* keys, hipStream_t s);
 // *counter += delta (graph replay: the device-resident generation counter)
 void advance_counter_launch(uint32_t* counter, uint32_t delta, hipStream_t s);
 // stats[0..3] = {min, max, sum, count} of scores (count as float)
@@ -106,8 +109,13 @@ void score_stats_launch(const float* scores, uint64_t S, float* stats, hipStream
 // the same 4 floats from a generation kernel's fused partials (n blocks)
 void stats_from_parts_launch(const float* parts, const unsigned long long* best, uint32_t n, uint64_t S, float* out,
                              hipStream_t s);
-// roulette: cumfit = inclusive prefix sum of max(score - min, 0); workspace >= 2*kMaxGrid floats
+// roulette: cumfit = inclusive prefix sum of max(score - min, 0); then the
+// guide table guide[0..S] for O(1) picks (GenArgs::roul_guide).  workspace:
+// roulette_workspace_floats(S); its word kRoulScale holds the bucket scale.
+constexpr uint32_t kRoulScale = 4 + 3 * 1024 + 1024;
+size_t roulette_workspace_floats(uint64_t S);
 void roulette_prefix_launch(const float* scores, uint64_t S, float* cumfit, float* workspace, hipStream_t s);
+void roulette_guide_launch(const float* cumfit, uint64_t S, uint32_t* guide, float* workspace, hipStream_t s);
 // rank selection: order = indices by ascending (score_key, index); workspace: rank_order_workspace_bytes(S)
 size_t rank_order_workspace_bytes(uint64_t S);
 void rank_order_launch(const float* scores, uint64_t S, uint32_t* order, void* workspace, hipStream_t s);

@@ -27,10 +27,12 @@
 //                 (c << 6) | (32 + n), whose .w is the next skip
 //   crossover     UNIFORM: gene g from A iff bit g % 32 of xo word g / 32
 //                 (word w = register w % 4 of draw(ST_XO, child, w / 4));
-//                 BLEND: gene 4c + j's u from register j of draw(ST_XO, child, c)
+//                 BLEND: gene g's u = word_to_unit(mut_skip_word(misc.y, g)),
+//                 a murmur3 finalizer of the child's seed word (a bijection with
+//                 full avalanche) instead of a Philox block per chunk
 // The per-child words need one Philox block each, so the transposed kernel
-// (real_gen_tp) computes them one lane per child; a gene-parallel lane only
-// draws for BLEND.
+// (real_gen_tp) computes them one lane per child; a gene-parallel lane draws
+// nothing but the UNIFORM mask of genomes beyond 32 genes.
 #pragma once
 
 #include <math.h>
@@ -193,6 +195,8 @@ PGA_HD uint32_t real_cut_word(const GenArgs& a, u32x4 misc) {
     return lo | (hi << 16);
   } else if (a.crossover == XO_ARITHMETIC) {
     return f2u(word_to_unit(misc.y));
+  } else if (a.crossover == XO_BLEND) {
+    return misc.y;  // the per-gene uniforms' seed
   }
   return 0u;
 }
@@ -215,11 +219,9 @@ PGA_HD void real_cross_chunk(const GenArgs& a, uint64_t child, uint32_t c, const
     case XO_UNIFORM:
       for (int j = 0; j < 4; ++j) v[j] = fsel((ubits >> j) & 1u, A[j], B[j]);
       break;
-    case XO_BLEND: {  // BLX-alpha: u in [-alpha, 1 + alpha] per gene
-      const u32x4 r = draw<NH>(a.key, ST_XO, child, c);
-      const uint32_t w[4] = {r.x, r.y, r.z, r.w};
+    case XO_BLEND: {  // BLX-alpha: u in [-alpha, 1 + alpha] per gene, seeded by cut (real_cut_word)
       for (int j = 0; j < 4; ++j) {
-        const float u = fmaf(1.f + 2.f * a.blend_alpha, word_to_unit(w[j]), -a.blend_alpha);
+        const float u = fmaf(1.f + 2.f * a.blend_alpha, word_to_unit(mut_skip_word(cut, 4 * c + j)), -a.blend_alpha);
         v[j] = clampf(fmaf(u, B[j] - A[j], A[j]), a.lo, a.hi);
       }
       break;

@@ -12,10 +12,17 @@
 
 #include "pga/device.hpp"
 
+#ifndef PGA_TP_NOSCORES
+#define PGA_TP_NOSCORES 0
+#endif
+#ifndef PGA_TP_SEG
+#define PGA_TP_SEG 4
+#endif
+
 namespace pga {
 namespace dev {
 
-constexpr uint32_t kSegBatches = 4;   // batches (x 64 children) per tournament segment
+constexpr uint32_t kSegBatches = PGA_TP_SEG;  // batches (x 64 children) per tournament segment
 constexpr uint32_t kTpMaxElite = 64;  // elites the transposed kernels route through their records
 
 // element i of a buffer with a 32-bit byte offset (uniform base + one VGPR)
@@ -24,13 +31,18 @@ __device__ __forceinline__ T ld32(const void* base, uint32_t i) {
   return *(const T*)((const char*)base + i * (uint32_t)sizeof(T));
 }
 
+// Tournament key modes: the f32 scores; the u16 keys of an integer
+// objective (exact); or quantized u16 keys of a float objective (core.hpp
+// qkey: equal keys fall back to the f32 scores, the exact result either way)
+enum TpKeys : int { TP_F32 = 0, TP_KEY16 = 1, TP_QKEY16 = 2 };
+
 // Parents (A, B) of children [begin + 64 B + lane] for the segment's batches
 // B < kSegBatches -> par[B * 64 + lane].  ixs: 4 x 64 uint4 of LDS scratch
-// (the contestants wait there while the loads fly).  KEY: integer
-// objectives compare their u16 tournament keys instead of the f32 scores.
-template <bool KEY>
+// (the contestants wait there while the loads fly).
+template <int KM>
 __device__ __forceinline__ void tp_select_segment(const GenArgs& a, uint32_t begin, uint32_t end, uint32_t lane,
                                                   uint4* ixs, uint2* par) {
+  constexpr bool KEY = KM != TP_F32;
   const uint32_t S = (uint32_t)a.S;
   const uint32_t nbatch = (end - begin + 63) / 64;
   const bool tourn = a.selection == SEL_TOURNAMENT;  // tour_k == 2 guaranteed by the launcher
@@ -65,6 +77,11 @@ __device__ __forceinline__ void tp_select_segment(const GenArgs& a, uint32_t beg
       k1[B] = ld32<uint16_t>(a.key_cur, j.y);
       k2[B] = ld32<uint16_t>(a.key_cur, j.z);
       k3[B] = ld32<uint16_t>(a.key_cur, j.w);
+    } else if constexpr (PGA_TP_NOSCORES) {  // experiment builds: tournaments without score loads
+      k0[B] = (float)(j.x & 1023u);
+      k1[B] = (float)(j.y & 1023u);
+      k2[B] = (float)(j.z & 1023u);
+      k3[B] = (float)(j.w & 1023u);
     } else {
       k0[B] = ld32<float>(a.score_cur, j.x);
       k1[B] = ld32<float>(a.score_cur, j.y);
@@ -73,37 +90,41 @@ __device__ __forceinline__ void tp_select_segment(const GenArgs& a, uint32_t beg
     }
   }
   if (roul) {
-    // fitness-proportional: the 2 x kSegBatches binary searches of
-    // roulette_pick (smallest i with cumfit[i] >= u * total) advance in
-    // lock step, one load each per halving
+    // fitness-proportional, by the guide table: the pick is the smallest i
+    // with cumfit[i] >= u * total (roulette_pick's binary search); the guide
+    // entry of the target's bucket is a lower bound for it, so one guide load,
+    // one cumfit load and (rarely) a short forward scan find it.  The
+    // 2 x kSegBatches picks of a lane advance in lock step.
     constexpr uint32_t NS = 2 * kSegBatches;
     const float total = a.cumfit[S - 1];
-    uint32_t lo[NS], hi[NS];
+    const float scale = *a.roul_scale;
+    uint32_t ix[NS];
     float tg[NS];
-#pragma unroll
+    #pragma unroll
     for (uint32_t i = 0; i < NS; ++i) {
       const uint32_t w = __builtin_bit_cast(uint32_t, (i & 1u) ? k1[i >> 1] : k0[i >> 1]);
       tg[i] = word_to_unit(w) * total;
-      lo[i] = total > 0.f ? 0u : word_to_index(w, S);
-      hi[i] = total > 0.f ? S - 1 : lo[i];
+      ix[i] = total > 0.f ? ld32<uint32_t>(a.roul_guide, roulette_bucket(tg[i], scale, S)) : word_to_index(w, S);
     }
-    for (uint32_t n = S; n > 1; n = (n + 1) >> 1) {  // wave-uniform trip count
-      float v[NS];
-#pragma unroll
-      for (uint32_t i = 0; i < NS; ++i) v[i] = ld32<float>(a.cumfit, (lo[i] + hi[i]) >> 1);
-#pragma unroll
+    float v[NS];
+    #pragma unroll
+    for (uint32_t i = 0; i < NS; ++i) v[i] = ld32<float>(a.cumfit, ix[i]);
+    for (uint32_t it = 0; it < S; ++it) {  // wave-uniform: until every pick of every lane is resolved
+      bool more = false;
+      #pragma unroll
+      for (uint32_t i = 0; i < NS; ++i) more |= total > 0.f && v[i] < tg[i];
+      if (!__any(more)) break;
+      #pragma unroll
       for (uint32_t i = 0; i < NS; ++i) {
-        const uint32_t mid = (lo[i] + hi[i]) >> 1;
-        if (lo[i] < hi[i]) {
-          if (v[i] < tg[i]) lo[i] = mid + 1;
-          else hi[i] = mid;
-        }
+        const bool adv = total > 0.f && v[i] < tg[i];
+        ix[i] += adv ? 1u : 0u;
+        v[i] = ld32<float>(a.cumfit, ix[i]);
       }
     }
-#pragma unroll
+    #pragma unroll
     for (uint32_t B = 0; B < kSegBatches; ++B) {
-      k0[B] = __builtin_bit_cast(KT, lo[2 * B]);
-      k1[B] = __builtin_bit_cast(KT, lo[2 * B + 1]);
+      k0[B] = __builtin_bit_cast(KT, ix[2 * B]);
+      k1[B] = __builtin_bit_cast(KT, ix[2 * B + 1]);
     }
   }
 #pragma unroll
@@ -113,6 +134,14 @@ __device__ __forceinline__ void tp_select_segment(const GenArgs& a, uint32_t beg
     if (tourn) {
       pa = k0[B] < k1[B] ? ix.y : ix.x;
       pb = k2[B] < k3[B] ? ix.w : ix.z;
+      if constexpr (KM == TP_QKEY16) {  // equal quantized keys: the exact compare (rare, divergent)
+        const uint32_t q0 = __builtin_bit_cast(uint32_t, k0[B]), q1 = __builtin_bit_cast(uint32_t, k1[B]);
+        const uint32_t q2 = __builtin_bit_cast(uint32_t, k2[B]), q3 = __builtin_bit_cast(uint32_t, k3[B]);
+        if (q0 == q1 || q0 == kQkNan || q1 == kQkNan)
+          pa = ld32<float>(a.score_cur, ix.x) < ld32<float>(a.score_cur, ix.y) ? ix.y : ix.x;
+        if (q2 == q3 || q2 == kQkNan || q3 == kQkNan)
+          pb = ld32<float>(a.score_cur, ix.z) < ld32<float>(a.score_cur, ix.w) ? ix.w : ix.z;
+      }
     } else if (rank || roul) {
       pa = __builtin_bit_cast(uint32_t, k0[B]);
       pb = __builtin_bit_cast(uint32_t, k1[B]);

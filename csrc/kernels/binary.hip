@@ -403,6 +403,11 @@ __global__ __launch_bounds__(kBlock) void binary_kernel(GenArgs a, unsigned long
 // paths, so a conditionally issued load would make the next wait drain it).
 // ---------------------------------------------------------------------------
 
+#ifdef PGA_TP_TIMING
+// experiment builds only (tools/variants.sh): per-wave clocks of the two phases
+__device__ unsigned long long pga_tp_clk[kMaxGrid * 4][4];
+#endif
+
 constexpr uint32_t kTpMaxElite = 64;  // elites the fast kernel routes through its records
 constexpr uint32_t kSegBatches = 4;   // batches (x 64 children) per tournament segment
 
@@ -412,11 +417,23 @@ constexpr uint32_t kSegBatches = 4;   // batches (x 64 children) per tournament 
 #ifndef PGA_TP_WAVES
 #define PGA_TP_WAVES 5
 #endif
+#ifndef PGA_TP_NOKEYS
+#define PGA_TP_NOKEYS 0
+#endif
 
 __device__ __forceinline__ uint32_t pos16(uint4 r1, uint32_t k) {  // k-th packed 16-bit position
   const uint32_t w = sel4(u32x4{r1.x, r1.y, r1.z, r1.w}, k >> 1);
   return (k & 1u) ? (w >> 16) : (w & 0xFFFFu);
 }
+
+// the uniform-crossover mask of chunk q of child c (ST_XO block q); experiment
+// builds can swap in a multiplicative hash to measure the Philox's share
+#ifdef PGA_TP_XOHASH
+#define PGA_TP_XOMASK(c, q) make_uint4(mut_skip_word((c) * 4u, (q)), mut_skip_word((c) * 4u + 1u, (q)), \
+                                       mut_skip_word((c) * 4u + 2u, (q)), mut_skip_word((c) * 4u + 3u, (q)))
+#else
+#define PGA_TP_XOMASK(c, q) u4(draw<true>(a.key, ST_XO, (c), (q)))
+#endif
 
 template <int GS, int OBJ, bool FULL, bool DENSE>
 __global__ __launch_bounds__(kBlock, OBJ == kObjKnapMfma ? 4 : PGA_TP_WAVES) void binary_gen_tp(GenArgs a, unsigned long long* best_parts) {
@@ -490,10 +507,17 @@ __global__ __launch_bounds__(kBlock, OBJ == kObjKnapMfma ? 4 : PGA_TP_WAVES) voi
   uint4(*rec)[64][2] = lds_rec[wid];
   uint2* par = lds_par[wid];
   static_assert(sizeof(lds_rec[0]) >= kSegBatches * 64 * sizeof(uint4), "contestant staging");
+#ifdef PGA_TP_TIMING
+  const unsigned long long clk0 = clock64();
+  unsigned long long clk_t = 0, clk_b = 0;
+#endif
   for (uint32_t begin = wbegin; begin < wend; begin += kSegBatches * 64u) {  // wave-uniform
     const uint32_t end = begin + kSegBatches * 64u < wend ? begin + kSegBatches * 64u : wend;
     const uint32_t nsteps = (end - begin + NG - 1) / NG;
     const uint32_t nbatch = (end - begin + 63) / 64;
+#ifdef PGA_TP_TIMING
+    const unsigned long long clkA = clock64();
+#endif
 
     // TOURNAMENTS of the whole segment: all key loads in flight at once; the
     // contestants wait in the record ring (free until the first RESOLVE)
@@ -523,6 +547,11 @@ __global__ __launch_bounds__(kBlock, OBJ == kObjKnapMfma ? 4 : PGA_TP_WAVES) voi
           const uint32_t rb = rank_pick(blk.w, b1.x, b1.y, S, a.rank_thresh);
           k0[B] = __builtin_bit_cast(KT, ELEM(const uint32_t, a.rank_order, ra));
           k1[B] = __builtin_bit_cast(KT, ELEM(const uint32_t, a.rank_order, rb));
+        } else if constexpr (KEY && PGA_TP_NOKEYS) {  // experiment: tournaments without key reads
+          k0[B] = j.x & 1023u;
+          k1[B] = j.y & 1023u;
+          k2[B] = j.z & 1023u;
+          k3[B] = j.w & 1023u;
         } else if constexpr (KEY) {
           k0[B] = ELEM(const uint16_t, a.key_cur, j.x);
           k1[B] = ELEM(const uint16_t, a.key_cur, j.y);
@@ -539,37 +568,41 @@ __global__ __launch_bounds__(kBlock, OBJ == kObjKnapMfma ? 4 : PGA_TP_WAVES) voi
         // the extra batches skip the Philox draw and are never resolved
       }
       if (roul) {
-        // fitness-proportional: the 2 x kSegBatches binary searches of
-        // roulette_pick (smallest i with cumfit[i] >= u * total) advance in
-        // lock step, one load each per halving, ceil(log2 S) halvings
+        // fitness-proportional, by the guide table: the pick is the smallest i
+        // with cumfit[i] >= u * total (roulette_pick's binary search); the guide
+        // entry of the target's bucket is a lower bound for it, so one guide load,
+        // one cumfit load and (rarely) a short forward scan find it.  The
+        // 2 x kSegBatches picks of a lane advance in lock step.
         constexpr uint32_t NS = 2 * kSegBatches;
         const float total = a.cumfit[S - 1];
-        uint32_t lo[NS], hi[NS];
+        const float scale = *a.roul_scale;
+        uint32_t ix[NS];
         float tg[NS];
-#pragma unroll
+        #pragma unroll
         for (uint32_t i = 0; i < NS; ++i) {
           const uint32_t w = __builtin_bit_cast(uint32_t, (i & 1u) ? k1[i >> 1] : k0[i >> 1]);
           tg[i] = word_to_unit(w) * total;
-          lo[i] = total > 0.f ? 0u : word_to_index(w, S);
-          hi[i] = total > 0.f ? S - 1 : lo[i];
+          ix[i] = total > 0.f ? ELEM(const uint32_t, a.roul_guide, roulette_bucket(tg[i], scale, S)) : word_to_index(w, S);
         }
-        for (uint32_t n = S; n > 1; n = (n + 1) >> 1) {  // wave-uniform trip count
-          float v[NS];
-#pragma unroll
-          for (uint32_t i = 0; i < NS; ++i) v[i] = ELEM(const float, a.cumfit, (lo[i] + hi[i]) >> 1);
-#pragma unroll
+        float v[NS];
+        #pragma unroll
+        for (uint32_t i = 0; i < NS; ++i) v[i] = ELEM(const float, a.cumfit, ix[i]);
+        for (uint32_t it = 0; it < S; ++it) {  // wave-uniform: until every pick of every lane is resolved
+          bool more = false;
+          #pragma unroll
+          for (uint32_t i = 0; i < NS; ++i) more |= total > 0.f && v[i] < tg[i];
+          if (!__any(more)) break;
+          #pragma unroll
           for (uint32_t i = 0; i < NS; ++i) {
-            const uint32_t mid = (lo[i] + hi[i]) >> 1;
-            if (lo[i] < hi[i]) {
-              if (v[i] < tg[i]) lo[i] = mid + 1;
-              else hi[i] = mid;
-            }
+            const bool adv = total > 0.f && v[i] < tg[i];
+            ix[i] += adv ? 1u : 0u;
+            v[i] = ELEM(const float, a.cumfit, ix[i]);
           }
         }
-#pragma unroll
+        #pragma unroll
         for (uint32_t B = 0; B < kSegBatches; ++B) {
-          k0[B] = __builtin_bit_cast(KT, lo[2 * B]);
-          k1[B] = __builtin_bit_cast(KT, lo[2 * B + 1]);
+          k0[B] = __builtin_bit_cast(KT, ix[2 * B]);
+          k1[B] = __builtin_bit_cast(KT, ix[2 * B + 1]);
         }
       }
 #pragma unroll
@@ -586,6 +619,10 @@ __global__ __launch_bounds__(kBlock, OBJ == kObjKnapMfma ? 4 : PGA_TP_WAVES) voi
         par[B * 64u + lane] = make_uint2(pa, pb);
       }
     }
+#ifdef PGA_TP_TIMING
+    const unsigned long long clkB = clock64();
+    clk_t += clkB - clkA;
+#endif
 
     // RESOLVE: parents, crossover plan and flip positions of batch B -> records
 #define PGA_TP_RESOLVE(B)                                                                                       \
@@ -663,7 +700,7 @@ __global__ __launch_bounds__(kBlock, OBJ == kObjKnapMfma ? 4 : PGA_TP_WAVES) voi
     const uint32_t c = begin + (t) * NG + g;                                                                \
     const uint4 r0 = rec[b & 1u][i * NG + g][0];                                                            \
     const uint32_t meta = r0.w;                                                                             \
-    const uint4 m = range ? range_keep_a(q, r0.z & 0xFFFFu, r0.z >> 16) : u4(draw<true>(a.key, ST_XO, c, q)); \
+    const uint4 m = range ? range_keep_a(q, r0.z & 0xFFFFu, r0.z >> 16) : PGA_TP_XOMASK(c, q);               \
     uint4 v = mix4(XA, XB, m);                                                                              \
     if (last) v = and4(v, lmask);                                                                           \
     uint4 fm = make_uint4(0, 0, 0, 0);                                                                      \
@@ -715,9 +752,22 @@ __global__ __launch_bounds__(kBlock, OBJ == kObjKnapMfma ? 4 : PGA_TP_WAVES) voi
     if (t < nsteps) PGA_TP_STEP(t, A0, B0, A1, B1)
 #undef PGA_TP_RESOLVE
 #undef PGA_TP_STEP
+#ifdef PGA_TP_TIMING
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this segment's stores issued and done
+    clk_b += clock64() - clkB;
+#endif
   }
 #undef ROW
 #undef ELEM
+#ifdef PGA_TP_TIMING
+  if (lane == 0) {
+    const uint32_t wv = blockIdx.x * NW + wid;
+    pga_tp_clk[wv][0] = clk_t;
+    pga_tp_clk[wv][1] = clk_b;
+    pga_tp_clk[wv][2] = clock64() - clk0;
+    pga_tp_clk[wv][3] = wend - wbegin;
+  }
+#endif
   unsigned long long bb = block_max_u64(my_best, lds_red);
   if (threadIdx.x == 0 && best_parts && EVALS) best_parts[blockIdx.x] = bb;
   if (EVALS && best_parts && a.stats_parts) block_stats_store(st, a.stats_parts);
@@ -738,7 +788,7 @@ uint32_t launch_mode(int mode, const GenArgs& a, unsigned long long* parts, hipS
       const bool fast = a.chunks <= (uint32_t)GS &&
                         ((a.selection == SEL_TOURNAMENT && a.tour_k == 2) || a.selection == SEL_RANDOM ||
                          (a.selection == SEL_RANK && a.rank_order != nullptr) ||
-                         (a.selection == SEL_ROULETTE && a.cumfit != nullptr)) &&
+                         (a.selection == SEL_ROULETTE && a.cumfit != nullptr && a.roul_guide != nullptr)) &&
                         !(a.n_elite > 1 && a.elite_idx == nullptr) && !force_generic_kernels();
       constexpr bool INT_OBJ = OBJ == OBJ_ONEMAX || OBJ == OBJ_LEADING_ONES || OBJ == OBJ_TRAP;
       // 32-bit offsets: the (S + kRowPad)-row buffers must stay below 4 GiB
@@ -788,6 +838,27 @@ uint32_t launch_obj(int mode, const GenArgs& a, unsigned long long* parts, hipSt
 }
 
 }  // namespace
+
+#ifdef PGA_TP_TIMING
+// experiment builds: mean per-wave cycles of the tournament / breed phases of
+// the last binary_gen_tp launch (bench/gen_bench.cpp prints it)
+extern "C" void pga_tp_timing_dump(uint32_t nwaves) {
+  static unsigned long long h[kMaxGrid * 4][4];
+  PGA_HIP_CHECK(hipMemcpyFromSymbol(h, HIP_SYMBOL(pga_tp_clk), sizeof(h)));
+  double t = 0, b = 0, tot = 0, n = 0, mx = 0;
+  for (uint32_t i = 0; i < nwaves && i < kMaxGrid * 4; ++i) {
+    if (h[i][2] == 0) continue;
+    t += (double)h[i][0];
+    b += (double)h[i][1];
+    tot += (double)h[i][2];
+    mx = std::max(mx, (double)h[i][2]);
+    n += 1;
+  }
+  std::printf("{\"tp_timing\": {\"waves\": %.0f, \"tourn_cycles\": %.0f, \"breed_cycles\": %.0f, "
+              "\"wave_cycles\": %.0f, \"max_wave_cycles\": %.0f, \"tourn_frac\": %.3f}}\n",
+              n, t / n, b / n, tot / n, mx, t / (t + b));
+}
+#endif
 
 bool build_knap_table(const float* values, const float* weights, uint32_t L, uint32_t chunks,
                       std::vector<uint8_t>& tab, uint32_t& digits, uint32_t& cols) {

@@ -149,6 +149,8 @@ __global__ __launch_bounds__(kBlock) void real_kernel(GenArgs a, unsigned long l
   const bool shift = (a.obj_i & 1) && a.obj_data2 && real_obj_rotatable(a.objective);
   const bool tile_needed = ROT || a.objective == OBJ_TSP_RANDOM_KEY || a.objective == OBJ_USER_FNPTR ||
                            a.objective == OBJ_ROSENBROCK;
+  float qlo = 0.f, qscale = 0.f;  // quantized tournament keys of the children (GEN, when kept)
+  if (MODE == MODE_GEN && a.key_next && a.qk) qkey_params(a.qk[0], a.qk[1], qlo, qscale);
 
   // ---- per-block setup ----
   if (MODE == MODE_GEN && a.n_elite > 0 && a.elite_idx == nullptr && blockIdx.x == 0) {
@@ -293,6 +295,7 @@ __global__ __launch_bounds__(kBlock) void real_kernel(GenArgs a, unsigned long l
       }
       if (valid && q == 0) {
         a.score_next[child] = score;
+        if (MODE == MODE_GEN && a.key_next) a.key_next[child] = (uint16_t)qkey(score, qlo, qscale);
         const unsigned long long pb = pack_best(score, child);
         my_best = pb > my_best ? pb : my_best;
         st.add(score);
@@ -342,6 +345,8 @@ __global__ __launch_bounds__(kBlock) void real_long_kernel(GenArgs a, unsigned l
   const bool shift = (a.obj_i & 1) && a.obj_data2 && real_obj_rotatable(a.objective);
   const bool rosen = a.objective == OBJ_ROSENBROCK;
   uint32_t* mpos = lds_mpos[g];
+  float qlo = 0.f, qscale = 0.f;  // quantized tournament keys of the children (GEN, when kept)
+  if (MODE == MODE_GEN && a.key_next && a.qk) qkey_params(a.qk[0], a.qk[1], qlo, qscale);
 
   if (MODE == MODE_GEN && a.n_elite > 0 && a.elite_idx == nullptr && blockIdx.x == 0) {
     unsigned long long b = block_reduce_parts(a.best_cur, a.n_best_cur, lds_red);
@@ -454,6 +459,7 @@ __global__ __launch_bounds__(kBlock) void real_long_kernel(GenArgs a, unsigned l
     }
     if (evals && q == 0) {
       a.score_next[child] = score;
+      if (MODE == MODE_GEN && a.key_next) a.key_next[child] = (uint16_t)qkey(score, qlo, qscale);
       const unsigned long long pk = pack_best(score, child);
       my_best = pk > my_best ? pk : my_best;
       st.add(score);
@@ -571,6 +577,7 @@ __device__ __forceinline__ void rot_tile4(float* xw, const float* ms, float z[4]
 #define PGA_RTP_WAVES 4
 #endif
 
+
 template <int GS, int OBJ, bool ROT>
 __global__ __launch_bounds__(kBlock, PGA_RTP_WAVES) void real_gen_tp(GenArgs a, unsigned long long* best_parts) {
   static_assert(!ROT || GS == 4 || GS == 8, "wave-local rotation: 16 or 32 padded dims");
@@ -612,6 +619,9 @@ __global__ __launch_bounds__(kBlock, PGA_RTP_WAVES) void real_gen_tp(GenArgs a, 
     w1[j] = 0.f;
     if (EVALS && d < L) real_obj_data(a, d, w0[j], w1[j]);
   }
+  // quantization of the next generation's tournament keys
+  float qlo = 0.f, qscale = 0.f;
+  if (EVALS) qkey_params(a.qk[0], a.qk[1], qlo, qscale);
   // 32-bit offsets (the launcher checks (S + pad) rows < 4 GiB)
   const uint32_t rb = a.row_words * 4u;
 #define RROW(base, row, ch) (*(float4*)((char*)(base) + ((uint32_t)(row) * rb + (uint32_t)(ch) * 16u)))
@@ -654,8 +664,9 @@ __global__ __launch_bounds__(kBlock, PGA_RTP_WAVES) void real_gen_tp(GenArgs a, 
     const uint32_t nsteps = (end - begin + NG - 1) / NG;
     const uint32_t nbatch = (end - begin + 63) / 64;
 
-    // TOURNAMENTS of the whole segment (contestants wait in the record ring)
-    tp_select_segment<false>(a, begin, end, lane, &rec[0][0][0], par);
+    // TOURNAMENTS of the whole segment (contestants wait in the record ring),
+    // on the quantized u16 keys when the objective scores the children here
+    tp_select_segment<EVALS ? TP_QKEY16 : TP_F32>(a, begin, end, lane, &rec[0][0][0], par);
 
     // RESOLVE: parents, crossover plan, mutation positions and draws of batch B -> records
 #define PGA_RTP_RESOLVE(B)                                                                                   \
@@ -775,6 +786,7 @@ __global__ __launch_bounds__(kBlock, PGA_RTP_WAVES) void real_gen_tp(GenArgs a, 
       acc.s2 = group_prod<GS>(acc.s2);                                                                      \
       const float sc = real_obj_finish(a, acc);                                                             \
       RELEM(float, a.score_next, c) = sc; /* every lane of the group stores the same score */              \
+      RELEM(uint16_t, a.key_next, c) = (uint16_t)qkey(sc, qlo, qscale);                                     \
       const unsigned long long pk = c < S ? pack_best(sc, c) : 0ull;                                        \
       my_best = pk > my_best ? pk : my_best;                                                                \
       st.add_if(q == 0u && c < S, sc);                                                                      \
@@ -812,9 +824,11 @@ bool real_tp_eligible(const GenArgs& a, uint32_t GS, bool rot) {
   if (rot && GS != 4 && GS != 8) return false;
   const bool sel_ok = (a.selection == SEL_TOURNAMENT && a.tour_k == 2) || a.selection == SEL_RANDOM ||
                       (a.selection == SEL_RANK && a.rank_order != nullptr) ||
-                      (a.selection == SEL_ROULETTE && a.cumfit != nullptr);
+                      (a.selection == SEL_ROULETTE && a.cumfit != nullptr && a.roul_guide != nullptr);
   if (!sel_ok) return false;
   if (a.n_elite > kTpMaxElite || (a.n_elite > 1 && a.elite_idx == nullptr)) return false;
+  // evaluating instances tournament on quantized keys (the Island keeps them)
+  if (a.objective != OBJ_NONE && (!a.key_cur || !a.key_next || !a.qk)) return false;
   // 32-bit offsets: the (S + kRowPad)-row buffers must stay below 4 GiB
   return (a.S + kRowPad) * (uint64_t)a.row_words * 4u <= 0xFFFFFFFFull;
 }

@@ -219,7 +219,7 @@ __global__ __launch_bounds__(kBlock) void prefix_part_kernel(const float* s, uin
   if (threadIdx.x == 0) block_sums[blockIdx.x] = sm;
 }
 
-__global__ __launch_bounds__(kBlock) void prefix_blocks_kernel(float* block_sums, uint32_t n) {
+__global__ __launch_bounds__(kBlock) void prefix_blocks_kernel(float* block_sums, uint32_t n, uint64_t S, float* meta) {
   // exclusive scan of n block sums, single block, sequential tiles
   __shared__ float lds[kBlock / 64];
   float carry = 0.f;
@@ -231,6 +231,41 @@ __global__ __launch_bounds__(kBlock) void prefix_blocks_kernel(float* block_sums
     if (i < n) block_sums[i] = carry + inc - v;
     carry += total;
     __syncthreads();
+  }
+  // guide-table scale ~ S / total (any positive value is exact, see
+  // roulette_bucket) and a zeroed long-span counter for roulette_guide_launch
+  if (threadIdx.x == 0) {
+    meta[0] = carry > 0.f ? (float)S / carry : 0.f;
+    ((uint32_t*)meta)[1] = 0u;
+  }
+}
+
+// guide[b] = i for every bucket b in (bucket(cumfit[i-1]), bucket(cumfit[i])];
+// spans of 32 buckets or more (one individual holding >= 32/S of the total
+// weight) go to a list that roulette_span_kernel fills cooperatively, so no
+// thread loops over a heavy individual's buckets
+__global__ __launch_bounds__(kBlock) void roulette_guide_kernel(const float* c, uint64_t S, const float* meta,
+                                                                 uint32_t* guide, uint32_t* nspans, uint4* spans) {
+  const float scale = meta[0];
+  const uint32_t B = (uint32_t)S;
+  for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < S; i += (uint64_t)gridDim.x * kBlock) {
+    const uint32_t hi = roulette_bucket(c[i], scale, B);
+    const uint32_t lo = i ? roulette_bucket(c[i - 1], scale, B) + 1u : 0u;
+    if (hi < lo) continue;
+    if (hi - lo < 32u) {
+      for (uint32_t b = lo; b <= hi; ++b) guide[b] = (uint32_t)i;
+    } else {
+      spans[atomicAdd(nspans, 1u)] = make_uint4(lo, hi, (uint32_t)i, 0u);
+    }
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void roulette_span_kernel(const uint32_t* nspans, const uint4* spans,
+                                                                uint32_t* guide) {
+  const uint32_t n = *nspans;
+  for (uint32_t k = blockIdx.x; k < n; k += gridDim.x) {
+    const uint4 sp = spans[k];
+    for (uint32_t b = sp.x + threadIdx.x; b <= sp.y; b += kBlock) guide[b] = sp.z;
   }
 }
 
@@ -903,6 +938,14 @@ __global__ __launch_bounds__(kBlock) void scores_to_keys_kernel(const float* s, 
   }
 }
 
+__global__ __launch_bounds__(kBlock) void scores_to_qkeys_kernel(const float* s, uint64_t S, const float* mm,
+                                                                  uint16_t* k) {
+  float lo, scale;
+  qkey_params(mm[0], mm[1], lo, scale);
+  for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < S; i += (uint64_t)gridDim.x * kBlock)
+    k[i] = (uint16_t)qkey(s[i], lo, scale);
+}
+
 inline size_t align_up(size_t x) { return (x + 255) & ~(size_t)255; }
 
 __global__ void advance_counter_kernel(uint32_t* c, uint32_t d) {
@@ -932,6 +975,12 @@ uint32_t best_of_scores_launch(const float* scores, uint64_t S, unsigned long lo
 void scores_to_keys_launch(const float* scores, uint64_t S, uint16_t* keys, hipStream_t s) {
   uint32_t grid = launch_grid(S, kBlock * 4);
   hipLaunchKernelGGL(scores_to_keys_kernel, grid, kBlock, 0, s, scores, S, keys);
+  PGA_HIP_CHECK(hipGetLastError());
+}
+
+void scores_to_qkeys_launch(const float* scores, uint64_t S, const float* mm, uint16_t* keys, hipStream_t s) {
+  uint32_t grid = launch_grid(S, kBlock * 4);
+  hipLaunchKernelGGL(scores_to_qkeys_kernel, grid, kBlock, 0, s, scores, S, mm, keys);
   PGA_HIP_CHECK(hipGetLastError());
 }
 
@@ -974,6 +1023,11 @@ void score_stats_launch(const float* scores, uint64_t S, float* stats, hipStream
   PGA_HIP_CHECK(hipGetLastError());
 }
 
+size_t roulette_workspace_floats(uint64_t S) {
+  // stats | stats partials | block sums | scale, span count, pad | spans (uint4)
+  return kRoulScale + 4 + 4 * ((S + 1) / 32 + 2);
+}
+
 void roulette_prefix_launch(const float* scores, uint64_t S, float* cumfit, float* ws, hipStream_t s) {
   // ws layout: [0..4) stats, [4 .. 4+3*1024) stats partials, then block sums
   score_stats_launch(scores, S, ws, s);
@@ -982,8 +1036,18 @@ void roulette_prefix_launch(const float* scores, uint64_t S, float* cumfit, floa
   const uint64_t per_block = (S + grid - 1) / grid;
   float* block_sums = ws + 4 + 3 * 1024;
   hipLaunchKernelGGL(prefix_part_kernel, grid, kBlock, 0, s, scores, S, per_block, ws, block_sums);
-  hipLaunchKernelGGL(prefix_blocks_kernel, 1, kBlock, 0, s, block_sums, grid);
+  hipLaunchKernelGGL(prefix_blocks_kernel, 1, kBlock, 0, s, block_sums, grid, S, ws + kRoulScale);
   hipLaunchKernelGGL(prefix_final_kernel, grid, kBlock, 0, s, scores, S, per_block, ws, block_sums, cumfit);
+  PGA_HIP_CHECK(hipGetLastError());
+}
+
+void roulette_guide_launch(const float* cumfit, uint64_t S, uint32_t* guide, float* ws, hipStream_t s) {
+  const uint32_t grid = launch_grid(S, kBlock);
+  uint32_t* nspans = (uint32_t*)(ws + kRoulScale) + 1;
+  uint4* spans = (uint4*)(ws + kRoulScale + 4);
+  hipLaunchKernelGGL(roulette_guide_kernel, grid, kBlock, 0, s, cumfit, S, (const float*)(ws + kRoulScale), guide,
+                     nspans, spans);
+  hipLaunchKernelGGL(roulette_span_kernel, 64, kBlock, 0, s, (const uint32_t*)nspans, (const uint4*)spans, guide);
   PGA_HIP_CHECK(hipGetLastError());
 }
 

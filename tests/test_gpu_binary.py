@@ -215,7 +215,7 @@ def test_rank_selection_bitexact(sp):
 @pytest.mark.parametrize("sel", ["rank", "roulette"])
 def test_rank_roulette_fast_kernel_bitexact(prob, elitism, sel):
     """Linear ranking (two rank picks, two rank-order loads per child) and
-    roulette (eight lock-step binary searches per lane) in the fast kernel's
+    roulette (guide table: one guide + one cumfit load per pick) in the fast kernel's
     first phase: u16-key objectives at full and partial lane groups, and an
     f32-score objective (non-integer knapsack), bit-exact vs the CPU backend."""
     g0 = torch.Generator().manual_seed(3)
@@ -237,6 +237,27 @@ def test_rank_roulette_fast_kernel_bitexact(prob, elitism, sel):
         g.run(1)
         c.run(1)
         same(g, c)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("heavy", [0, 1 << 20])
+def test_roulette_guide_table_heavy_tail(heavy):
+    """Roulette picks through the guide table equal the CPU's binary search
+    on integer-valued scores (exact prefix sums), also when one individual
+    holds half the weight (its bucket span goes through the long-span list)
+    and when most weights are zero (long runs of equal cumfit)."""
+    S = 65536
+    g, c = pair(pga.models.OneMax(64), S, seed=9, selection="roulette", elitism=1)
+    gen = torch.Generator().manual_seed(5)
+    sc = torch.randint(0, 16, (S,), generator=gen).float()
+    sc[torch.rand(S, generator=gen) < 0.6] = 0.0  # 60% zero weight (min 0)
+    sc[1234] = float(heavy) if heavy else sc[1234]
+    for ga in (g, c):
+        ga.scores.copy_(sc.to(ga.scores.device))
+        ga.island.rebest()
+    g.run(1)
+    c.run(1)
+    same(g, c)
 
 
 @pytest.mark.gpu
