@@ -18,6 +18,8 @@
 #include <sched.h>
 #include <unistd.h>
 
+#include <exception>
+
 #include "pga/cpu.hpp"
 
 namespace pga {
@@ -39,20 +41,32 @@ class WorkerPool {
   }
   unsigned size() const { return (unsigned)threads_.size() + 1; }
 
-  // run job(slot) for slot in [0, n): slot 0 on the caller, the rest on workers
+  // run job(slot) for slot in [0, n): slot 0 on the caller, the rest on
+  // workers.  Every slot runs to its end before run() returns, a throwing one
+  // included; the first exception (caller's or a worker's) is rethrown here.
   void run(unsigned n, const std::function<void(unsigned)>& job) {
     {
       std::lock_guard<std::mutex> g(m_);
       job_ = &job;
       active_ = n;
       pending_ = n - 1;
+      error_ = nullptr;
       ++epoch_;
     }
     cv_.notify_all();
-    job(0);
+    std::exception_ptr mine;
+    try {
+      job(0);
+    } catch (...) {
+      mine = std::current_exception();
+    }
     std::unique_lock<std::mutex> l(m_);
     done_.wait(l, [&] { return pending_ == 0; });
     job_ = nullptr;
+    std::exception_ptr e = mine ? mine : error_;
+    error_ = nullptr;
+    l.unlock();
+    if (e) std::rethrow_exception(e);
   }
 
   std::mutex busy;  // one generation at a time; concurrent callers run serially
@@ -68,8 +82,14 @@ class WorkerPool {
       if (id >= active_) continue;
       const std::function<void(unsigned)>* job = job_;
       l.unlock();
-      (*job)(id);
+      std::exception_ptr e;
+      try {
+        (*job)(id);
+      } catch (...) {
+        e = std::current_exception();
+      }
       l.lock();
+      if (e && !error_) error_ = e;
       if (--pending_ == 0) done_.notify_one();
     }
   }
@@ -79,6 +99,7 @@ class WorkerPool {
   std::condition_variable cv_, done_;
   const std::function<void(unsigned)>* job_ = nullptr;
   unsigned active_ = 0, pending_ = 0;
+  std::exception_ptr error_;  // first worker exception of the current run
   uint64_t epoch_ = 0;
   bool stop_ = false;
 };

@@ -391,7 +391,8 @@ void Island::prepare_generation() {
   if (cfg_.selection == SEL_RANK) {
     const float* sc = (const float*)scores_[cur_].ptr;
     if (on_gpu() && integer_objective(cfg_.objective, cfg_.L) && keys_[cur_].ptr)
-      rank_order16_launch((const uint16_t*)keys_[cur_].ptr, cfg_.S, (uint32_t*)rank_order_.ptr, rank_ws_.ptr, stream);
+      rank_order16_launch((const uint16_t*)keys_[cur_].ptr, cfg_.S, cfg_.L + 1, (uint32_t*)rank_order_.ptr,
+                          rank_ws_.ptr, stream);
     else if (on_gpu()) rank_order_launch(sc, cfg_.S, (uint32_t*)rank_order_.ptr, rank_ws_.ptr, stream);
     else cpu::rank_order(sc, cfg_.S, (uint32_t*)rank_order_.ptr);
   }
@@ -429,7 +430,7 @@ void Island::run_plain(uint32_t n) {
       stats_ok_[cur_ ^ 1] = false;
     }
     swap();
-    if (hist_on_ && !capturing_) append_history();
+    if (hist_on_ && !hist_manual_ && !capturing_) append_history();
   }
 }
 

@@ -340,6 +340,7 @@ struct GenArgs {
   // padding mask for the last chunk (BINARY)
   u32x4 last_mask;
 
+
   // hipGraph replay: when set, the generation counter is read from device
   // memory (key.gen = *gen_dev + gen_off) so one captured graph of G
   // generations can be replayed without re-recording kernel arguments

@@ -110,6 +110,14 @@ class Island {
   // fused partials, no pass over the scores); history() copies the rows out.
   // Turning it on clears the history and disables hipGraph replay.
   void set_stats_history(bool on);
+  // manual history: generations append no row themselves; the caller appends
+  // one per generation with record_history_row() once the scores are final
+  // (an objective evaluated outside the island, e.g. GeneticAlgorithm's
+  // torch_objective)
+  void set_history_manual(bool on) { hist_manual_ = on; }
+  void record_history_row() {
+    if (hist_on_) append_history();
+  }
   bool stats_history() const { return hist_on_; }
   std::vector<float> history();
   std::vector<uint32_t> topk_host(uint32_t k, bool largest);
@@ -214,7 +222,7 @@ class Island {
   Buffer hist_;
   std::vector<float> hist_host_;  // CPU backend
   uint64_t hist_n_ = 0;
-  bool hist_on_ = false;
+  bool hist_on_ = false, hist_manual_ = false;
   int mig_policy_ = MIG_TOPK;
   float mut_inv_ = 0.f;
   bool mut_sparse_ = false;  // BINARY bit-flip uses the sparse (Binomial) sampler

@@ -116,11 +116,20 @@ constexpr uint32_t kRoulScale = 4 + 3 * 1024 + 1024;
 size_t roulette_workspace_floats(uint64_t S);
 void roulette_prefix_launch(const float* scores, uint64_t S, float* cumfit, float* workspace, hipStream_t s);
 void roulette_guide_launch(const float* cumfit, uint64_t S, uint32_t* guide, float* workspace, hipStream_t s);
+// stable LSD radix sort (sort.hip, 4-bit digits, one decoupled look-back
+// launch per digit): (keys, vals) by the low `bits` bits of the keys,
+// ascending, or descending (all 32 bits; equal keys keep their order).
+// vals == nullptr: the values are 0..n-1.  n < 2^30.
+size_t radix_sort_workspace_bytes(uint64_t n);
+void radix_sort_pairs(const uint32_t* keys, const uint32_t* vals, uint64_t n, uint32_t bits, bool descending,
+                      uint32_t* keys_out, uint32_t* vals_out, void* workspace, hipStream_t s);
 // rank selection: order = indices by ascending (score_key, index); workspace: rank_order_workspace_bytes(S)
 size_t rank_order_workspace_bytes(uint64_t S);
 void rank_order_launch(const float* scores, uint64_t S, uint32_t* order, void* workspace, hipStream_t s);
-// the same order from the u16 tournament keys of an integer objective (2 radix passes)
-void rank_order16_launch(const uint16_t* keys16, uint64_t S, uint32_t* order, void* workspace, hipStream_t s);
+// the same order from the u16 tournament keys of an integer objective (keys
+// < key_range: only their bits are sorted, 3 passes for OneMax-1024)
+void rank_order16_launch(const uint16_t* keys16, uint64_t S, uint32_t key_range, uint32_t* order, void* workspace,
+                         hipStream_t s);
 // top-k by score (descending, ties -> lower index); idx_out[k]; workspace: topk_workspace_bytes(S)
 size_t topk_workspace_bytes(uint64_t S, uint32_t k);
 // sorted = false: the k indices in selection order (keys above the threshold by

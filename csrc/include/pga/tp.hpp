@@ -15,6 +15,7 @@
 #ifndef PGA_TP_NOSCORES
 #define PGA_TP_NOSCORES 0
 #endif
+// batches (x 64 children) per tournament segment
 #ifndef PGA_TP_SEG
 #define PGA_TP_SEG 4
 #endif
@@ -22,7 +23,7 @@
 namespace pga {
 namespace dev {
 
-constexpr uint32_t kSegBatches = PGA_TP_SEG;  // batches (x 64 children) per tournament segment
+constexpr uint32_t kSegBatches = PGA_TP_SEG;
 constexpr uint32_t kTpMaxElite = 64;  // elites the transposed kernels route through their records
 
 // element i of a buffer with a 32-bit byte offset (uniform base + one VGPR)
@@ -150,14 +151,29 @@ __device__ __forceinline__ void tp_select_segment(const GenArgs& a, uint32_t beg
   }
 }
 
-// this wave's children [wbegin, wend): contiguous, a multiple of NG long
-__device__ __forceinline__ void tp_wave_range(uint32_t S, uint32_t NG, uint32_t& wbegin, uint32_t& wend) {
+// Work distribution of the transposed kernels: wave w of the grid breeds the
+// contiguous children [w per, (w + 1) per), per = ceil(S / W) rounded up to
+// a multiple of the children per step (NG).  Equal static shares leave a
+// tail: a SIMD issues oldest-wave-first, so the first-dispatched eighth of
+// the waves ends at ~54 us on average and the last at ~74 (phase clocks,
+// round 3), and the kernel's last ~20 us run on a thinning grid.  Two ways
+// to balance it were measured and dropped (tools/gpu_exp3.sh, gpu_exp4.sh):
+//   - dynamic units of 128 children pulled from 64 ticket heads, each on its
+//     own 128-B line: +14 us per generation of device-scope atomic latency
+//     (one shared line for every ticket: 10x the kernel);
+//   - shares skewed by dispatch order (1 +- s): the young waves still ended
+//     last (s = 0.15 moved the first eighth's mean end 54 -> 58 us, the last
+//     eighth's not at all); +3 us on the headline, +4 us on Rastrigin.
+__device__ __forceinline__ void tp_wave_range(uint32_t S, uint32_t NG, uint32_t& wbegin, uint32_t& wend,
+                                              uint32_t& first) {
   constexpr uint32_t NW = kBlock / 64;
   const uint64_t W = (uint64_t)gridDim.x * NW, w = (uint64_t)blockIdx.x * NW + (threadIdx.x >> 6);
   uint64_t per = (S + W - 1) / W;
   per = (per + NG - 1) / NG * NG;
   wbegin = (uint32_t)(w * per < S ? w * per : S);
   wend = (uint32_t)(wbegin + per < S ? wbegin + per : S);
+  const uint64_t f = (uint64_t)blockIdx.x * NW * per;
+  first = (uint32_t)(f < S ? f : S);
 }
 
 }  // namespace dev

@@ -28,6 +28,7 @@
 
 #include "pga/device.hpp"
 #include "pga/ops.hpp"
+#include "pga/tp.hpp"
 
 namespace pga {
 namespace {
@@ -404,12 +405,13 @@ __global__ __launch_bounds__(kBlock) void binary_kernel(GenArgs a, unsigned long
 // ---------------------------------------------------------------------------
 
 #ifdef PGA_TP_TIMING
-// experiment builds only (tools/variants.sh): per-wave clocks of the two phases
-__device__ unsigned long long pga_tp_clk[kMaxGrid * 4][4];
+// experiment builds only (tools/variants.sh): per-wave clocks of the two
+// phases, wall-clock start / end and the XCD the wave ran on
+__device__ unsigned long long pga_tp_clk[kMaxGrid * 4][8];
 #endif
 
-constexpr uint32_t kTpMaxElite = 64;  // elites the fast kernel routes through its records
-constexpr uint32_t kSegBatches = 4;   // batches (x 64 children) per tournament segment
+// kTpMaxElite (elites the fast kernel routes through its records),
+// kSegBatches and the work units: tp.hpp
 
 // 5 waves/SIMD: 4, 5 and 6 measured alike for the breed phase alone (the
 // fabric, not occupancy, is the bound); 5 gives the tournament phase its
@@ -479,15 +481,12 @@ __global__ __launch_bounds__(kBlock, OBJ == kObjKnapMfma ? 4 : PGA_TP_WAVES) voi
 #define ROW(base, row, ch) (*(uint4*)((char*)(base) + ((uint32_t)(row) * rb + (uint32_t)(ch) * 16u)))
 
   // this wave's children [wbegin, wend): contiguous, a multiple of NG long
-  const uint64_t W = (uint64_t)gridDim.x * NW, w = (uint64_t)blockIdx.x * NW + wid;
-  uint64_t per = (S + W - 1) / W;
-  per = (per + NG - 1) / NG * NG;
-  const uint32_t wbegin = (uint32_t)(w * per < S ? w * per : S);
-  const uint32_t wend = (uint32_t)(wbegin + per < S ? wbegin + per : S);
+  uint32_t wbegin, wend, bfirst;
+  tp_wave_range(S, NG, wbegin, wend, bfirst);
 
   // elite sources of children [0, n_elite) (n_elite <= kTpMaxElite), for the
   // blocks that hold any of them
-  if (a.n_elite > 0 && (uint64_t)blockIdx.x * NW * per < a.n_elite) {
+  if (a.n_elite > 0 && bfirst < a.n_elite) {
     if (a.elite_idx) {
       for (uint32_t i = threadIdx.x; i < a.n_elite; i += kBlock) lds_el[i] = a.elite_idx[i];
     } else {
@@ -508,7 +507,7 @@ __global__ __launch_bounds__(kBlock, OBJ == kObjKnapMfma ? 4 : PGA_TP_WAVES) voi
   uint2* par = lds_par[wid];
   static_assert(sizeof(lds_rec[0]) >= kSegBatches * 64 * sizeof(uint4), "contestant staging");
 #ifdef PGA_TP_TIMING
-  const unsigned long long clk0 = clock64();
+  const unsigned long long clk0 = clock64(), rt0 = wall_clock64();
   unsigned long long clk_t = 0, clk_b = 0;
 #endif
   for (uint32_t begin = wbegin; begin < wend; begin += kSegBatches * 64u) {  // wave-uniform
@@ -766,6 +765,9 @@ __global__ __launch_bounds__(kBlock, OBJ == kObjKnapMfma ? 4 : PGA_TP_WAVES) voi
     pga_tp_clk[wv][1] = clk_b;
     pga_tp_clk[wv][2] = clock64() - clk0;
     pga_tp_clk[wv][3] = wend - wbegin;
+    pga_tp_clk[wv][4] = rt0;
+    pga_tp_clk[wv][5] = wall_clock64();
+    pga_tp_clk[wv][6] = __builtin_amdgcn_s_getreg((3 << 11) | 20);  // HW_REG_XCC_ID[3:0]
   }
 #endif
   unsigned long long bb = block_max_u64(my_best, lds_red);
@@ -794,13 +796,16 @@ uint32_t launch_mode(int mode, const GenArgs& a, unsigned long long* parts, hipS
       // 32-bit offsets: the (S + kRowPad)-row buffers must stay below 4 GiB
       const bool o32 = (a.S + kRowPad) * (uint64_t)a.row_words * 4u <= 0xFFFFFFFFull;
       if (fast && o32 && a.n_elite <= kTpMaxElite && (!INT_OBJ || a.key_cur != nullptr)) {
+        if constexpr (OBJ == OBJ_KNAPSACK && GS >= 4 && GS <= 32) {
+          if (a.knap_tab != nullptr &&
+              (a.knap_cols == 0 || a.knap_cols > kKnapMaxCols || a.knap_dig == 0 || a.knap_dig > 4 ||
+               a.knap_cols != (uint32_t)GS / 2u * a.knap_dig))
+            throw std::invalid_argument("knapsack digit table does not match the genome geometry");
+        }
         const bool dense = a.mutation == MUT_BIT_FLIP && a.mut_rate > 0.f && !a.mut_sparse;
         const bool full = a.chunks == (uint32_t)GS;
         if constexpr (OBJ == OBJ_KNAPSACK && GS >= 4 && GS <= 32) {
           if (a.knap_tab != nullptr) {  // integer-exact instance: the matrix-core evaluation
-            if (a.knap_cols == 0 || a.knap_cols > kKnapMaxCols || a.knap_dig == 0 || a.knap_dig > 4 ||
-                a.knap_cols != (uint32_t)GS / 2u * a.knap_dig)
-              throw std::invalid_argument("knapsack digit table does not match the genome geometry");
             if (full) {
               if (dense) return go(binary_gen_tp<GS, kObjKnapMfma, true, true>, a, parts, kBlock, s);
               return go(binary_gen_tp<GS, kObjKnapMfma, true, false>, a, parts, kBlock, s);
@@ -843,9 +848,11 @@ uint32_t launch_obj(int mode, const GenArgs& a, unsigned long long* parts, hipSt
 // experiment builds: mean per-wave cycles of the tournament / breed phases of
 // the last binary_gen_tp launch (bench/gen_bench.cpp prints it)
 extern "C" void pga_tp_timing_dump(uint32_t nwaves) {
-  static unsigned long long h[kMaxGrid * 4][4];
+  static unsigned long long h[kMaxGrid * 4][8];
   PGA_HIP_CHECK(hipMemcpyFromSymbol(h, HIP_SYMBOL(pga_tp_clk), sizeof(h)));
   double t = 0, b = 0, tot = 0, n = 0, mx = 0;
+  unsigned long long rt_min = ~0ull, rt_max = 0, st_max = 0;
+  uint32_t nw = 0;
   for (uint32_t i = 0; i < nwaves && i < kMaxGrid * 4; ++i) {
     if (h[i][2] == 0) continue;
     t += (double)h[i][0];
@@ -853,10 +860,33 @@ extern "C" void pga_tp_timing_dump(uint32_t nwaves) {
     tot += (double)h[i][2];
     mx = std::max(mx, (double)h[i][2]);
     n += 1;
+    rt_min = std::min(rt_min, h[i][4]);
+    rt_max = std::max(rt_max, h[i][5]);
+    st_max = std::max(st_max, h[i][4]);
+    nw = i + 1;
   }
   std::printf("{\"tp_timing\": {\"waves\": %.0f, \"tourn_cycles\": %.0f, \"breed_cycles\": %.0f, "
-              "\"wave_cycles\": %.0f, \"max_wave_cycles\": %.0f, \"tourn_frac\": %.3f}}\n",
-              n, t / n, b / n, tot / n, mx, t / (t + b));
+              "\"wave_cycles\": %.0f, \"max_wave_cycles\": %.0f, \"tourn_frac\": %.3f, "
+              "\"span_us\": %.2f, \"last_start_us\": %.2f}}\n",
+              n, t / n, b / n, tot / n, mx, t / (t + b), (rt_max - rt_min) / 100.0, (st_max - rt_min) / 100.0);
+  // wall-clock end time (us after the first start, 100 MHz clock) per XCD and
+  // by block order (older blocks first): is the tail an XCD or an age effect?
+  double xe[8] = {0}, xm[8] = {0}, xn[8] = {0};
+  const uint32_t bins = 8;
+  double be[bins] = {0}, bm[bins] = {0}, bn[bins] = {0}, bs[bins] = {0};
+  for (uint32_t i = 0; i < nw; ++i) {
+    if (h[i][2] == 0) continue;
+    const double e = (h[i][5] - rt_min) / 100.0, st = (h[i][4] - rt_min) / 100.0;
+    const uint32_t x = (uint32_t)(h[i][6] & 7u), k = i * bins / nw;
+    xe[x] += e; xn[x] += 1; xm[x] = std::max(xm[x], e);
+    be[k] += e; bn[k] += 1; bm[k] = std::max(bm[k], e); bs[k] += st;
+  }
+  std::printf("{\"tp_xcd_end_us\": [");
+  for (int x = 0; x < 8; ++x) std::printf("%s[%.1f, %.1f]", x ? ", " : "", xn[x] ? xe[x] / xn[x] : 0.0, xm[x]);
+  std::printf("], \"tp_order_start_end_max_us\": [");
+  for (uint32_t k = 0; k < bins; ++k)
+    std::printf("%s[%.1f, %.1f, %.1f]", k ? ", " : "", bn[k] ? bs[k] / bn[k] : 0.0, bn[k] ? be[k] / bn[k] : 0.0, bm[k]);
+  std::printf("]}\n");
 }
 #endif
 

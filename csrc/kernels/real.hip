@@ -627,8 +627,8 @@ __global__ __launch_bounds__(kBlock, PGA_RTP_WAVES) void real_gen_tp(GenArgs a, 
 #define RROW(base, row, ch) (*(float4*)((char*)(base) + ((uint32_t)(row) * rb + (uint32_t)(ch) * 16u)))
 #define RELEM(T, base, i) (*(T*)((char*)(base) + (uint32_t)(i) * (uint32_t)sizeof(T)))
 
-  uint32_t wbegin, wend;
-  tp_wave_range(S, NG, wbegin, wend);
+  uint32_t wbegin, wend, bfirst;  // this wave's children (tp.hpp)
+  tp_wave_range(S, NG, wbegin, wend, bfirst);
 
   float* xw = lds_rot + (ROT ? wid * 16 * kRotTW : 0);  // this wave's X/Z tile
   float* ms = lds_rot + (ROT ? NW * 16 * kRotTW : 0);   // M[n][k], block-shared
@@ -637,17 +637,13 @@ __global__ __launch_bounds__(kBlock, PGA_RTP_WAVES) void real_gen_tp(GenArgs a, 
       const uint32_t n = i / kRotTW, k = i % kRotTW;
       ms[i] = (n < L && k < L) ? a.obj_data[n * L + k] : 0.f;
     }
-  // elite sources of children [0, n_elite) for the blocks that hold any of them
-  {
-    uint32_t per = (uint32_t)((S + (uint64_t)gridDim.x * NW - 1) / ((uint64_t)gridDim.x * NW));
-    per = (per + NG - 1) / NG * NG;
-    if (a.n_elite > 0 && (uint64_t)blockIdx.x * NW * per < a.n_elite) {
-      if (a.elite_idx) {
-        for (uint32_t i = threadIdx.x; i < a.n_elite; i += kBlock) lds_el[i] = a.elite_idx[i];
-      } else {
-        unsigned long long b = block_reduce_parts(a.best_cur, a.n_best_cur, lds_red);
-        if (threadIdx.x == 0) lds_el[0] = (uint32_t)best_index(b);
-      }
+  // elite sources of children [0, n_elite), for the blocks that hold any of them
+  if (a.n_elite > 0 && bfirst < a.n_elite) {
+    if (a.elite_idx) {
+      for (uint32_t i = threadIdx.x; i < a.n_elite; i += kBlock) lds_el[i] = a.elite_idx[i];
+    } else {
+      unsigned long long b = block_reduce_parts(a.best_cur, a.n_best_cur, lds_red);
+      if (threadIdx.x == 0) lds_el[0] = (uint32_t)best_index(b);
     }
   }
   if (per_gene)

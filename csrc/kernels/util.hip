@@ -5,7 +5,6 @@
 // (pga_get_best, src/pga.cu:218-236) and implements its stubbed top-N /
 // migration entry points (src/pga.cu:238-248, :368-374) on the device.
 #include <hip/hip_runtime.h>
-#include <hipcub/hipcub.hpp>
 
 #include <cmath>
 #include <mutex>
@@ -1051,78 +1050,11 @@ void roulette_guide_launch(const float* cumfit, uint64_t S, uint32_t* guide, flo
   PGA_HIP_CHECK(hipGetLastError());
 }
 
-// ---------------- rank order (linear ranking selection) ----------------
-// order = individuals by ascending (score_key, index): keys + iota, then one
-// stable LSD radix sort of 32-bit keys (hipcub; 4 passes of 8 bits on gfx950)
-__global__ __launch_bounds__(kBlock) void rank_keys_kernel(const float* s, uint64_t S, uint32_t* keys, uint32_t* idx) {
-  for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < S; i += (uint64_t)gridDim.x * kBlock) {
-    keys[i] = score_key(s[i]);
-    idx[i] = (uint32_t)i;
-  }
-}
-
-namespace {
-size_t rank_cub_bytes(uint64_t S) {
-  size_t b = 0;
-  PGA_HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(nullptr, b, (uint32_t*)nullptr, (uint32_t*)nullptr,
-                                                   (uint32_t*)nullptr, (uint32_t*)nullptr, (int)S));
-  return (b + 255) & ~(size_t)255;
-}
-}  // namespace
-
-size_t rank_order_workspace_bytes(uint64_t S) {
-  const size_t arr = ((4 * S) + 255) & ~(size_t)255;
-  return 3 * arr + rank_cub_bytes(S);
-}
-
-__global__ __launch_bounds__(kBlock) void iota_kernel(uint64_t S, uint32_t* idx) {
-  for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < S; i += (uint64_t)gridDim.x * kBlock)
-    idx[i] = (uint32_t)i;
-}
-
-// integer objectives: the u16 tournament keys order exactly like the scores
-// (non-negative integers <= 65535), so two 8-bit radix passes suffice
-void rank_order16_launch(const uint16_t* keys16, uint64_t S, uint32_t* order, void* ws, hipStream_t s) {
-  if (S >= (1ull << 31)) throw std::runtime_error("rank selection: population too large for the device sort");
-  const size_t arr = ((4 * S) + 255) & ~(size_t)255;
-  uint16_t* keys_out = (uint16_t*)((char*)ws + arr);
-  uint32_t* idx_in = (uint32_t*)((char*)ws + 2 * arr);
-  void* tmp = (char*)ws + 3 * arr;
-  size_t tb = 0;
-  PGA_HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, keys16, keys_out, idx_in, order, (int)S, 0, 16, s));
-  if (tb > rank_cub_bytes(S)) throw std::runtime_error("rank selection: workspace too small");
-  tb = rank_cub_bytes(S);
-  uint32_t grid = launch_grid(S, kBlock * 4);
-  if (grid > 2048) grid = 2048;
-  hipLaunchKernelGGL(iota_kernel, grid, kBlock, 0, s, S, idx_in);
-  PGA_HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(tmp, tb, keys16, keys_out, idx_in, order, (int)S, 0, 16, s));
-  PGA_HIP_CHECK(hipGetLastError());
-}
-
-void rank_order_launch(const float* scores, uint64_t S, uint32_t* order, void* ws, hipStream_t s) {
-  if (S >= (1ull << 31)) throw std::runtime_error("rank selection: population too large for the device sort");
-  const size_t arr = ((4 * S) + 255) & ~(size_t)255;
-  uint32_t* keys_in = (uint32_t*)ws;
-  uint32_t* keys_out = (uint32_t*)((char*)ws + arr);
-  uint32_t* idx_in = (uint32_t*)((char*)ws + 2 * arr);
-  void* tmp = (char*)ws + 3 * arr;
-  size_t tb = rank_cub_bytes(S);
-  uint32_t grid = launch_grid(S, kBlock * 4);
-  if (grid > 2048) grid = 2048;
-  hipLaunchKernelGGL(rank_keys_kernel, grid, kBlock, 0, s, scores, S, keys_in, idx_in);
-  PGA_HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(tmp, tb, keys_in, keys_out, idx_in, order, (int)S, 0, 32, s));
-  PGA_HIP_CHECK(hipGetLastError());
-}
-
 size_t topk_workspace_bytes(uint64_t S, uint32_t k) {
-  size_t cub_bytes = 0;
-  PGA_HIP_CHECK(hipcub::DeviceRadixSort::SortPairsDescending(nullptr, cub_bytes, (uint32_t*)nullptr,
-                                                             (uint32_t*)nullptr, (uint32_t*)nullptr,
-                                                             (uint32_t*)nullptr, (int)k));
   (void)S;
-  // layout: state | counts | 3 k-arrays | cub temp | value histogram (kept zeroed)
+  // layout: state | counts | 3 k-arrays | radix-sort workspace (sorted mode) | value histogram (kept zeroed)
   return align_up(sizeof(TopkState)) + align_up(sizeof(uint32_t) * (2 * 1024 + 4)) + 3 * align_up(4ull * k) +
-         align_up(cub_bytes) + align_up(4ull * kTopkMaxRange);
+         align_up(radix_sort_workspace_bytes(k)) + align_up(4ull * kTopkMaxRange);
 }
 
 namespace {
@@ -1161,12 +1093,8 @@ void topk_run(TopkKeys<BITS> keys, uint64_t S, uint32_t k, bool sorted, uint32_t
   }
   hipLaunchKernelGGL(topk_write_kernel<BITS>, cgrid, kBlock, 0, s, keys, S, per_block, st, cnt, cgrid, keys_buf, idx);
   PGA_HIP_CHECK(hipGetLastError());
-  size_t cub_bytes = 0;
-  PGA_HIP_CHECK(hipcub::DeviceRadixSort::SortPairsDescending(nullptr, cub_bytes, keys_buf, keys_sorted, idx, idx_out,
-                                                             (int)k));
-  // stable descending sort keeps equal keys in ascending index order
-  PGA_HIP_CHECK(hipcub::DeviceRadixSort::SortPairsDescending(p, cub_bytes, keys_buf, keys_sorted, idx, idx_out,
-                                                             (int)k, 0, BITS, s));
+  // stable descending sort (sort.hip) keeps equal keys in ascending index order
+  radix_sort_pairs(keys_buf, idx, k, BITS, true, keys_sorted, idx_out, p, s);
 }
 }  // namespace
 
@@ -1188,11 +1116,7 @@ void topk_launch(const float* scores, const uint16_t* keys16, uint32_t key_range
     uint32_t* cnt = (uint32_t*)p;
     p += align_up(sizeof(uint32_t) * (2 * 1024 + 4));
     p += 3 * align_up(4ull * k);
-    size_t cub_bytes = 0;
-    PGA_HIP_CHECK(hipcub::DeviceRadixSort::SortPairsDescending(nullptr, cub_bytes, (uint32_t*)nullptr,
-                                                               (uint32_t*)nullptr, (uint32_t*)nullptr,
-                                                               (uint32_t*)nullptr, (int)k));
-    p += align_up(cub_bytes);
+    p += align_up(radix_sort_workspace_bytes(k));
     uint32_t* G = (uint32_t*)p;  // zero on allocation and after every use
     const uint32_t R = key_range;
     uint32_t grid = launch_grid(S, kBlock * 16);

@@ -9,7 +9,9 @@
 #include <torch/extension.h>
 #include <pybind11/stl.h>
 
+#include <atomic>
 #include <memory>
+#include <stdexcept>
 
 #include "pga/cpu.hpp"
 #include "pga/island.hpp"
@@ -125,6 +127,21 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     pga::cpu::perm_crossover(op, A.data(), B.data(), (uint32_t)A.size(), lo, hi, C.data());
     return C;
   });
+  // test hook of the CPU worker pool: sums [0, n) over the pool's slots; the
+  // slot holding index throw_at (if < n) throws, which must surface here as
+  // one exception after every slot has finished
+  m.def("_pool_sum", [](uint64_t n, uint64_t throw_at) {
+    std::atomic<uint64_t> sum{0};
+    pga::cpu::parallel_for(n, 1, [&](uint64_t b, uint64_t e, unsigned) {
+      uint64_t acc = 0;
+      for (uint64_t i = b; i < e; ++i) {
+        if (i == throw_at) throw std::runtime_error("pool test: slot failed");
+        acc += i;
+      }
+      sum += acc;
+    });
+    return sum.load();
+  });
   // the deterministic Box-Muller of the REAL gaussian mutation (real_ops.hpp)
   m.def("gauss_z", [](uint32_t w1, uint32_t w2) { return pga::gauss_z(w1, w2); });
   m.def("gauss_z_batch", [](torch::Tensor w) {
@@ -184,6 +201,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
            },
            py::arg("n"), py::arg("target"), py::arg("check_every") = 10)
       .def("set_stats_history", &Island::set_stats_history)
+      .def("set_history_manual", &Island::set_history_manual)
+      .def("record_history_row", &Island::record_history_row)
       .def_property_readonly("stats_history", &Island::stats_history)
       .def("history",
            [](Island& i) {

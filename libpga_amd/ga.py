@@ -179,6 +179,7 @@ class GeneticAlgorithm:
                 for _ in range(n):
                     self._island.run(1)
                     self._custom_eval()
+                    self._island.record_history_row()  # from the evaluated scores
             done += n
             if target is not None and self.best_score() >= target:
                 break
@@ -213,6 +214,9 @@ class GeneticAlgorithm:
         """Start (clearing) or stop the per-generation statistics history:
         every generation appends {min, max, sum, count} on the device from
         its kernel's fused partials (no pass over the scores, no sync)."""
+        # a torch objective scores each generation after its kernel: its rows
+        # are appended once _custom_eval has run (GeneticAlgorithm.run)
+        self._island.set_history_manual(self.torch_objective is not None)
         self._island.set_stats_history(bool(on))
 
     def history(self) -> torch.Tensor:

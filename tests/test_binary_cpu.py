@@ -258,3 +258,34 @@ def test_rank_selection_converges_and_is_deterministic():
     assert runs[0].max().item() == 64.0
     with pytest.raises(Exception):
         make(pga.models.OneMax(64), S=64, selection="rank", rank_pressure=2.5)
+
+
+def test_worker_pool_exceptions():
+    """A throwing slot of the CPU worker pool (csrc/cpu/parallel.cpp) surfaces
+    as one exception on the caller after every slot finished, on the caller's
+    slot and on a worker's alike, and the pool keeps working afterwards."""
+    from libpga_amd import _C
+    n = 4096
+    assert _C._pool_sum(n, n) == n * (n - 1) // 2
+    for bad in (0, n - 1, n // 2):
+        with pytest.raises(RuntimeError, match="slot failed"):
+            _C._pool_sum(n, bad)
+        assert _C._pool_sum(n, n) == n * (n - 1) // 2
+
+
+def test_torch_objective_history():
+    """History rows of a torch-objective run are the statistics of the scores
+    that objective produced (rows appended after its evaluation), one per
+    generation, equal to stats() taken after every step."""
+    fn = lambda g: (g[:, ::2].float().sum(-1) - g[:, 1::2].float().sum(-1))  # noqa: E731
+    ga = make(pga.models.BinaryTorchObjective(64, fn, optimum=32), S=256, elitism=1)
+    ga.record_history()
+    want = []
+    for _ in range(5):
+        ga.step()
+        s = ga.stats()
+        want.append([s["min"], s["max"], s["mean"]])
+    h = ga.history()
+    assert h.shape == (5, 4)
+    assert torch.allclose(h[:, :3], torch.tensor(want), rtol=1e-6, atol=1e-5)
+    assert torch.all(h[:, 3] == 256)

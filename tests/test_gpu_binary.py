@@ -353,16 +353,17 @@ def stripe_reference(scores, rows, k):
 @pytest.mark.parametrize("S,k", [(5000, 50), (100003, 997)])
 @pytest.mark.parametrize("prob", ["onemax", "knapsack"])
 def test_stripe_migration_gpu(S, k, prob):
-    """Stripe policy (the default): GPU == CPU backend bit for bit, == the
-    torch reference, and the immigrate kernel's fused best partials and
-    statistics describe the new population exactly."""
+    """Stripe policy (opt-in; exact top-k is the default): GPU == CPU
+    backend bit for bit, == the torch reference, and the immigrate kernel's
+    fused best partials and statistics describe the new population exactly."""
     p = pga.models.OneMax(1024) if prob == "onemax" else pga.models.Knapsack01.random(700, seed=4)
     g, c = pair(p, S, elitism=1)
     g.run(3)
     c.run(3)
     same(g, c)
     gi, ci = g.island, c.island
-    assert gi.migration_policy == pga._ext.C.MIG_STRIPE
+    assert gi.migration_policy == pga._ext.C.MIG_TOPK  # the default
+    gi.migration_policy = ci.migration_policy = pga._ext.C.MIG_STRIPE
     rw = int(gi.row_words)
     out_g = torch.empty(k * rw, dtype=torch.int32, device=DEV), torch.empty(k, device=DEV)
     out_c = torch.empty(k * rw, dtype=torch.int32), torch.empty(k)

@@ -28,7 +28,8 @@ BUILD = os.path.join(ROOT, "build")
 ARCH = os.environ.get("PGA_ARCH", "gfx950")
 
 KERNELS = ["csrc/kernels/binary.hip", "csrc/kernels/real.hip", "csrc/kernels/perm.hip",
-           "csrc/kernels/util.hip", "csrc/kernels/compat.hip", "csrc/kernels/qubo.hip"]
+           "csrc/kernels/util.hip", "csrc/kernels/compat.hip", "csrc/kernels/qubo.hip",
+           "csrc/kernels/sort.hip"]
 HOST = ["csrc/engine/island.cpp", "csrc/engine/trace.cpp", "csrc/engine/jit.cpp", "csrc/cpu/cpu_ops.cpp", "csrc/cpu/cpu_real.cpp", "csrc/cpu/cpu_perm.cpp", "csrc/cpu/parallel.cpp"]
 CAPI = ["csrc/capi/pga_capi.cpp", "csrc/capi/comm.cpp", "csrc/capi/comm_rccl.cpp"]
 COMPAT = []
