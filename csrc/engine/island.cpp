@@ -382,7 +382,9 @@ void Island::prepare_generation() {
   if (cfg_.selection == SEL_ROULETTE) {
     const float* sc = (const float*)scores_[cur_].ptr;
     if (on_gpu()) {
-      roulette_prefix_launch(sc, cfg_.S, (float*)cumfit_.ptr, (float*)cum_ws_.ptr, stream);
+      const bool fused = stats_ok_[cur_] && stats_parts_[cur_].ptr;  // min from the GEN kernel's partials
+      roulette_prefix_launch(sc, cfg_.S, fused ? (const float*)stats_parts_[cur_].ptr : nullptr, n_best_[cur_],
+                             (float*)cumfit_.ptr, (float*)cum_ws_.ptr, stream);
       roulette_guide_launch((const float*)cumfit_.ptr, cfg_.S, (uint32_t*)roul_guide_.ptr, (float*)cum_ws_.ptr, stream);
     } else {
       cpu::roulette_prefix(sc, cfg_.S, (float*)cumfit_.ptr);

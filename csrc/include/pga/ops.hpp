@@ -112,14 +112,17 @@ void stats_from_parts_launch(const float* parts, const unsigned long long* best,
 // roulette: cumfit = inclusive prefix sum of max(score - min, 0); then the
 // guide table guide[0..S] for O(1) picks (GenArgs::roul_guide).  workspace:
 // roulette_workspace_floats(S); its word kRoulScale holds the bucket scale.
+// The minimum comes from the generation kernel's fused {min, sum} partials
+// (parts, nparts blocks) when given, else from a score pass.
 constexpr uint32_t kRoulScale = 4 + 3 * 1024 + 1024;
 size_t roulette_workspace_floats(uint64_t S);
-void roulette_prefix_launch(const float* scores, uint64_t S, float* cumfit, float* workspace, hipStream_t s);
+void roulette_prefix_launch(const float* scores, uint64_t S, const float* parts, uint32_t nparts, float* cumfit,
+                            float* workspace, hipStream_t s);
 void roulette_guide_launch(const float* cumfit, uint64_t S, uint32_t* guide, float* workspace, hipStream_t s);
-// stable LSD radix sort (sort.hip, 4-bit digits, one decoupled look-back
-// launch per digit): (keys, vals) by the low `bits` bits of the keys,
-// ascending, or descending (all 32 bits; equal keys keep their order).
-// vals == nullptr: the values are 0..n-1.  n < 2^30.
+// stable LSD radix sort (sort.hip: reduce-then-scan, digits of up to 8 bits,
+// count / scan / scatter launches per pass): (keys, vals) by the low `bits`
+// bits of the keys, ascending, or descending (all 32 bits; equal keys keep
+// their order).  vals == nullptr: the values are 0..n-1.  n < 2^32.
 size_t radix_sort_workspace_bytes(uint64_t n);
 void radix_sort_pairs(const uint32_t* keys, const uint32_t* vals, uint64_t n, uint32_t bits, bool descending,
                       uint32_t* keys_out, uint32_t* vals_out, void* workspace, hipStream_t s);
@@ -127,7 +130,7 @@ void radix_sort_pairs(const uint32_t* keys, const uint32_t* vals, uint64_t n, ui
 size_t rank_order_workspace_bytes(uint64_t S);
 void rank_order_launch(const float* scores, uint64_t S, uint32_t* order, void* workspace, hipStream_t s);
 // the same order from the u16 tournament keys of an integer objective (keys
-// < key_range: only their bits are sorted, 3 passes for OneMax-1024)
+// < key_range: only their bits are sorted, 2 passes for OneMax-1024)
 void rank_order16_launch(const uint16_t* keys16, uint64_t S, uint32_t key_range, uint32_t* order, void* workspace,
                          hipStream_t s);
 // top-k by score (descending, ties -> lower index); idx_out[k]; workspace: topk_workspace_bytes(S)

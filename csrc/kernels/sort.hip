@@ -1,20 +1,24 @@
 // sort.hip — stable LSD radix sort of (key, value) pairs on gfx950, written
 // for the engine's two sorts: the rank order of linear-ranking selection
-// (every generation, S keys) and the sorted top-k (k keys).  No library sort:
-// 4-bit digits, one "onesweep" launch per digit (Merrill & Garland's
-// decoupled look-back single-pass scan, applied per digit).
+// (every generation, S keys) and the sorted top-k (k keys).  No library sort.
 //
-// Per pass a workgroup takes the next TILE = 256 x 8 keys (tile ids handed
-// out by an atomic ticket, so every lower tile is already owned by a resident
-// workgroup and the look-back below always terminates), ranks them stably in
-// LDS (a [16 digits][256 threads] counter table, scanned digit-major), then
-// lanes 0..15 of wave 0 publish the tile's per-digit counts and look back over
-// the earlier tiles' status words for the exclusive prefix of each digit.  A
-// status word carries its own payload ({flag, count} in 32 bits, one store),
-// so neither side needs a fence: the consumer polls it with L1-bypassing
-// atomic loads.  Keys land at digit_base[d] + prefix[d] + local rank.
-// digit_base comes from one up-front histogram launch that counts every
-// pass's digits at once (digit counts do not depend on the key order).
+// Reduce-then-scan, up to 8-bit digits (the passes split the key bits evenly:
+// OneMax-1024's 11-bit keys sort in 6 + 5 bits), three launches per pass:
+//   COUNT    a workgroup per TILE of 4096 keys counts its digits into
+//            counts[digit * tiles + tile] (digit-major);
+//   SCAN     exclusive scan of counts: each entry becomes the global output
+//            base of (digit, tile) — one launch of 1024 threads when the table
+//            fits 16384 entries (1M keys / 6-bit digits does), else two levels;
+//   SCATTER  the tile again, every wave its own 1024 consecutive keys in 16
+//            rounds of 64: the lanes that share a digit find each other with
+//            one ballot per digit bit (a match-any), rank among themselves by
+//            popcount below the lane, and bump the wave's LDS digit counter
+//            once per group.  Stable by construction (rounds in key order,
+//            lanes in key order, waves in key order), no atomics, no look-back
+//            chain: every workgroup of a pass is independent.
+// The previous onesweep design (decoupled look-back over 512 tiles of 2048
+// keys, 4-bit digits) serialised on the look-back: 28 us per pass at 1M keys
+// (profiles/rank_roulette_r03.md).
 //
 // Reference: the reference has no selection but binary tournament
 // (src/pga.cu:278-292); linear ranking is the "placeholder" selection enum
@@ -29,187 +33,260 @@ namespace {
 
 using namespace dev;
 
-constexpr uint32_t kRadixBits = 4;
-constexpr uint32_t kRadix = 1u << kRadixBits;  // 16 digits
-constexpr uint32_t kItems = 8;                   // keys per thread
-constexpr uint32_t kTile = kBlock * kItems;      // 2048 keys per workgroup
-constexpr uint32_t kMaxPasses = 8;               // 32-bit keys
-constexpr uint32_t kFlagAgg = 1u << 30, kFlagIncl = 2u << 30, kCountMask = (1u << 30) - 1u;
+constexpr uint32_t kMaxDigitBits = 8;
+constexpr uint32_t kMaxDigits = 1u << kMaxDigitBits;
+constexpr uint32_t kWaveKeys = 1024;                   // per wave: 16 rounds of 64
+constexpr uint32_t kRounds = kWaveKeys / 64;
+constexpr uint32_t kTile = kWaveKeys * (kBlock / 64);  // 4096 keys per workgroup
+constexpr uint32_t kScanBlock = 1024, kScanPer = 16;   // one scan workgroup: 16384 entries
+constexpr uint32_t kScanChunk = kScanBlock * kScanPer;
 
 inline size_t al(size_t x) { return (x + 255) & ~(size_t)255; }
+inline uint64_t tiles_of(uint64_t n) { return (n + kTile - 1) / kTile; }
 
-// workspace: [hist kMaxPasses x 16 | tickets kMaxPasses | pad] [status passes x tiles x 16] [keys A] [vals A]
+// workspace: [counts kMaxDigits x tiles][chunk sums][chunk sums of sums][keys W][vals W]
 struct RadixWs {
-  uint32_t* hist;
-  uint32_t* ticket;
-  uint32_t* status;
+  uint32_t* counts;
+  uint32_t* sums;
+  uint32_t* sums2;
   uint32_t* k;
   uint32_t* v;
-  size_t head_bytes;  // hist + tickets + status: zeroed before every sort
 };
 
 RadixWs radix_ws(void* ws, uint64_t n) {
-  const uint64_t tiles = (n + kTile - 1) / kTile;
+  const uint64_t entries = (uint64_t)kMaxDigits * tiles_of(n);
+  const uint64_t chunks = (entries + kScanChunk - 1) / kScanChunk;
   char* p = (char*)ws;
   RadixWs w;
-  w.hist = (uint32_t*)p;
-  w.ticket = w.hist + kMaxPasses * kRadix;
-  p += al(4ull * (kMaxPasses * kRadix + kMaxPasses));
-  w.status = (uint32_t*)p;
-  p += al(4ull * kMaxPasses * tiles * kRadix);
-  w.head_bytes = (size_t)(p - (char*)ws);
+  w.counts = (uint32_t*)p;
+  p += al(4ull * entries);
+  w.sums = (uint32_t*)p;
+  p += al(4ull * chunks);
+  w.sums2 = (uint32_t*)p;
+  p += al(4ull * ((chunks + kScanChunk - 1) / kScanChunk));
   w.k = (uint32_t*)p;
   p += al(4ull * n);
   w.v = (uint32_t*)p;
   return w;
 }
 
-// keys (and iota values when vals == nullptr) -> staging; every pass's digit
-// histogram.  Key sources: u32 keys, u16 keys (zero-extended), or f32 scores
-// (score_key: ascending score order), selected by which pointer is set.
-__global__ __launch_bounds__(kBlock) void radix_hist_kernel(const uint32_t* k32, const uint16_t* k16, const float* f32,
-                                                            bool invert, const uint32_t* vals, uint64_t n,
-                                                            uint32_t passes, uint32_t* keys_out, uint32_t* vals_out,
-                                                            uint32_t* hist) {
-  __shared__ uint32_t h[kMaxPasses][kRadix];
-  for (uint32_t i = threadIdx.x; i < kMaxPasses * kRadix; i += kBlock) (&h[0][0])[i] = 0;
-  __syncthreads();
-  for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (uint64_t)gridDim.x * kBlock) {
-    uint32_t key = k32 ? k32[i] : (k16 ? (uint32_t)k16[i] : score_key(f32[i]));
-    if (invert) key = ~key;
-    keys_out[i] = key;
-    vals_out[i] = vals ? vals[i] : (uint32_t)i;
-    for (uint32_t p = 0; p < passes; ++p) atomicAdd(&h[p][(key >> (kRadixBits * p)) & (kRadix - 1)], 1u);
-  }
-  __syncthreads();
-  for (uint32_t i = threadIdx.x; i < passes * kRadix; i += kBlock) {
-    const uint32_t c = (&h[0][0])[i];
-    if (c) atomicAdd(&hist[i], c);
-  }
+// A pass's key source: the caller's keys on pass 0 (u32, u16 zero-extended, or
+// f32 scores through score_key; optionally inverted for descending order),
+// the staged u32 keys after it.
+struct KeySrc {
+  const uint32_t* k32;
+  const uint16_t* k16;
+  const float* f32;
+  const uint32_t* vals;  // pass-0 values (nullptr: the key's index)
+  bool invert;
+};
+
+// the source kind is a template parameter: a runtime choice per load would
+// put a branch (and a wait for the load) between the 32 loads of a lane
+enum { SRC_U32 = 0, SRC_U16 = 1, SRC_F32 = 2 };
+template <int SRC>
+__device__ __forceinline__ uint32_t load_key(const KeySrc& s, uint64_t i) {
+  uint32_t key = SRC == SRC_U32 ? s.k32[i] : (SRC == SRC_U16 ? (uint32_t)s.k16[i] : score_key(s.f32[i]));
+  return s.invert ? ~key : key;
 }
 
-__device__ __forceinline__ uint32_t ld_status(const uint32_t* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void st_status(uint32_t* p, uint32_t v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+// the lanes of this wave whose (digit < D) equals mine; lanes without a key
+// (digit == D, past the end) match nobody
+__device__ __forceinline__ uint64_t match_digit(uint32_t dig, bool ok, uint32_t bits) {
+  uint64_t m = __ballot(ok);
+  for (uint32_t b = 0; b < bits; ++b) {  // wave-uniform trip count
+    const bool set = (dig >> b) & 1u;
+    const uint64_t bb = __ballot(set);
+    m &= set ? bb : ~bb;
+  }
+  return ok ? m : 0ull;
 }
 
-// One digit pass: keys/vals in -> out, stable, by digit (key >> shift) & 15.
-__global__ __launch_bounds__(kBlock) void radix_pass_kernel(const uint32_t* __restrict__ kin,
-                                                            const uint32_t* __restrict__ vin,
-                                                            uint32_t* __restrict__ kout, uint32_t* __restrict__ vout,
-                                                            uint64_t n, uint32_t pass, const uint32_t* hist,
-                                                            uint32_t* ticket, uint32_t* status) {
-  __shared__ uint32_t cnt[kRadix][kBlock];   // [digit][thread], then its digit-major exclusive scan
-  __shared__ uint32_t lds_tile, lds_base[kRadix], lds_wsum[kBlock / 64];
+// Per-tile digit counts (order-independent): one LDS atomic per group of
+// lanes sharing a digit (a skewed key distribution would otherwise serialise
+// up to 64 same-address atomics per instruction).
+template <int SRC>
+__global__ __launch_bounds__(kBlock) void radix_count_kernel(KeySrc src, uint64_t n, uint32_t shift, uint32_t bits,
+                                                             uint64_t tiles, uint32_t* __restrict__ counts) {
+  __shared__ uint32_t h[kMaxDigits];
+  const uint32_t D = 1u << bits;
+  for (uint32_t d = threadIdx.x; d < D; d += kBlock) h[d] = 0;
+  __syncthreads();
+  const uint64_t t0 = (uint64_t)blockIdx.x * kTile;
+  const uint64_t below = (1ull << lane_id()) - 1ull;
+  uint32_t dig[kTile / kBlock];
+#pragma unroll
+  for (uint32_t i = 0; i < kTile / kBlock; ++i) {  // all loads first
+    const uint64_t e = t0 + (uint64_t)i * kBlock + threadIdx.x;
+    const uint32_t d = (load_key<SRC>(src, e < n ? e : n - 1) >> shift) & (D - 1);  // unconditional load
+    dig[i] = e < n ? d : D;
+  }
+#pragma unroll
+  for (uint32_t i = 0; i < kTile / kBlock; ++i) {
+    const bool ok = dig[i] < D;
+    const uint64_t peers = match_digit(dig[i], ok, bits);
+    if (ok && (peers & below) == 0ull) atomicAdd(&h[dig[i]], (uint32_t)__popcll(peers));
+  }
+  __syncthreads();
+  for (uint32_t d = threadIdx.x; d < D; d += kBlock) counts[(uint64_t)d * tiles + blockIdx.x] = h[d];
+}
+
+// In-place exclusive scan of chunks of kScanChunk entries (one workgroup per
+// chunk); the chunk totals go to sums (when non-null).
+__global__ __launch_bounds__(kScanBlock) void scan_chunk_kernel(uint32_t* __restrict__ x, uint64_t m,
+                                                                uint32_t* __restrict__ sums) {
+  __shared__ uint32_t wsum[kScanBlock / 64];
   const uint32_t t = threadIdx.x, lane = lane_id(), wid = t >> 6;
-  const uint32_t shift = kRadixBits * pass;
-  if (t == 0) lds_tile = atomicAdd(&ticket[pass], 1u);
-  for (uint32_t d = 0; d < kRadix; ++d) cnt[d][t] = 0;
-  __syncthreads();
-  const uint32_t tile = lds_tile;
-  const uint64_t base = (uint64_t)tile * kTile + (uint64_t)t * kItems;  // blocked: thread t owns 8 consecutive keys
-
-  uint32_t key[kItems], val[kItems], dig[kItems], rnk[kItems];
+  const uint64_t base = (uint64_t)blockIdx.x * kScanChunk + (uint64_t)t * kScanPer;
+  uint32_t v[kScanPer], s = 0;
 #pragma unroll
-  for (uint32_t i = 0; i < kItems; ++i) {
-    const bool ok = base + i < n;
-    key[i] = ok ? kin[base + i] : 0xFFFFFFFFu;
-    val[i] = ok ? vin[base + i] : 0u;
-    dig[i] = ok ? (key[i] >> shift) & (kRadix - 1) : kRadix;  // past the end: no digit
+  for (uint32_t j = 0; j < kScanPer; ++j) {
+    const uint32_t y = x[base + j < m ? base + j : m - 1];  // unconditional load
+    v[j] = base + j < m ? y : 0u;
+    s += v[j];
   }
-#pragma unroll
-  for (uint32_t i = 0; i < kItems; ++i) {  // rank within the thread (column t is private)
-    if (dig[i] < kRadix) {
-      rnk[i] = cnt[dig[i]][t];
-      cnt[dig[i]][t] = rnk[i] + 1;
-    }
-  }
-  __syncthreads();
-  // exclusive scan of cnt in digit-major order: thread t owns the 16
-  // consecutive entries [16 t, 16 t + 16) of the flattened table
-  uint32_t* flat = &cnt[0][0];
-  uint32_t loc[kRadix], s = 0;
-#pragma unroll
-  for (uint32_t j = 0; j < kRadix; ++j) {
-    loc[j] = s;
-    s += flat[kRadix * t + j];
-  }
-  uint32_t incl = s;  // wave inclusive scan of the thread sums
+  uint32_t incl = s;
 #pragma unroll
   for (int o = 1; o < 64; o <<= 1) {
     const uint32_t y = (uint32_t)__shfl_up((int)incl, o, 64);
     if (lane >= (uint32_t)o) incl += y;
   }
-  if (lane == 63) lds_wsum[wid] = incl;
+  if (lane == 63) wsum[wid] = incl;
   __syncthreads();
-  uint32_t off = incl - s;
-  for (uint32_t w = 0; w < wid; ++w) off += lds_wsum[w];
+  uint32_t off = incl - s, tot = 0;
+  for (uint32_t w = 0; w < kScanBlock / 64; ++w) {
+    off += w < wid ? wsum[w] : 0u;
+    tot += wsum[w];
+  }
 #pragma unroll
-  for (uint32_t j = 0; j < kRadix; ++j) flat[kRadix * t + j] = off + loc[j];
+  for (uint32_t j = 0; j < kScanPer; ++j) {
+    if (base + j < m) x[base + j] = off;
+    off += v[j];
+  }
+  if (sums && t == 0) sums[blockIdx.x] = tot;
+}
+
+__global__ __launch_bounds__(kBlock) void scan_add_kernel(uint32_t* __restrict__ x, uint64_t m,
+                                                          const uint32_t* __restrict__ sums) {
+  const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (i < m) x[i] += sums[i / kScanChunk];
+}
+
+// Scatter one tile stably by digit.  Thread layout: wave w owns keys
+// [t0 + w * 1024, t0 + (w + 1) * 1024), round r lane l is key w * 1024 + r * 64 + l.
+template <int SRC, int VAL>  // VAL: 0 = the key's index, 1 = src.vals, 2 = vin
+__global__ __launch_bounds__(kBlock) void radix_scatter_kernel(KeySrc src, const uint32_t* __restrict__ vin, uint64_t n,
+                                                               uint32_t shift, uint32_t bits, uint64_t tiles,
+                                                               const uint32_t* __restrict__ base,
+                                                               uint32_t* __restrict__ kout, uint32_t* __restrict__ vout) {
+  __shared__ uint32_t cnt[kBlock / 64][kMaxDigits];  // per wave: running digit counts, then output bases
+  const uint32_t D = 1u << bits;
+  const uint32_t lane = lane_id(), wid = threadIdx.x >> 6;
+  for (uint32_t d = lane; d < D; d += 64) cnt[wid][d] = 0;
+  const uint64_t w0 = (uint64_t)blockIdx.x * kTile + (uint64_t)wid * kWaveKeys;
+  uint32_t key[kRounds], val[kRounds];
+#pragma unroll
+  for (uint32_t r = 0; r < kRounds; ++r) {  // every load in flight before the ranking
+    const uint64_t e = w0 + r * 64u + lane;
+    const uint64_t ec = e < n ? e : n - 1;  // unconditional loads (a guarded load waits before the next)
+    key[r] = load_key<SRC>(src, ec);
+    val[r] = VAL == 2 ? vin[ec] : (VAL == 1 ? src.vals[ec] : (uint32_t)e);
+  }
+  const uint64_t below = (1ull << lane) - 1ull;
+  uint32_t pos[kRounds];
+#pragma unroll
+  for (uint32_t r = 0; r < kRounds; ++r) {
+    const bool ok = w0 + r * 64u + lane < n;
+    const uint32_t dig = ok ? (key[r] >> shift) & (D - 1) : D;
+    const uint64_t peers = match_digit(dig, ok, bits);
+    const uint32_t rk = (uint32_t)__popcll(peers & below);
+    // every lane of a group reads the counter, then the group's first lane bumps
+    // it: a wave's LDS operations retire in order
+    const uint32_t c = ok ? cnt[wid][dig] : 0u;
+    __builtin_amdgcn_wave_barrier();
+    if (ok && rk == 0u) cnt[wid][dig] = c + (uint32_t)__popcll(peers);
+    __builtin_amdgcn_wave_barrier();
+    pos[r] = ok ? c + rk : 0xFFFFFFFFu;
+  }
   __syncthreads();
-  // cnt[d][u] = keys of the tile with digit < d, plus digit d in threads < u
-  if (wid == 0 && lane < kRadix) {
-    const uint32_t d = lane;
-    const uint32_t start = cnt[d][0];
-    const uint32_t total = (d + 1 < kRadix ? cnt[d + 1][0] : (uint32_t)min((uint64_t)kTile, n - (uint64_t)tile * kTile)) - start;
-    uint32_t* st = status + ((uint64_t)pass * ((n + kTile - 1) / kTile) + tile) * kRadix;
-    st_status(st + d, (tile == 0 ? kFlagIncl : kFlagAgg) | total);
-    uint32_t prefix = 0;
-    if (tile > 0) {
-      // look back: add aggregates until an inclusive prefix is found
-      for (int64_t j = (int64_t)tile - 1; j >= 0; --j) {
-        const uint32_t* sp = st - (uint64_t)(tile - j) * kRadix + d;
-        uint32_t w = ld_status(sp);
-        for (uint32_t spin = 0; (w >> 30) == 0u && spin < (1u << 24); ++spin) {  // bounded: predecessors are resident
-          __builtin_amdgcn_s_sleep(1);
-          w = ld_status(sp);
-        }
-        prefix += w & kCountMask;
-        if ((w >> 30) == 2u) break;
-      }
-      st_status(st + d, kFlagIncl | (prefix + total));
+  // per digit: the tile's global base plus the keys of the earlier waves
+  for (uint32_t d = threadIdx.x; d < D; d += kBlock) {
+    uint32_t o = base[(uint64_t)d * tiles + blockIdx.x];
+#pragma unroll
+    for (uint32_t w = 0; w < kBlock / 64; ++w) {
+      const uint32_t c = cnt[w][d];
+      cnt[w][d] = o;
+      o += c;
     }
-    // digit base over all keys: the histogram's exclusive prefix
-    uint32_t db = 0;
-    for (uint32_t e = 0; e < d; ++e) db += hist[pass * kRadix + e];
-    lds_base[d] = db + prefix - start;  // + cnt[d][u] + rank = output position
   }
   __syncthreads();
 #pragma unroll
-  for (uint32_t i = 0; i < kItems; ++i) {
-    if (dig[i] < kRadix) {
-      const uint32_t pos = lds_base[dig[i]] + cnt[dig[i]][t] + rnk[i];
-      kout[pos] = key[i];
-      vout[pos] = val[i];
+  for (uint32_t r = 0; r < kRounds; ++r) {
+    if (pos[r] != 0xFFFFFFFFu) {
+      const uint32_t p = cnt[wid][(key[r] >> shift) & (D - 1)] + pos[r];
+      if (kout) kout[p] = key[r];
+      vout[p] = val[r];
     }
   }
 }
 
-uint32_t passes_for(uint32_t bits) { return (bits + kRadixBits - 1) / kRadixBits; }
+// exclusive scan of m entries in place (m <= kScanChunk^3)
+void scan_exclusive(uint32_t* x, uint64_t m, const RadixWs& w, hipStream_t s) {
+  const uint64_t chunks = (m + kScanChunk - 1) / kScanChunk;
+  if (chunks <= 1) {
+    hipLaunchKernelGGL(scan_chunk_kernel, 1, kScanBlock, 0, s, x, m, (uint32_t*)nullptr);
+    return;
+  }
+  hipLaunchKernelGGL(scan_chunk_kernel, (uint32_t)chunks, kScanBlock, 0, s, x, m, w.sums);
+  const uint64_t chunks2 = (chunks + kScanChunk - 1) / kScanChunk;
+  if (chunks2 > kScanChunk) throw std::invalid_argument("radix sort: too many keys");
+  if (chunks2 <= 1) {
+    hipLaunchKernelGGL(scan_chunk_kernel, 1, kScanBlock, 0, s, w.sums, chunks, (uint32_t*)nullptr);
+  } else {
+    hipLaunchKernelGGL(scan_chunk_kernel, (uint32_t)chunks2, kScanBlock, 0, s, w.sums, chunks, w.sums2);
+    hipLaunchKernelGGL(scan_chunk_kernel, 1, kScanBlock, 0, s, w.sums2, chunks2, (uint32_t*)nullptr);
+    hipLaunchKernelGGL(scan_add_kernel, (uint32_t)((chunks + kBlock - 1) / kBlock), kBlock, 0, s, w.sums, chunks,
+                       w.sums2);
+  }
+  hipLaunchKernelGGL(scan_add_kernel, (uint32_t)((m + kBlock - 1) / kBlock), kBlock, 0, s, x, m, w.sums);
+}
 
-// one sort: zero the counters, stage + histogram, the digit passes.  The
-// passes ping-pong between the workspace staging (A) and the output (B); the
-// keys are staged where an even number of flips ends in B.
-void radix_run(const uint32_t* k32, const uint16_t* k16, const float* f32, bool invert, const uint32_t* vals,
-               uint64_t n, uint32_t bits, uint32_t* kout, uint32_t* vout, void* ws, hipStream_t s) {
+// one sort: per pass count -> scan -> scatter.  The passes ping-pong between
+// the workspace staging (W) and the output (O); pass i writes O when an even
+// number of passes follows it, so the last one lands in O.
+void radix_run(const KeySrc& src0, uint64_t n, uint32_t bits, uint32_t* kout, uint32_t* vout, void* ws, hipStream_t s) {
   if (n == 0) return;
-  if (n > (uint64_t)kCountMask) throw std::invalid_argument("radix sort: more than 2^30 keys");
-  const uint32_t passes = passes_for(bits < 1 ? 1 : (bits > 32 ? 32 : bits));
+  if (n > 0xFFFFFFFFull) throw std::invalid_argument("radix sort: more than 2^32 - 1 keys");
+  bits = bits < 1 ? 1 : (bits > 32 ? 32 : bits);
+  const uint32_t passes = (bits + kMaxDigitBits - 1) / kMaxDigitBits;
   RadixWs w = radix_ws(ws, n);
-  PGA_HIP_CHECK(hipMemsetAsync(ws, 0, w.head_bytes, s));
-  uint32_t* ck = passes % 2 ? w.k : kout;
-  uint32_t* cv = passes % 2 ? w.v : vout;
-  const uint32_t grid = launch_grid(n, kBlock * 8);
-  hipLaunchKernelGGL(radix_hist_kernel, grid, kBlock, 0, s, k32, k16, f32, invert, vals, n, passes, ck, cv, w.hist);
-  const uint32_t tiles = (uint32_t)((n + kTile - 1) / kTile);
+  const uint64_t tiles = tiles_of(n);
+  if (tiles > 0x7FFFFFFFull) throw std::invalid_argument("radix sort: too many tiles");
+  uint32_t shift = 0;
+  const uint32_t *ck = nullptr, *cv = nullptr;
   for (uint32_t p = 0; p < passes; ++p) {
-    uint32_t* dk = ck == w.k ? kout : w.k;
-    uint32_t* dv = cv == w.v ? vout : w.v;
-    hipLaunchKernelGGL(radix_pass_kernel, tiles, kBlock, 0, s, ck, cv, dk, dv, n, p, w.hist, w.ticket, w.status);
+    // split the bits evenly: the first (bits % passes) passes take one more
+    const uint32_t pb = bits / passes + (p < bits % passes ? 1u : 0u);
+    const bool to_out = (passes - 1 - p) % 2 == 0;
+    uint32_t* dk = to_out ? kout : w.k;
+    uint32_t* dv = to_out ? vout : w.v;
+    KeySrc src = p == 0 ? src0 : KeySrc{ck, nullptr, nullptr, nullptr, false};
+    const int kind = p > 0 ? SRC_U32 : (src.k32 ? SRC_U32 : (src.k16 ? SRC_U16 : SRC_F32));
+    const int vk = p > 0 ? 2 : (src.vals ? 1 : 0);
+    const dim3 g((uint32_t)tiles);
+    if (kind == SRC_U32) hipLaunchKernelGGL(radix_count_kernel<SRC_U32>, g, kBlock, 0, s, src, n, shift, pb, tiles, w.counts);
+    if (kind == SRC_U16) hipLaunchKernelGGL(radix_count_kernel<SRC_U16>, g, kBlock, 0, s, src, n, shift, pb, tiles, w.counts);
+    if (kind == SRC_F32) hipLaunchKernelGGL(radix_count_kernel<SRC_F32>, g, kBlock, 0, s, src, n, shift, pb, tiles, w.counts);
+    scan_exclusive(w.counts, (uint64_t)(1u << pb) * tiles, w, s);
+#define PGA_SCATTER(K, V) hipLaunchKernelGGL((radix_scatter_kernel<K, V>), g, kBlock, 0, s, src, cv, n, shift, pb, tiles, w.counts, dk, dv)
+    if (vk == 2) PGA_SCATTER(SRC_U32, 2);
+    else if (kind == SRC_U32) { if (vk) PGA_SCATTER(SRC_U32, 1); else PGA_SCATTER(SRC_U32, 0); }
+    else if (kind == SRC_U16) { if (vk) PGA_SCATTER(SRC_U16, 1); else PGA_SCATTER(SRC_U16, 0); }
+    else { if (vk) PGA_SCATTER(SRC_F32, 1); else PGA_SCATTER(SRC_F32, 0); }
+#undef PGA_SCATTER
     ck = dk;
     cv = dv;
+    shift += pb;
   }
   PGA_HIP_CHECK(hipGetLastError());
 }
@@ -217,13 +294,14 @@ void radix_run(const uint32_t* k32, const uint16_t* k16, const float* f32, bool 
 }  // namespace
 
 size_t radix_sort_workspace_bytes(uint64_t n) {
-  const uint64_t tiles = (n + kTile - 1) / kTile;
-  return al(4ull * (kMaxPasses * kRadix + kMaxPasses)) + al(4ull * kMaxPasses * tiles * kRadix) + 2 * al(4ull * n);
+  const uint64_t entries = (uint64_t)kMaxDigits * tiles_of(n);
+  const uint64_t chunks = (entries + kScanChunk - 1) / kScanChunk;
+  return al(4ull * entries) + al(4ull * chunks) + al(4ull * ((chunks + kScanChunk - 1) / kScanChunk)) + 2 * al(4ull * n);
 }
 
 void radix_sort_pairs(const uint32_t* keys, const uint32_t* vals, uint64_t n, uint32_t bits, bool descending,
                       uint32_t* keys_out, uint32_t* vals_out, void* ws, hipStream_t s) {
-  radix_run(keys, nullptr, nullptr, descending, vals, n, descending ? 32 : bits, keys_out, vals_out, ws, s);
+  radix_run(KeySrc{keys, nullptr, nullptr, vals, descending}, n, descending ? 32 : bits, keys_out, vals_out, ws, s);
 }
 
 // ---------------- rank order (linear ranking selection) ----------------
@@ -233,7 +311,7 @@ size_t rank_order_workspace_bytes(uint64_t S) { return radix_sort_workspace_byte
 
 void rank_order_launch(const float* scores, uint64_t S, uint32_t* order, void* ws, hipStream_t s) {
   uint32_t* keys_out = (uint32_t*)((char*)ws + radix_sort_workspace_bytes(S));
-  radix_run(nullptr, nullptr, scores, false, nullptr, S, 32, keys_out, order, ws, s);
+  radix_run(KeySrc{nullptr, nullptr, scores, nullptr, false}, S, 32, keys_out, order, ws, s);
 }
 
 // integer objectives: the u16 tournament keys order exactly like the scores;
@@ -243,7 +321,7 @@ void rank_order16_launch(const uint16_t* keys16, uint64_t S, uint32_t key_range,
   uint32_t bits = 1;
   while (bits < 16 && (1u << bits) < key_range) ++bits;
   uint32_t* keys_out = (uint32_t*)((char*)ws + radix_sort_workspace_bytes(S));
-  radix_run(nullptr, keys16, nullptr, false, nullptr, S, bits, keys_out, order, ws, s);
+  radix_run(KeySrc{nullptr, keys16, nullptr, nullptr, false}, S, bits, keys_out, order, ws, s);
 }
 
 }  // namespace pga

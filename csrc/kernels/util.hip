@@ -206,10 +206,29 @@ __device__ __forceinline__ float block_excl_scan(float v, float* lds, float& tot
   return off + v;  // inclusive
 }
 
+// Roulette in three launches: PART (per-block weight sums), FINAL (each block
+// reduces the sums before it for its carry, scans its range into cumfit; the
+// last block publishes the guide scale), GUIDE (bucket -> first individual).
+// The score minimum comes from the generation kernel's fused {min, sum}
+// partials when it stored them (PART reduces them in every block and block 0
+// publishes it), else from score_stats_launch beforehand.
+__device__ __forceinline__ float parts_min(const float* parts, uint32_t n, float* lds) {
+  float mn = INFINITY;
+  for (uint32_t i = threadIdx.x; i < n; i += kBlock) mn = fminf(mn, parts[2 * i]);
+  return block_reduce(mn, lds, FMin());
+}
+
 __global__ __launch_bounds__(kBlock) void prefix_part_kernel(const float* s, uint64_t S, uint64_t per_block,
-                                                             const float* stats, float* block_sums) {
+                                                             const float* parts, uint32_t nparts, float* stats,
+                                                             float* block_sums) {
   __shared__ float lds[kBlock / 64];
-  const float mn = stats[0];
+  float mn;
+  if (parts) {
+    mn = parts_min(parts, nparts, lds);
+    if (blockIdx.x == 0 && threadIdx.x == 0) stats[0] = mn;
+  } else {
+    mn = stats[0];
+  }
   const uint64_t b0 = (uint64_t)blockIdx.x * per_block;
   const uint64_t b1 = b0 + per_block < S ? b0 + per_block : S;
   float sm = 0.f;
@@ -218,71 +237,60 @@ __global__ __launch_bounds__(kBlock) void prefix_part_kernel(const float* s, uin
   if (threadIdx.x == 0) block_sums[blockIdx.x] = sm;
 }
 
-__global__ __launch_bounds__(kBlock) void prefix_blocks_kernel(float* block_sums, uint32_t n, uint64_t S, float* meta) {
-  // exclusive scan of n block sums, single block, sequential tiles
-  __shared__ float lds[kBlock / 64];
-  float carry = 0.f;
-  for (uint32_t t0 = 0; t0 < n; t0 += kBlock) {
-    uint32_t i = t0 + threadIdx.x;
-    float v = i < n ? block_sums[i] : 0.f;
-    float total;
-    float inc = block_excl_scan(v, lds, total);
-    if (i < n) block_sums[i] = carry + inc - v;
-    carry += total;
-    __syncthreads();
-  }
-  // guide-table scale ~ S / total (any positive value is exact, see
-  // roulette_bucket) and a zeroed long-span counter for roulette_guide_launch
-  if (threadIdx.x == 0) {
-    meta[0] = carry > 0.f ? (float)S / carry : 0.f;
-    ((uint32_t*)meta)[1] = 0u;
-  }
-}
-
-// guide[b] = i for every bucket b in (bucket(cumfit[i-1]), bucket(cumfit[i])];
-// spans of 32 buckets or more (one individual holding >= 32/S of the total
-// weight) go to a list that roulette_span_kernel fills cooperatively, so no
-// thread loops over a heavy individual's buckets
-__global__ __launch_bounds__(kBlock) void roulette_guide_kernel(const float* c, uint64_t S, const float* meta,
-                                                                 uint32_t* guide, uint32_t* nspans, uint4* spans) {
-  const float scale = meta[0];
-  const uint32_t B = (uint32_t)S;
-  for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < S; i += (uint64_t)gridDim.x * kBlock) {
-    const uint32_t hi = roulette_bucket(c[i], scale, B);
-    const uint32_t lo = i ? roulette_bucket(c[i - 1], scale, B) + 1u : 0u;
-    if (hi < lo) continue;
-    if (hi - lo < 32u) {
-      for (uint32_t b = lo; b <= hi; ++b) guide[b] = (uint32_t)i;
-    } else {
-      spans[atomicAdd(nspans, 1u)] = make_uint4(lo, hi, (uint32_t)i, 0u);
-    }
-  }
-}
-
-__global__ __launch_bounds__(kBlock) void roulette_span_kernel(const uint32_t* nspans, const uint4* spans,
-                                                                uint32_t* guide) {
-  const uint32_t n = *nspans;
-  for (uint32_t k = blockIdx.x; k < n; k += gridDim.x) {
-    const uint4 sp = spans[k];
-    for (uint32_t b = sp.x + threadIdx.x; b <= sp.y; b += kBlock) guide[b] = sp.z;
-  }
-}
-
 __global__ __launch_bounds__(kBlock) void prefix_final_kernel(const float* s, uint64_t S, uint64_t per_block,
-                                                              const float* stats, const float* block_off,
-                                                              float* cumfit) {
+                                                              const float* stats, const float* block_sums,
+                                                              float* cumfit, float* meta) {
   __shared__ float lds[kBlock / 64];
   const float mn = stats[0];
+  // carry = the sums of the blocks before this one, in a fixed order
+  float pre = 0.f;
+  for (uint32_t j = threadIdx.x; j < blockIdx.x; j += kBlock) pre += block_sums[j];
+  float carry = block_reduce(pre, lds, FAdd());
   const uint64_t b0 = (uint64_t)blockIdx.x * per_block;
   const uint64_t b1 = b0 + per_block < S ? b0 + per_block : S;
-  float carry = block_off[blockIdx.x];
   for (uint64_t t0 = b0; t0 < b1; t0 += kBlock) {
     uint64_t i = t0 + threadIdx.x;
     float v = i < b1 ? fmaxf(s[i] - mn, 0.f) : 0.f;
     float total;
     float inc = block_excl_scan(v, lds, total);
     if (i < b1) cumfit[i] = carry + inc;
+    if (i == S - 1) meta[0] = carry + inc > 0.f ? (float)S / (carry + inc) : 0.f;  // guide scale (roulette_bucket)
     carry += total;
+    __syncthreads();
+  }
+}
+
+// guide[b] = i for every bucket b in (bucket(cumfit[i-1]), bucket(cumfit[i])].
+// Spans of 32 buckets or more (one individual holding >= 32/S of the total
+// weight) are queued in LDS and filled by the whole block, so no thread loops
+// over a heavy individual's buckets.
+__global__ __launch_bounds__(kBlock) void roulette_guide_kernel(const float* c, uint64_t S, const float* meta,
+                                                                 uint32_t* guide) {
+  __shared__ uint4 spans[kBlock];
+  __shared__ uint32_t nsp;
+  const float scale = meta[0];
+  const uint32_t B = (uint32_t)S;
+  for (uint64_t t0 = (uint64_t)blockIdx.x * kBlock; t0 < S; t0 += (uint64_t)gridDim.x * kBlock) {  // block-uniform
+    if (threadIdx.x == 0) nsp = 0;
+    __syncthreads();
+    const uint64_t i = t0 + threadIdx.x;
+    if (i < S) {
+      const uint32_t hi = roulette_bucket(c[i], scale, B);
+      const uint32_t lo = i ? roulette_bucket(c[i - 1], scale, B) + 1u : 0u;
+      if (hi >= lo) {
+        if (hi - lo < 32u) {
+          for (uint32_t b = lo; b <= hi; ++b) guide[b] = (uint32_t)i;
+        } else {
+          spans[atomicAdd(&nsp, 1u)] = make_uint4(lo, hi, (uint32_t)i, 0u);
+        }
+      }
+    }
+    __syncthreads();
+    const uint32_t n = nsp;
+    for (uint32_t k = 0; k < n; ++k) {
+      const uint4 sp = spans[k];
+      for (uint32_t b = sp.x + threadIdx.x; b <= sp.y; b += kBlock) guide[b] = sp.z;
+    }
     __syncthreads();
   }
 }
@@ -1023,30 +1031,28 @@ void score_stats_launch(const float* scores, uint64_t S, float* stats, hipStream
 }
 
 size_t roulette_workspace_floats(uint64_t S) {
-  // stats | stats partials | block sums | scale, span count, pad | spans (uint4)
-  return kRoulScale + 4 + 4 * ((S + 1) / 32 + 2);
+  // stats | stats partials | block sums | scale, pad
+  (void)S;
+  return kRoulScale + 4;
 }
 
-void roulette_prefix_launch(const float* scores, uint64_t S, float* cumfit, float* ws, hipStream_t s) {
-  // ws layout: [0..4) stats, [4 .. 4+3*1024) stats partials, then block sums
-  score_stats_launch(scores, S, ws, s);
+void roulette_prefix_launch(const float* scores, uint64_t S, const float* parts, uint32_t nparts, float* cumfit,
+                            float* ws, hipStream_t s) {
+  // ws layout: [0..4) stats, [4 .. 4+3*1024) stats partials, then block sums, then [kRoulScale] the guide scale
+  if (!parts) score_stats_launch(scores, S, ws, s);
   uint32_t grid = launch_grid(S, kBlock * 4);
   if (grid > 1024) grid = 1024;
   const uint64_t per_block = (S + grid - 1) / grid;
   float* block_sums = ws + 4 + 3 * 1024;
-  hipLaunchKernelGGL(prefix_part_kernel, grid, kBlock, 0, s, scores, S, per_block, ws, block_sums);
-  hipLaunchKernelGGL(prefix_blocks_kernel, 1, kBlock, 0, s, block_sums, grid, S, ws + kRoulScale);
-  hipLaunchKernelGGL(prefix_final_kernel, grid, kBlock, 0, s, scores, S, per_block, ws, block_sums, cumfit);
+  hipLaunchKernelGGL(prefix_part_kernel, grid, kBlock, 0, s, scores, S, per_block, parts, nparts, ws, block_sums);
+  hipLaunchKernelGGL(prefix_final_kernel, grid, kBlock, 0, s, scores, S, per_block, ws, block_sums, cumfit,
+                     ws + kRoulScale);
   PGA_HIP_CHECK(hipGetLastError());
 }
 
 void roulette_guide_launch(const float* cumfit, uint64_t S, uint32_t* guide, float* ws, hipStream_t s) {
   const uint32_t grid = launch_grid(S, kBlock);
-  uint32_t* nspans = (uint32_t*)(ws + kRoulScale) + 1;
-  uint4* spans = (uint4*)(ws + kRoulScale + 4);
-  hipLaunchKernelGGL(roulette_guide_kernel, grid, kBlock, 0, s, cumfit, S, (const float*)(ws + kRoulScale), guide,
-                     nspans, spans);
-  hipLaunchKernelGGL(roulette_span_kernel, 64, kBlock, 0, s, (const uint32_t*)nspans, (const uint4*)spans, guide);
+  hipLaunchKernelGGL(roulette_guide_kernel, grid, kBlock, 0, s, cumfit, S, (const float*)(ws + kRoulScale), guide);
   PGA_HIP_CHECK(hipGetLastError());
 }
 

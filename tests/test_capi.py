@@ -272,7 +272,10 @@ def test_stats_history(lib):
 
 
 def run_ex(args, inp=None, timeout=300):
-    r = subprocess.run(args, input=inp, capture_output=True, text=True, timeout=timeout)
+    # a fixed seed: pga_init otherwise seeds from time(NULL) like the reference
+    env = dict(os.environ)
+    env.setdefault("PGA_SEED", "20261017")
+    r = subprocess.run(args, input=inp, capture_output=True, text=True, timeout=timeout, env=env)
     return r.returncode, r.stdout + r.stderr
 
 
@@ -292,7 +295,7 @@ def test_example_e1_callbacks_4m():
 
 @pytest.mark.gpu
 def test_example_e2_knapsack():
-    rc, out = run_ex([os.path.join(EX, "e2_knapsack"), "10"])
+    rc, out = run_ex([os.path.join(EX, "e2_knapsack"), "40"])
     assert rc == 0, out
     assert "0 0 1 1 0 0" in out
 
