@@ -96,6 +96,9 @@ struct pga_solver {
   uint32_t mig_k = 0;
   // one row of device staging for the cross-rank best genome (broadcast)
   void* best_row = nullptr;
+  // pga_run_islands: same-shape islands as one batched launch per generation
+  bool batch_islands = true;
+  uint64_t batched_gens = 0;
 };
 
 namespace {
@@ -880,6 +883,15 @@ unsigned run_islands_until(const std::vector<pga_t*>& solvers, unsigned n, unsig
     for (pga_t* p : solvers) {
       use_device(p);
       const bool gpu = p->device >= 0;
+      if (gpu && p->pops.size() > 1 && p->batch_islands) {
+        // same-shape islands: one launch per generation for all of them
+        std::vector<pga::Island*> v;
+        for (population_t* pop : p->pops) v.push_back(pop->isl.get());
+        if (pga::Island::run_batched(v, k, p->stream)) {
+          p->batched_gens += k;
+          continue;
+        }
+      }
       if (gpu) fork_islands(p);
       for (population_t* pop : p->pops) pop->isl->run(k);
       if (gpu) join_islands(p);
@@ -917,6 +929,14 @@ unsigned run_islands_until(const std::vector<pga_t*>& solvers, unsigned n, unsig
   return g;
 }
 }  // namespace
+
+int pga_set_batch_islands(pga_t* p, int on) {
+  if (!p) return -1;
+  p->batch_islands = on != 0;
+  return 0;
+}
+
+unsigned long long pga_batched_generations(const pga_t* p) { return p ? p->batched_gens : 0ull; }
 
 void pga_run_islands(pga_t* p, unsigned n, unsigned m, float pct) {
   if (!p || p->pops.empty()) return;

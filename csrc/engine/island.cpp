@@ -423,6 +423,11 @@ void Island::run_plain(uint32_t n) {
     TraceRange tg("pga.generation", 2);
     prepare_generation();
     GenArgs a = make_args(MODE_GEN);
+    if (jit_ && fused_jit_generation(a)) {  // the objective linked into the generation kernel
+      swap();
+      if (hist_on_ && !hist_manual_ && !capturing_) append_history();
+      continue;
+    }
     n_best_[cur_ ^ 1] = launch(MODE_GEN, a, (unsigned long long*)best_[cur_ ^ 1].ptr);
     stats_ok_[cur_ ^ 1] = a.stats_parts != nullptr;
     qk_valid_[cur_ ^ 1] = a.qk != nullptr && !jit_;  // every REAL GEN kernel writes the keys it is given
@@ -434,6 +439,45 @@ void Island::run_plain(uint32_t n) {
     swap();
     if (hist_on_ && !hist_manual_ && !capturing_) append_history();
   }
+}
+
+bool Island::run_batched(const std::vector<Island*>& isls, uint32_t n, hipStream_t s) {
+  const size_t N = isls.size();
+  if (N < 2 || N > binary_max_batch()) return false;
+  const Island* i0 = isls[0];
+  for (const Island* i : isls) {
+    if (!i || !i->on_gpu() || i->device_ != i0->device_ || i->cfg_.encoding != ENC_BINARY || i->jit_ ||
+        i->user_fn_ || i->user_xo_fn_ || i->user_mut_fn_ || i->hist_on_ || i->cfg_.S != i0->cfg_.S || i->cfg_.L != i0->cfg_.L)
+      return false;
+    for (const Island* j : isls)
+      if (j != i && j->rows_[0].ptr == i->rows_[0].ptr) return false;  // the same island twice
+  }
+  TraceRange tr("pga.run_batched");
+  std::vector<GenArgs> args(N);
+  std::vector<unsigned long long*> parts(N);
+  for (uint32_t g = 0; g < n; ++g) {
+    for (size_t k = 0; k < N; ++k) {
+      Island& I = *isls[k];
+      I.stream = s;
+      I.prepare_generation();
+      args[k] = I.make_args(MODE_GEN);
+      parts[k] = (unsigned long long*)I.best_[I.cur_ ^ 1].ptr;
+    }
+    const uint32_t grid = binary_launch_batch(args.data(), parts.data(), (uint32_t)N, s);
+    if (grid == 0) {
+      if (g == 0) return false;  // not eligible (decided on the first generation's arguments)
+      throw std::logic_error("batched islands stopped qualifying mid-run");
+    }
+    for (size_t k = 0; k < N; ++k) {
+      Island& I = *isls[k];
+      const int nx = I.cur_ ^ 1;
+      I.n_best_[nx] = grid;
+      I.stats_ok_[nx] = args[k].stats_parts != nullptr;
+      I.qk_valid_[nx] = false;
+      I.swap();
+    }
+  }
+  return true;
 }
 
 uint32_t Island::run_until(uint32_t n, float target, uint32_t check_every) {
@@ -711,7 +755,28 @@ void Island::set_jit_objective(std::shared_ptr<JitKernel> k) {
     k->function(device_);  // load the module now: errors surface here, not mid-run
   }
   jit_ = std::move(k);
+  jit_fused_off_ = false;
   invalidate();
+}
+
+bool Island::fused_jit_generation(GenArgs& a) {
+  if (!on_gpu() || cfg_.encoding != ENC_BINARY || jit_fused_off_) return false;
+  uint32_t gs = 0;
+  bool full = false, dense = false;
+  if (!binary_tp_plan(a, gs, full, dense)) return false;
+  hipFunction_t f = jit_->gen_function(device_, gs, full, dense, cfg_.L);
+  if (!f) {
+    jit_fused_off_ = true;  // fall back to generation + evaluation pass (jit_->fused_error() says why)
+    return false;
+  }
+  TraceRange tr("pga.jit_generation", 2);
+  const int nx = cur_ ^ 1;
+  a.stats_parts = (float*)stats_parts_[nx].ptr;  // the fused kernel stores {min, sum} partials like the built-ins
+  n_best_[nx] = jit_->gen_launch(f, &a, sizeof(a), cfg_.S, (unsigned long long*)best_[nx].ptr, kMaxGrid, stream);
+  stats_ok_[nx] = a.stats_parts != nullptr;
+  qk_valid_[nx] = false;
+  ++jit_fused_gens_;
+  return true;
 }
 
 uint32_t Island::jit_eval(const void* rows, float* scores, uint64_t n, unsigned long long* parts) {

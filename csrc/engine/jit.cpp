@@ -2,12 +2,22 @@
 #include "pga/jit.hpp"
 
 #include <dlfcn.h>
+#include <spawn.h>
+#include <sys/wait.h>
+#include <unistd.h>
 
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <functional>
 #include <mutex>
 #include <stdexcept>
 
 #include "pga/core.hpp"
 #include "pga/ops.hpp"
+
+extern char** environ;
 
 namespace pga {
 
@@ -138,6 +148,7 @@ std::shared_ptr<JitKernel> jit_compile(int encoding, const std::string& source, 
   k->encoding = encoding;
   k->name = name;
   k->source = jit_kernel_source(encoding, source, name);
+  k->user_source = source;
   rtc_program prog = nullptr;
   if (r.create(&prog, k->source.c_str(), "pga_jit_objective.hip", 0, nullptr, nullptr) != 0)
     throw std::runtime_error("hiprtcCreateProgram failed");
@@ -170,6 +181,8 @@ std::shared_ptr<JitKernel> jit_compile(int encoding, const std::string& source, 
 JitKernel::~JitKernel() {
   for (hipModule_t m : modules_)
     if (m) (void)hipModuleUnload(m);
+  for (const GenVariant& v : gen_)
+    if (v.mod) (void)hipModuleUnload(v.mod);
 }
 
 hipFunction_t JitKernel::function(int device) {
@@ -202,6 +215,155 @@ uint32_t JitKernel::eval(int device, const void* rows, uint32_t row_words, uint6
   void* args[] = {&r, &rw, &n, &l, &data, &scores, &parts, &tile};
   PGA_HIP_CHECK(hipModuleLaunchKernel(f, (unsigned)blocks, 1, 1, 256, 1, 1, (unsigned)lds, s, args, nullptr));
   return (uint32_t)blocks;
+}
+
+// ------------------------------------------------------------ fused generation
+std::string jit_bitcode_dir() {
+  if (const char* e = std::getenv("PGA_JIT_DIR")) return e;
+  Dl_info info;
+  if (dladdr((const void*)&jit_compile, &info) && info.dli_fname) {
+    std::string so = info.dli_fname;
+    const size_t k = so.find_last_of('/');
+    const std::string dir = k == std::string::npos ? "." : so.substr(0, k);
+    for (const std::string& c : {dir + "/jit", dir + "/../build/jit"}) {
+      FILE* f = std::fopen((c + "/gen_8_1_0.bc").c_str(), "rb");
+      if (f) {
+        std::fclose(f);
+        return c;
+      }
+    }
+  }
+  return "build/jit";
+}
+
+namespace {
+// the jitgen.hip symbol of binary_gen_tp<GS, kObjJit = 1001, FULL, DENSE>
+std::string gen_symbol(uint32_t gs, bool full, bool dense) {
+  return "_ZN3pga6jitgen13binary_gen_tpILi" + std::to_string(gs) + "ELi1001ELb" + (full ? "1" : "0") + "ELb" +
+         (dense ? "1" : "0") + "EEEvNS_7GenArgsEPy";
+}
+
+std::vector<char> read_file(const std::string& path) {
+  std::vector<char> v;
+  FILE* f = std::fopen(path.c_str(), "rb");
+  if (!f) return v;
+  char buf[1 << 16];
+  size_t n;
+  while ((n = std::fread(buf, 1, sizeof(buf), f)) > 0) v.insert(v.end(), buf, buf + n);
+  std::fclose(f);
+  return v;
+}
+
+// Runs `cmd` (a /bin/sh command line) as a child process (posix_spawn, never
+// an exec of this process), output appended to `log`; returns its exit status.
+int spawn_shell(const std::string& cmd, const std::string& log) {
+  const std::string full = cmd + " >> '" + log + "' 2>&1";
+  const char* argv[] = {"/bin/sh", "-c", full.c_str(), nullptr};
+  pid_t pid = 0;
+  if (posix_spawn(&pid, "/bin/sh", nullptr, nullptr, (char* const*)argv, environ) != 0) return -1;
+  int st = 0;
+  if (waitpid(pid, &st, 0) != pid) return -1;
+  return WIFEXITED(st) ? WEXITSTATUS(st) : -1;
+}
+
+std::string jit_cache_dir() {
+  if (const char* e = std::getenv("PGA_JIT_CACHE")) return e;
+  return "/tmp/pga_jit_cache_" + std::to_string((unsigned)getuid());
+}
+
+std::string read_text(const std::string& path) {
+  std::vector<char> v = read_file(path);
+  return std::string(v.begin(), v.end());
+}
+}  // namespace
+
+// The user objective is compiled to LLVM bitcode and linked with the kernel's
+// bitcode by the ROCm toolchain this library was built with (hipcc + clang/lld
+// LTO), in a child process, cached on disk by content.  Not hiprtcLink*: in a
+// process where another HIP runtime is already loaded (PyTorch bundles its own
+// HIP / COMGR) hipRTC links with that older LLVM, which cannot read bitcode
+// from this build's compiler.
+hipFunction_t JitKernel::gen_function(int device, uint32_t gs, bool full, bool dense, uint32_t L) {
+  if (encoding != ENC_BINARY || fused_failed_ || device < 0) return nullptr;
+  const uint64_t key = ((uint64_t)L << 8) | (gs * 4u + (full ? 2u : 0u) + (dense ? 1u : 0u));
+  for (const GenVariant& v : gen_)
+    if (v.device == device && v.key == key) return v.fn;
+  auto fail = [&](const std::string& why) -> hipFunction_t {
+    fused_failed_ = true;
+    fused_error_ = why;
+    return nullptr;
+  };
+  const std::string variant = std::to_string(gs) + "_" + (full ? "1" : "0") + "_" + (dense ? "1" : "0");
+  const std::string kbc = jit_bitcode_dir() + "/gen_" + variant + ".bc";
+  if (read_file(kbc).empty()) return fail("no generation-kernel bitcode at " + kbc + " (tools/build.py builds it)");
+  const char* rp = std::getenv("ROCM_PATH");
+  const std::string rocm = rp && *rp ? rp : "/opt/rocm";
+  // the user's source + the external-linkage entry the kernel bitcode calls:
+  // the row arrives as a global pointer (global loads, not flat) and the
+  // genome length as a constant, so fixed-trip loops over the row unroll with
+  // every load in flight (the length is part of the cache key)
+  const std::string src = "#include <hip/hip_runtime.h>\n#line 1 \"user_objective\"\n" + user_source + "\n" +
+                          "extern \"C\" __device__ float pga_user_objective(__attribute__((address_space(1))) "
+                          "const unsigned int* w, unsigned int, const float* d) { return " + name +
+                          "((const unsigned int*)w, " + std::to_string(L) + "u, d); }\n";
+  const std::string h = std::to_string(std::hash<std::string>{}(src + "|" + read_text(kbc)));
+  const std::string dir = jit_cache_dir();
+  const std::string base = dir + "/obj_" + h;
+  const std::string co = base + "_" + variant + ".co", log = base + "_" + variant + ".log";
+  std::vector<char> image = read_file(co);
+  if (image.empty()) {
+    if (spawn_shell("mkdir -p '" + dir + "'", "/dev/null") != 0) return fail("cannot create " + dir);
+    const std::string tmp = co + ".tmp" + std::to_string((unsigned)getpid());
+    FILE* f = std::fopen((base + ".hip").c_str(), "wb");
+    if (!f) return fail("cannot write " + base + ".hip");
+    std::fwrite(src.data(), 1, src.size(), f);
+    std::fclose(f);
+    // unoptimised bitcode on both sides: the link optimises the whole kernel
+    // once, with the objective inlined (optimising twice costs registers)
+    const std::string cc = "'" + rocm + "/bin/hipcc' -x hip --offload-arch=gfx950 -O3 -Xclang -disable-llvm-passes "
+                           "-std=c++17 -ffp-contract=fast -fgpu-rdc --cuda-device-only -emit-llvm -c '" + base +
+                           ".hip' -o '" + base + ".bc'";
+    const std::string ld = "'" + rocm + "/lib/llvm/bin/clang' --target=amdgcn-amd-amdhsa -mcpu=gfx950 -O3 '" + kbc +
+                           "' '" + base + ".bc' -o '" + tmp + "' && mv '" + tmp + "' '" + co + "'";
+    if (spawn_shell(cc, log) != 0) return fail("compiling the objective to bitcode failed:\n" + read_text(log));
+    if (spawn_shell(ld, log) != 0) return fail("linking the fused generation kernel failed:\n" + read_text(log));
+    image = read_file(co);
+    if (image.empty()) return fail("the linker produced no code object: " + co);
+  }
+  PGA_HIP_CHECK(hipSetDevice(device));
+  GenVariant v{device, key, nullptr, nullptr, 1, std::make_shared<std::vector<char>>(std::move(image))};
+  hipError_t e = hipModuleLoadData(&v.mod, v.image->data());
+  if (e == hipSuccess) e = hipModuleGetFunction(&v.fn, v.mod, gen_symbol(gs, full, dense).c_str());
+  if (e != hipSuccess) {
+    if (v.mod) (void)hipModuleUnload(v.mod);
+    return fail(std::string("loading the fused generation kernel: ") + hipGetErrorString(e));
+  }
+  int occ = 0;
+  if (hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&occ, v.fn, 256, 0) != hipSuccess || occ <= 0) occ = 1;
+  v.occ = (uint32_t)occ;
+  gen_.push_back(v);
+  return v.fn;
+}
+
+uint32_t JitKernel::gen_launch(hipFunction_t f, const void* args, size_t args_bytes, uint64_t S,
+                               unsigned long long* parts, uint32_t max_grid, hipStream_t s) {
+  uint32_t occ = 1;
+  for (const GenVariant& v : gen_)
+    if (v.fn == f) occ = v.occ;
+  // the same grid launch_grid_occ gives the built-in kernels: resident blocks x CUs
+  uint64_t need = (S + 255) / 256, cap = (uint64_t)device_cu_count() * occ;
+  if (cap > max_grid) cap = max_grid;
+  const uint32_t grid = (uint32_t)std::max<uint64_t>(1, std::min(need, cap));
+  // kernel arguments as one packed buffer: (GenArgs a, unsigned long long* parts)
+  std::vector<char> buf(args_bytes + 16);
+  std::memcpy(buf.data(), args, args_bytes);
+  size_t off = (args_bytes + 7) & ~(size_t)7;
+  std::memcpy(buf.data() + off, &parts, sizeof(parts));
+  size_t total = off + sizeof(parts);
+  void* cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, buf.data(), HIP_LAUNCH_PARAM_BUFFER_SIZE, &total,
+                 HIP_LAUNCH_PARAM_END};
+  PGA_HIP_CHECK(hipModuleLaunchKernel(f, grid, 1, 1, 256, 1, 1, 0, s, nullptr, cfg));
+  return grid;
 }
 
 }  // namespace pga

@@ -86,11 +86,20 @@ class Island {
   // Its data pointer is objective data slot 0.  nullptr detaches.
   void set_jit_objective(std::shared_ptr<JitKernel> k);
   bool has_jit() const { return (bool)jit_; }
+  // generations whose JIT objective ran inside the generation kernel (fused),
+  // and why fusion is off when it is ("" while it works or was never tried)
+  uint64_t jit_fused_generations() const { return jit_fused_gens_; }
+  std::string jit_fused_error() const { return jit_ ? jit_->fused_error() : std::string(); }
 
   // ---- stages ----
   void initialize();          // random population + evaluation (generation 0)
   void evaluate();            // scores(cur) <- objective(rows(cur))
   void run(uint32_t n);       // n fused generations
+  // n generations of several islands of one device as ONE launch per
+  // generation (binary_launch_batch: BINARY, same shape / operators, built-in
+  // integer objective); every island's stream is set to s.  Returns false
+  // (nothing run) when the islands do not qualify: run them one by one.
+  static bool run_batched(const std::vector<Island*>& isls, uint32_t n, hipStream_t s);
   // up to n generations, stopping once the best score reaches `target`; the
   // best is read (one stream sync) every `check_every` generations (0: 10).
   // Returns the generations run.
@@ -234,6 +243,9 @@ class Island {
   std::shared_ptr<JitKernel> jit_;
   // JIT evaluation of `n` rows at `rows` -> scores, block bests -> parts; returns the grid
   uint32_t jit_eval(const void* rows, float* scores, uint64_t n, unsigned long long* parts);
+  bool fused_jit_generation(GenArgs& a);
+  bool jit_fused_off_ = false;
+  uint64_t jit_fused_gens_ = 0;
   u32x4 last_mask_{0, 0, 0, 0};
 
   // graph replay state

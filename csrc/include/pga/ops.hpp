@@ -50,6 +50,16 @@ bool force_generic_kernels();
 // ---- encodings: one launch per call, returns the grid used (= number of
 // valid entries written to best_parts, when the mode evaluates) ----
 uint32_t binary_launch(int mode, const GenArgs& a, unsigned long long* best_parts, hipStream_t s);
+// whether a MODE_GEN launch of these arguments takes the hot two-phase kernel
+// (binary_gen_tp) and which variant: group size, full groups, dense mutation.
+// For f32-score objectives (the fused JIT generation kernel, jit.hpp).
+bool binary_tp_plan(const GenArgs& a, uint32_t& gs, bool& full, bool& dense);
+// batched islands (binary_batch.hip): one MODE_GEN launch of up to
+// binary_max_batch() same-shape islands (args[i], best partials parts[i]);
+// returns each island's grid (its best-partials count), 0 when the islands do
+// not qualify (nothing launched: run them one by one)
+uint32_t binary_max_batch();
+uint32_t binary_launch_batch(const GenArgs* args, unsigned long long* const* parts, uint32_t n, hipStream_t s);
 // Knapsack digit table for the matrix-core evaluation (binary.hip): false
 // (table empty) when the instance does not qualify -- non-integer values or
 // weights, sums of magnitudes >= 2^24, fewer than 4 lanes per individual, or

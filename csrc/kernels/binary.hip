@@ -29,751 +29,12 @@
 #include "pga/device.hpp"
 #include "pga/ops.hpp"
 #include "pga/tp.hpp"
+#include "pga/binary_dev.hpp"
 
 namespace pga {
 namespace {
 
 using namespace dev;
-
-// per-lane objective accumulator over the chunks a lane owns
-template <int OBJ>
-struct BinObj {
-  uint32_t u = 0;                 // ONEMAX / TRAP counts
-  uint32_t first0 = 0xFFFFFFFFu;  // LEADING_ONES: first zero bit position
-  float v = 0.f, w = 0.f;         // KNAPSACK
-
-  __device__ __forceinline__ void add(const GenArgs& a, uint4 x, uint32_t c) {
-    const uint32_t wd[4] = {x.x, x.y, x.z, x.w};
-    if (OBJ == OBJ_ONEMAX) {
-      u += __popc(x.x) + __popc(x.y) + __popc(x.z) + __popc(x.w);
-    } else if (OBJ == OBJ_KNAPSACK) {
-      const float* val = a.obj_data;
-      const float* wt = a.obj_data + a.L;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        uint32_t bits = wd[j];
-        const uint32_t base = c * 128u + 32u * j;
-        while (bits) {
-          uint32_t b = __ffs(bits) - 1;
-          bits &= bits - 1;
-          v += val[base + b];
-          w += wt[base + b];
-        }
-      }
-    } else if (OBJ == OBJ_TRAP) {
-      const uint32_t k = (uint32_t)a.obj_i;
-      const uint32_t km = k >= 32 ? 0xFFFFFFFFu : ((1u << k) - 1u);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const uint32_t base = c * 128u + 32u * j;
-        for (uint32_t i = 0; i < 32u; i += k) {
-          if (base + i + k > a.L) break;
-          uint32_t ones = __popc((wd[j] >> i) & km);
-          u += ones == k ? k : (k - 1 - ones);
-        }
-      }
-    } else if (OBJ == OBJ_LEADING_ONES) {
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        uint32_t inv = ~wd[j];
-        if (inv != 0u) {
-          uint32_t p = c * 128u + 32u * j + (__ffs(inv) - 1);
-          first0 = p < first0 ? p : first0;
-          break;
-        }
-      }
-    }
-  }
-
-  template <int GS>
-  __device__ __forceinline__ float finish(const GenArgs& a) {
-    if (OBJ == OBJ_ONEMAX || OBJ == OBJ_TRAP) return (float)group_sum_u<GS>(u);
-    if (OBJ == OBJ_KNAPSACK) {
-      float vv = group_sum<GS>(v), ww = group_sum<GS>(w);
-      return ww <= a.obj_f0 ? vv : a.obj_f0 - ww;
-    }
-    if (OBJ == OBJ_LEADING_ONES) {
-      uint32_t m = group_min_u<GS>(first0);
-      return (float)(m < a.L ? m : a.L);
-    }
-    return 0.f;
-  }
-};
-
-__device__ __forceinline__ uint4 u4(u32x4 v) { return make_uint4(v.x, v.y, v.z, v.w); }
-__device__ __forceinline__ uint4 and4(uint4 a, uint4 b) { return make_uint4(a.x & b.x, a.y & b.y, a.z & b.z, a.w & b.w); }
-__device__ __forceinline__ uint4 xor4(uint4 a, uint4 b) { return make_uint4(a.x ^ b.x, a.y ^ b.y, a.z ^ b.z, a.w ^ b.w); }
-__device__ __forceinline__ uint4 mix4(uint4 a, uint4 b, uint4 m) {  // a where m, else b
-  return make_uint4((a.x & m.x) | (b.x & ~m.x), (a.y & m.y) | (b.y & ~m.y), (a.z & m.z) | (b.z & ~m.z),
-                    (a.w & m.w) | (b.w & ~m.w));
-}
-__device__ __forceinline__ uint4 range_keep_a(uint32_t c, uint32_t lo, uint32_t hi) {  // 1 = bit from A
-  const uint32_t b0 = c * 128u;
-  return make_uint4(~range_mask32(b0, lo, hi), ~range_mask32(b0 + 32, lo, hi), ~range_mask32(b0 + 64, lo, hi),
-                    ~range_mask32(b0 + 96, lo, hi));
-}
-__device__ __forceinline__ uint4 bit4(uint32_t b) {  // one bit of a 128-bit chunk
-  const uint32_t m = 1u << (b & 31u), j = b >> 5;
-  return make_uint4(j == 0 ? m : 0u, j == 1 ? m : 0u, j == 2 ? m : 0u, j == 3 ? m : 0u);
-}
-__device__ __forceinline__ uint32_t chunk_len(uint32_t L, uint32_t c) {
-  const uint32_t b = c * 128u;
-  return L - b >= 128u ? 128u : L - b;
-}
-
-// ---------------------------------------------------------------------------
-// 0/1 knapsack on the matrix cores (the hot kernel's evaluation when the
-// instance is integer-exact, see build_knap_table).
-//
-// score needs V = bits . values and W = bits . weights per child.  A wave's
-// step holds its NG children as 64 16-byte chunks (lane = g*GS + q), staged
-// in its LDS scratch as 16 "virtual rows" of 512 bits: virtual row m = the
-// chunks of lanes 4m..4m+3 = part r = m % R (R = GS/4) of child m / R.  One
-// v_mfma_i32_16x16x64_i8 per 64-bit slice s (8 slices):
-//   A[m][k] = bit k of virtual row m (expanded to int8 0/1),
-//   B[k][c] = digit d of quantity qty (values | weights) of the gene bit k of
-//             part r stands for, column c = (2r + qty) * D + d,
-// with balanced base-256 digits in [-128, 127] (D <= 4), so C[m][c] is an
-// exact partial dot product in i32 and only the columns of row m's own part
-// are used:  V = sum_r sum_d C[gR + r][2rD + d] 256^d  (W: qty = 1).
-// The element order inside a slice (element j of lane group h <-> bit 16h + j
-// of the slice's 64) is the same for A and B, so the hardware's internal k
-// permutation cannot matter; the integer result equals the CPU backend's
-// float sum bit for bit (every partial sum is an integer below 2^24).
-// Reference: test2/test.cu:28-36 (the knapsack objective); SURVEY.md C10.
-// ---------------------------------------------------------------------------
-typedef int v4i __attribute__((ext_vector_type(4)));
-constexpr int kObjKnapMfma = 1000;  // launcher-only objective id: OBJ_KNAPSACK via knap_mfma
-constexpr uint32_t kKnapSlices = 8;  // 512-bit virtual row / 64-bit MFMA k-step
-constexpr uint32_t kKnapMaxCols = 16;
-
-__device__ __forceinline__ v4i expand16(uint32_t h) {  // 16 bits -> 16 int8 {0,1}
-  v4i r;
-  r[0] = (int)(__umul24(h & 0xFu, 0x00204081u) & 0x01010101u);
-  r[1] = (int)(__umul24((h >> 4) & 0xFu, 0x00204081u) & 0x01010101u);
-  r[2] = (int)(__umul24((h >> 8) & 0xFu, 0x00204081u) & 0x01010101u);
-  r[3] = (int)(__umul24((h >> 12) & 0xFu, 0x00204081u) & 0x01010101u);
-  return r;
-}
-
-// chunk slot of lane 4m + h in the wave scratch: virtual row m, lane group h,
-// XOR-swizzled so that both the lane-order store and the (h, n) fragment
-// read touch 8 distinct 16-byte bank groups per 8 lanes
-__device__ __forceinline__ uint32_t knap_slot(uint32_t m, uint32_t h) { return 4u * m + (h ^ ((m >> 1) & 3u)); }
-constexpr uint32_t kKnapCStride = 20;  // ints per C column in the scratch (padded against bank conflicts)
-constexpr uint32_t kKnapScratch = 16 * kKnapCStride / 4;  // uint4 per wave (>= 64 chunk slots)
-
-// every lane of the wave calls this with its chunk `v` (zero if it holds
-// none); returns the score of the lane's child.  scr: the wave's scratch
-// (kKnapScratch uint4); tab: the digit table in LDS, [s][h][16 columns] x
-// 16 B, columns >= knap_cols zero.
-template <int GS>
-__device__ __forceinline__ float knap_mfma(const GenArgs& a, uint4 v, uint32_t lane, uint32_t q, uint4* scr,
-                                           const uint4* tab) {
-  constexpr uint32_t R = GS / 4;
-  const uint32_t D = a.knap_dig, NC = a.knap_cols;
-  scr[knap_slot(lane >> 2, lane & 3u)] = v;
-  wave_lds_sync();
-  const uint32_t h = lane >> 4, n = lane & 15u;
-  const uint4 x = scr[knap_slot(n, h)];  // A: virtual row n, lane group h's 128 bits
-  const uint32_t xs[4] = {x.x, x.y, x.z, x.w};
-  const uint4* tb = tab + h * kKnapMaxCols + n;
-  v4i acc = {0, 0, 0, 0};
-#pragma unroll
-  for (uint32_t s = 0; s < kKnapSlices; ++s) {
-    const uint4 t = tb[s * 4u * kKnapMaxCols];
-    const uint32_t bits = (s & 1u) ? (xs[s >> 1] >> 16) : (xs[s >> 1] & 0xFFFFu);
-    acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(expand16(bits), v4i{(int)t.x, (int)t.y, (int)t.z, (int)t.w}, acc,
-                                                0, 0, 0);
-  }
-  wave_lds_sync();
-  int* cl = (int*)scr;  // C, column-major: [column n][row 4h + i], stride kKnapCStride
-  *(v4i*)(cl + n * kKnapCStride + 4u * h) = acc;
-  wave_lds_sync();
-  const uint32_t g = lane / GS;
-  uint32_t V = 0, W = 0;  // mod 2^32: exact, the true sums are below 2^24
-  for (uint32_t e = q; e < NC; e += GS) {
-    const uint32_t r = e / (2u * D), d = e % D;
-    const uint32_t c = (uint32_t)cl[e * kKnapCStride + g * R + r] << (8u * d);
-    if ((e / D) & 1u) W += c;
-    else V += c;
-  }
-  const float vv = (float)(int)group_sum_u<GS>(V), ww = (float)(int)group_sum_u<GS>(W);
-  return ww <= a.obj_f0 ? vv : a.obj_f0 - ww;
-}
-
-// Sparse bit-flip sampler, group-cooperative form: continue the sequence of
-// mutation words at j with n distinct positions already flipped in fm (this
-// lane's chunk q), until K distinct positions are flipped.  A candidate is a
-// repeat iff its owner lane already has the bit: one ballot per candidate.
-template <int GS, bool NH = false>
-__device__ __forceinline__ uint4 sparse_continue(const GenArgs& a, uint64_t child, uint32_t K, uint32_t n, uint32_t j,
-                                              uint4 fm, uint32_t q, uint32_t gbase) {
-  u32x4 blk = draw<NH>(a.key, ST_BMUT, child, j >> 2);
-  while (n < K) {  // group-uniform
-    if ((j & 3u) == 0u) blk = draw<NH>(a.key, ST_BMUT, child, j >> 2);
-    const uint32_t p = word_to_index(sel4(blk, j & 3u), a.L);
-    ++j;
-    const uint32_t b = p & 127u;
-    const bool own = (p >> 7) == q;
-    const uint32_t wd = sel4(u32x4{fm.x, fm.y, fm.z, fm.w}, b >> 5);
-    unsigned long long bal = __ballot(own && ((wd >> (b & 31u)) & 1u));
-    if (GS < 64) bal = (bal >> gbase) & ((1ull << GS) - 1ull);
-    if (bal == 0ull) {
-      if (own) fm = xor4(fm, bit4(b));
-      ++n;
-    }
-  }
-  return fm;
-}
-
-// Sparse bit-flip sampler, sequential form (the definition, cpu_ops.cpp
-// sparse_positions): the first kk distinct word_to_index(mutation word j, L),
-// packed as 16-bit positions (0xFFFF = none; positions are < kSparseMaxL);
-// jn = the next unused word.
-template <bool NH>
-__device__ __forceinline__ uint4 sparse_seq(const RngKey& key, uint64_t child, uint32_t kk, uint32_t L, uint32_t& jn) {
-  uint32_t w0 = 0xFFFFFFFFu, w1 = 0xFFFFFFFFu, w2 = 0xFFFFFFFFu, w3 = 0xFFFFFFFFu;
-  uint32_t n = 0, j = 0;
-  u32x4 blk{0, 0, 0, 0};
-  while (n < kk) {
-    if ((j & 3u) == 0u) blk = draw<NH>(key, ST_BMUT, child, j >> 2);
-    const uint32_t p = word_to_index(sel4(blk, j & 3u), L);
-    ++j;
-    const bool seen = (w0 & 0xFFFFu) == p || (w0 >> 16) == p || (w1 & 0xFFFFu) == p || (w1 >> 16) == p ||
-                      (w2 & 0xFFFFu) == p || (w2 >> 16) == p || (w3 & 0xFFFFu) == p || (w3 >> 16) == p;
-    if (!seen) {
-      const uint32_t sh = (n & 1u) * 16u, keep = ~(0xFFFFu << sh), v = p << sh, wi = n >> 1;
-      w0 = wi == 0u ? (w0 & keep) | v : w0;
-      w1 = wi == 1u ? (w1 & keep) | v : w1;
-      w2 = wi == 2u ? (w2 & keep) | v : w2;
-      w3 = wi == 3u ? (w3 & keep) | v : w3;
-      ++n;
-    }
-  }
-  jn = j;
-  return make_uint4(w0, w1, w2, w3);
-}
-
-// ---------------------------------------------------------------------------
-// Generic kernel: every mode, every operator, any genome length.
-// ---------------------------------------------------------------------------
-template <int GS, int OBJ, int MODE>
-__global__ __launch_bounds__(kBlock) void binary_kernel(GenArgs a, unsigned long long* best_parts) {
-  resolve_gen(a);
-  __shared__ unsigned long long lds_red[kBlock / 64];
-  __shared__ uint32_t lds_elite;
-  __shared__ uint32_t lds_thr[kMutCap];
-
-  const uint32_t lane = lane_id();
-  const uint32_t q = lane & (GS - 1);
-  const uint32_t gbase = lane & ~(uint32_t)(GS - 1);
-  constexpr uint32_t GPB = kBlock / GS;
-  const uint32_t g_in_block = threadIdx.x / GS;
-  const uint64_t rs = a.row_words >> 2;  // row stride in uint4
-  const uint4* cur = (const uint4*)a.cur;
-  uint4* nxt = (uint4*)a.next;
-  const uint32_t nchunks = a.chunks;
-  const uint32_t L = a.L;
-  constexpr bool MUTATES = MODE == MODE_GEN || MODE == MODE_MUTATE;
-  constexpr bool EVALS = OBJ != OBJ_NONE && (MODE == MODE_GEN || MODE == MODE_INIT || MODE == MODE_EVAL);
-  const bool bitflip = MUTATES && a.mutation == MUT_BIT_FLIP && a.mut_rate > 0.f;
-  const bool sparse = bitflip && a.mut_sparse;
-  const bool reset_one = MUTATES && a.mutation == MUT_RESET_ONE;
-
-  if (MODE == MODE_GEN && a.n_elite > 0 && a.elite_idx == nullptr && blockIdx.x == 0) {
-    unsigned long long b = block_reduce_parts(a.best_cur, a.n_best_cur, lds_red);
-    if (threadIdx.x == 0) lds_elite = (uint32_t)best_index(b);
-  }
-  if (bitflip)
-    for (uint32_t i = threadIdx.x; i < kMutCap; i += kBlock) lds_thr[i] = a.mut_thr[i];
-  __syncthreads();
-
-  unsigned long long my_best = 0;
-  ScoreStats st;
-  const uint64_t stride = (uint64_t)gridDim.x * GPB;
-  for (uint64_t child = (uint64_t)blockIdx.x * GPB + g_in_block; child < a.S; child += stride) {
-    float score = 0.f;
-    {
-      // elitism: child = copy of the elite row, re-evaluated like every child
-      const bool elite = MODE == MODE_GEN && child < a.n_elite;
-      uint32_t pa = 0, pb = 0;
-      bool xo = false;
-      uint32_t blo = 0, bhi = 0;  // ONE/TWO_POINT: bits [blo, bhi) come from parent B
-      u32x4 misc{0, 0, 0, 0};
-      if (MODE == MODE_GEN || MODE == MODE_CROSS || MODE == MODE_MUTATE) misc = bin_misc(a.key, child);
-      if (elite) {
-        pa = pb = a.elite_idx ? a.elite_idx[child] : lds_elite;
-      } else if (MODE == MODE_GEN || MODE == MODE_CROSS) {
-        st_select_parents(a, child, pa, pb);
-        xo = a.crossover != XO_NONE && do_crossover(a, misc.x);
-        if (a.crossover == XO_ONE_POINT) {
-          blo = word_to_index(misc.y, L);
-          bhi = L;
-        } else if (a.crossover == XO_TWO_POINT) {
-          uint32_t c1 = word_to_index(misc.y, L);
-          uint32_t c2 = word_to_index(misc.z, L);
-          blo = c1 < c2 ? c1 : c2;
-          bhi = c1 < c2 ? c2 : c1;
-        }
-      }
-      uint32_t rpos = 0xFFFFFFFFu;  // RESET_ONE: the one flipped bit
-      if (reset_one && !elite && misc.w < a.mut_ind_thresh) rpos = word_to_index(bin_mut_word(a.key, child, 0), L);
-      uint4 fm = make_uint4(0, 0, 0, 0);  // sparse bit-flip: flips of chunk q (L <= 8192: one chunk per lane)
-      if (sparse && !elite) fm = sparse_continue<GS>(a, child, binom_count(misc.w, lds_thr), 0, 0, fm, q, gbase);
-
-      BinObj<OBJ> acc;
-      for (uint32_t c0 = 0; c0 < nchunks; c0 += GS) {  // group-uniform segment loop
-        const uint32_t c = c0 + q;
-        if (c >= nchunks) continue;
-        uint4 v = make_uint4(0, 0, 0, 0);
-        if (MODE == MODE_INIT) {
-          v = u4(draw(a.key, ST_INIT, child, c));
-        } else if (MODE == MODE_EVAL || MODE == MODE_MUTATE) {
-          v = cur[child * rs + c];
-        } else {
-          const uint4 A = cur[(uint64_t)pa * rs + c];
-          if (xo) {
-            const uint4 B = cur[(uint64_t)pb * rs + c];
-            const uint4 m = a.crossover == XO_UNIFORM ? u4(draw(a.key, ST_XO, child, c)) : range_keep_a(c, blo, bhi);
-            v = mix4(A, B, m);
-          } else {
-            v = A;
-          }
-        }
-        if (c == nchunks - 1) v = and4(v, u4(a.last_mask));
-        if (bitflip && !sparse && !elite) {
-          v = xor4(v, u4(chunk_flip_mask(a, child, c, chunk_len(L, c), bin_chunk_mut_word(a.key, child, c), lds_thr)));
-        } else if (sparse) {
-          v = xor4(v, fm);
-        } else if (reset_one && (rpos >> 7) == c) {
-          v = xor4(v, bit4(rpos & 127u));
-        }
-        if (MODE != MODE_EVAL) nxt[child * rs + c] = v;
-        if (EVALS) acc.add(a, v, c);
-      }
-      if (EVALS) score = acc.template finish<GS>(a);
-    }
-    if (EVALS && q == 0) {
-      a.score_next[child] = score;
-      if (a.key_next) a.key_next[child] = (uint16_t)score;
-      const unsigned long long pb = pack_best(score, child);
-      my_best = pb > my_best ? pb : my_best;
-      st.add(score);
-    }
-  }
-  if (EVALS && best_parts) {
-    unsigned long long b = block_max_u64(my_best, lds_red);
-    if (threadIdx.x == 0) best_parts[blockIdx.x] = b;
-    if (a.stats_parts) block_stats_store(st, a.stats_parts);
-  }
-}
-
-// ---------------------------------------------------------------------------
-// The hot generation kernel: transposed tournaments.
-//
-// A wave owns a contiguous range of children and breeds NG = 64/GS of them per
-// STEP (group g: child begin + t*NG + g).  Steps come in BATCHES of GS steps =
-// 64 children, and the per-child work that does not touch the genome runs
-// transposed, one lane per child of a whole batch.  The range is cut into
-// SEGMENTS of up to kSegBatches batches, each in two phases:
-//   TOURNAMENTS  every batch of the segment at once: one Philox block = the 4
-//                contestants of a child, all 4 x kSegBatches key loads in
-//                flight together, compare -> (parent A, parent B) in LDS
-//                (linear ranking: two rank picks, two rank-order loads)
-//   BREED        per batch, RESOLVE: the misc block (crossover test, cut
-//                points, mutation count K) and the sparse bit-flip positions
-//                (one more block, first K distinct by a pairwise check) -> a
-//                32-byte child RECORD in the wave's LDS ring (2 batches);
-//                per step: XO mask Philox (one block per chunk), mix, flips,
-//                popcount, group butterfly, stores.
-// Why two phases: the EA (L2 -> fabric) traffic is the bound (PMC: ~530 MB
-// per generation at 1M x 1024 bits, ~5.7 TB/s).  Tournament keys are a 2 MB
-// array read at random; interleaved with the row gathers, ~1/4 of the key
-// reads missed the XCD's 4 MB L2 (a 128-B line each, ~1/4 of all EA bytes).
-// At kernel start every wave is in its tournament phase, so the L2 holds
-// little but key lines and the key reads cost ~2 MB of fabric per XCD.
-// A child costs 3/64 of a Philox per lane for its child-level words, and
-// mutation is a short loop over the record's positions instead of a
-// divergent geometric search in every chunk.
-//
-// Breed pipeline (per step t): RESOLVE batch (t+1)/GS if (t+1)%GS==0; load
-// the parent rows of step t+1; breed step t from the rows loaded one step
-// earlier.  Every vector memory operation is unconditional (s_waitcnt vmcnt
-// retires in order and hipcc assumes the fewest outstanding loads over all
-// paths, so a conditionally issued load would make the next wait drain it).
-// ---------------------------------------------------------------------------
-
-#ifdef PGA_TP_TIMING
-// experiment builds only (tools/variants.sh): per-wave clocks of the two
-// phases, wall-clock start / end and the XCD the wave ran on
-__device__ unsigned long long pga_tp_clk[kMaxGrid * 4][8];
-#endif
-
-// kTpMaxElite (elites the fast kernel routes through its records),
-// kSegBatches and the work units: tp.hpp
-
-// 5 waves/SIMD: 4, 5 and 6 measured alike for the breed phase alone (the
-// fabric, not occupancy, is the bound); 5 gives the tournament phase its
-// 16 key loads in flight without spilling (6: 23 spilled VGPRs, +8%)
-#ifndef PGA_TP_WAVES
-#define PGA_TP_WAVES 5
-#endif
-#ifndef PGA_TP_NOKEYS
-#define PGA_TP_NOKEYS 0
-#endif
-
-__device__ __forceinline__ uint32_t pos16(uint4 r1, uint32_t k) {  // k-th packed 16-bit position
-  const uint32_t w = sel4(u32x4{r1.x, r1.y, r1.z, r1.w}, k >> 1);
-  return (k & 1u) ? (w >> 16) : (w & 0xFFFFu);
-}
-
-// the uniform-crossover mask of chunk q of child c (ST_XO block q); experiment
-// builds can swap in a multiplicative hash to measure the Philox's share
-#ifdef PGA_TP_XOHASH
-#define PGA_TP_XOMASK(c, q) make_uint4(mut_skip_word((c) * 4u, (q)), mut_skip_word((c) * 4u + 1u, (q)), \
-                                       mut_skip_word((c) * 4u + 2u, (q)), mut_skip_word((c) * 4u + 3u, (q)))
-#else
-#define PGA_TP_XOMASK(c, q) u4(draw<true>(a.key, ST_XO, (c), (q)))
-#endif
-
-template <int GS, int OBJ, bool FULL, bool DENSE>
-__global__ __launch_bounds__(kBlock, OBJ == kObjKnapMfma ? 4 : PGA_TP_WAVES) void binary_gen_tp(GenArgs a, unsigned long long* best_parts) {
-  resolve_gen(a);
-  constexpr uint32_t NW = kBlock / 64;
-  constexpr uint32_t NG = 64 / GS;  // children per wave per step
-  constexpr bool EVALS = OBJ != OBJ_NONE;
-  // integer objectives tournament on their exact u16 keys (L2-resident)
-  constexpr bool KEY = OBJ == OBJ_ONEMAX || OBJ == OBJ_LEADING_ONES || OBJ == OBJ_TRAP;
-  __shared__ uint4 lds_rec[NW][2][64][2];           // per wave: 2 batches x 64 records x 32 B
-  __shared__ uint2 lds_par[NW][kSegBatches * 64];  // per wave: the segment's (parent A, parent B)
-  __shared__ uint32_t lds_thr[kMutCap];
-  __shared__ uint32_t lds_el[kTpMaxElite];  // elite sources
-  __shared__ unsigned long long lds_red[NW];
-  constexpr bool KMF = OBJ == kObjKnapMfma;
-  __shared__ uint4 lds_kscr[KMF ? NW : 1][kKnapScratch];             // knapsack: per-wave chunk / C scratch
-  __shared__ uint4 lds_ktab[KMF ? kKnapSlices * 4 * kKnapMaxCols : 1];  // knapsack: digit table
-
-  const uint32_t lane = lane_id(), wid = threadIdx.x >> 6;
-  const uint32_t q = lane & (GS - 1), gbase = lane & ~(uint32_t)(GS - 1), g = lane / GS;
-  const uint4* cur = (const uint4*)a.cur;
-  uint4* nxt = (uint4*)a.next;
-  const uint32_t L = a.L, S = (uint32_t)a.S;
-  // FULL: chunks == GS, every lane owns a chunk
-  const bool have = FULL || q < a.chunks, last = q == a.chunks - 1;
-  const uint32_t qq = have ? q : 0u;
-  const uint32_t clen = have ? chunk_len(L, q) : 0u;
-  const bool tourn = a.selection == SEL_TOURNAMENT;  // tour_k == 2 guaranteed by the launcher
-  const bool rank = a.selection == SEL_RANK;
-  const bool roul = a.selection == SEL_ROULETTE;     // else random
-  const bool xo_on = a.crossover != XO_NONE;
-  const bool range = a.crossover != XO_UNIFORM;  // ONE/TWO_POINT, or NONE (empty range)
-  // DENSE: per-chunk geometric bit-flips; otherwise the record carries the
-  // flip positions (sparse bit-flip, RESET_ONE, or none)
-  const bool bitflip = a.mutation == MUT_BIT_FLIP && a.mut_rate > 0.f;
-  const bool sparse = !DENSE && bitflip;
-  const bool reset_one = !DENSE && a.mutation == MUT_RESET_ONE;
-  const uint4 lmask = u4(a.last_mask);
-  // Every row / score byte offset fits 32 bits (the launcher checks (S + pad)
-  // rows < 4 GiB): uniform base + 32-bit lane offset, one VGPR per address
-  const uint32_t rb = a.row_words * 4u;
-#define ELEM(T, base, i) (*(T*)((char*)(base) + (uint32_t)(i) * (uint32_t)sizeof(T)))
-#define ROW(base, row, ch) (*(uint4*)((char*)(base) + ((uint32_t)(row) * rb + (uint32_t)(ch) * 16u)))
-
-  // this wave's children [wbegin, wend): contiguous, a multiple of NG long
-  uint32_t wbegin, wend, bfirst;
-  tp_wave_range(S, NG, wbegin, wend, bfirst);
-
-  // elite sources of children [0, n_elite) (n_elite <= kTpMaxElite), for the
-  // blocks that hold any of them
-  if (a.n_elite > 0 && bfirst < a.n_elite) {
-    if (a.elite_idx) {
-      for (uint32_t i = threadIdx.x; i < a.n_elite; i += kBlock) lds_el[i] = a.elite_idx[i];
-    } else {
-      unsigned long long b = block_reduce_parts(a.best_cur, a.n_best_cur, lds_red);
-      if (threadIdx.x == 0) lds_el[0] = (uint32_t)best_index(b);
-    }
-  }
-  if (bitflip)
-    for (uint32_t i = threadIdx.x; i < kMutCap; i += kBlock) lds_thr[i] = a.mut_thr[i];
-  if (KMF)
-    for (uint32_t i = threadIdx.x; i < kKnapSlices * 4 * kKnapMaxCols; i += kBlock)
-      lds_ktab[i] = ((const uint4*)a.knap_tab)[i];
-  __syncthreads();
-
-  unsigned long long my_best = 0;
-  ScoreStats st;
-  uint4(*rec)[64][2] = lds_rec[wid];
-  uint2* par = lds_par[wid];
-  static_assert(sizeof(lds_rec[0]) >= kSegBatches * 64 * sizeof(uint4), "contestant staging");
-#ifdef PGA_TP_TIMING
-  const unsigned long long clk0 = clock64(), rt0 = wall_clock64();
-  unsigned long long clk_t = 0, clk_b = 0;
-#endif
-  for (uint32_t begin = wbegin; begin < wend; begin += kSegBatches * 64u) {  // wave-uniform
-    const uint32_t end = begin + kSegBatches * 64u < wend ? begin + kSegBatches * 64u : wend;
-    const uint32_t nsteps = (end - begin + NG - 1) / NG;
-    const uint32_t nbatch = (end - begin + 63) / 64;
-#ifdef PGA_TP_TIMING
-    const unsigned long long clkA = clock64();
-#endif
-
-    // TOURNAMENTS of the whole segment: all key loads in flight at once; the
-    // contestants wait in the record ring (free until the first RESOLVE)
-    {
-      uint4* ixs = &rec[0][0][0];  // [B * 64 + lane]: 4 x 64 x 16 B = the ring's 4 KiB
-      // raw keys (u16 zero-extended, or f32 scores), compared only after every
-      // load of the segment is issued: a conversion here would make hipcc wait
-      // for each batch's loads before issuing the next batch's
-      using KT = typename std::conditional<KEY, uint32_t, float>::type;
-      KT k0[kSegBatches], k1[kSegBatches], k2[kSegBatches], k3[kSegBatches];
-#pragma unroll
-      for (uint32_t B = 0; B < kSegBatches; ++B) {
-        const uint32_t tc = begin + B * 64u + lane;
-        const uint32_t cc = tc < end ? tc : end - 1;
-        u32x4 blk{0u, 0u, 0u, 0u};
-        if (B < nbatch) blk = draw<true>(a.key, ST_SEL, cc, 0);  // wave-uniform; batches past the end load line 0
-        const uint4 ix = make_uint4(word_to_index(blk.x, S), word_to_index(blk.y, S), word_to_index(blk.z, S),
-                                    word_to_index(blk.w, S));
-        ixs[B * 64u + lane] = ix;
-        const uint4 j = tourn ? ix : make_uint4(0, 0, 0, 0);
-        if (roul) {  // wave-uniform: the two selection words, searched below for every batch at once
-          k0[B] = __builtin_bit_cast(KT, blk.x);
-          k1[B] = __builtin_bit_cast(KT, blk.y);
-        } else if (rank) {  // wave-uniform: linear ranking, the two parents straight from the rank order
-          const u32x4 b1 = draw<true>(a.key, ST_SEL, cc, 1);
-          const uint32_t ra = rank_pick(blk.x, blk.y, blk.z, S, a.rank_thresh);
-          const uint32_t rb = rank_pick(blk.w, b1.x, b1.y, S, a.rank_thresh);
-          k0[B] = __builtin_bit_cast(KT, ELEM(const uint32_t, a.rank_order, ra));
-          k1[B] = __builtin_bit_cast(KT, ELEM(const uint32_t, a.rank_order, rb));
-        } else if constexpr (KEY && PGA_TP_NOKEYS) {  // experiment: tournaments without key reads
-          k0[B] = j.x & 1023u;
-          k1[B] = j.y & 1023u;
-          k2[B] = j.z & 1023u;
-          k3[B] = j.w & 1023u;
-        } else if constexpr (KEY) {
-          k0[B] = ELEM(const uint16_t, a.key_cur, j.x);
-          k1[B] = ELEM(const uint16_t, a.key_cur, j.y);
-          k2[B] = ELEM(const uint16_t, a.key_cur, j.z);
-          k3[B] = ELEM(const uint16_t, a.key_cur, j.w);
-        } else {
-          k0[B] = ELEM(const float, a.score_cur, j.x);
-          k1[B] = ELEM(const float, a.score_cur, j.y);
-          k2[B] = ELEM(const float, a.score_cur, j.z);
-          k3[B] = ELEM(const float, a.score_cur, j.w);
-        }
-        // no early exit past the segment's last batch: straight-line loads keep
-        // every key in a register (a wave-uniform break spilled the last four);
-        // the extra batches skip the Philox draw and are never resolved
-      }
-      if (roul) {
-        // fitness-proportional, by the guide table: the pick is the smallest i
-        // with cumfit[i] >= u * total (roulette_pick's binary search); the guide
-        // entry of the target's bucket is a lower bound for it, so one guide load,
-        // one cumfit load and (rarely) a short forward scan find it.  The
-        // 2 x kSegBatches picks of a lane advance in lock step.
-        constexpr uint32_t NS = 2 * kSegBatches;
-        const float total = a.cumfit[S - 1];
-        const float scale = *a.roul_scale;
-        uint32_t ix[NS];
-        float tg[NS];
-        #pragma unroll
-        for (uint32_t i = 0; i < NS; ++i) {
-          const uint32_t w = __builtin_bit_cast(uint32_t, (i & 1u) ? k1[i >> 1] : k0[i >> 1]);
-          tg[i] = word_to_unit(w) * total;
-          ix[i] = total > 0.f ? ELEM(const uint32_t, a.roul_guide, roulette_bucket(tg[i], scale, S)) : word_to_index(w, S);
-        }
-        float v[NS];
-        #pragma unroll
-        for (uint32_t i = 0; i < NS; ++i) v[i] = ELEM(const float, a.cumfit, ix[i]);
-        for (uint32_t it = 0; it < S; ++it) {  // wave-uniform: until every pick of every lane is resolved
-          bool more = false;
-          #pragma unroll
-          for (uint32_t i = 0; i < NS; ++i) more |= total > 0.f && v[i] < tg[i];
-          if (!__any(more)) break;
-          #pragma unroll
-          for (uint32_t i = 0; i < NS; ++i) {
-            const bool adv = total > 0.f && v[i] < tg[i];
-            ix[i] += adv ? 1u : 0u;
-            v[i] = ELEM(const float, a.cumfit, ix[i]);
-          }
-        }
-        #pragma unroll
-        for (uint32_t B = 0; B < kSegBatches; ++B) {
-          k0[B] = __builtin_bit_cast(KT, ix[2 * B]);
-          k1[B] = __builtin_bit_cast(KT, ix[2 * B + 1]);
-        }
-      }
-#pragma unroll
-      for (uint32_t B = 0; B < kSegBatches; ++B) {
-        const uint4 ix = ixs[B * 64u + lane];
-        uint32_t pa = ix.x, pb = ix.y;
-        if (tourn) {
-          pa = k0[B] < k1[B] ? ix.y : ix.x;
-          pb = k2[B] < k3[B] ? ix.w : ix.z;
-        } else if (rank || roul) {
-          pa = __builtin_bit_cast(uint32_t, k0[B]);
-          pb = __builtin_bit_cast(uint32_t, k1[B]);
-        }
-        par[B * 64u + lane] = make_uint2(pa, pb);
-      }
-    }
-#ifdef PGA_TP_TIMING
-    const unsigned long long clkB = clock64();
-    clk_t += clkB - clkA;
-#endif
-
-    // RESOLVE: parents, crossover plan and flip positions of batch B -> records
-#define PGA_TP_RESOLVE(B)                                                                                       \
-  {                                                                                                             \
-    const uint32_t tc = begin + (B) * 64u + lane;                                                               \
-    const uint32_t cc = tc < end ? tc : end - 1;                                                                \
-    const uint2 pp = par[(B) * 64u + lane];                                                                     \
-    uint32_t pa = pp.x, pb = pp.y;                                                                              \
-    const u32x4 misc = bin_misc<true>(a.key, cc);                                                               \
-    const bool elite = tc < a.n_elite;                                                                          \
-    const bool xo = !elite && xo_on && do_crossover(a, misc.x);                                                 \
-    if (elite) pa = lds_el[tc];                                                                                 \
-    pb = xo ? pb : pa;                                                                                          \
-    uint32_t lo = 0, hi = 0;                                                                                    \
-    if (range && xo) {                                                                                          \
-      const uint32_t x1 = word_to_index(misc.y, L);                                                             \
-      if (a.crossover == XO_ONE_POINT) {                                                                        \
-        lo = x1;                                                                                                \
-        hi = L;                                                                                                 \
-      } else {                                                                                                  \
-        const uint32_t x2 = word_to_index(misc.z, L);                                                           \
-        lo = x1 < x2 ? x1 : x2;                                                                                 \
-        hi = x1 < x2 ? x2 : x1;                                                                                 \
-      }                                                                                                         \
-    }                                                                                                           \
-    uint32_t K = 0, jn = 0;                                                                                     \
-    uint4 P = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu);                                   \
-    if (reset_one && !elite && misc.w < a.mut_ind_thresh) {                                                     \
-      K = 1;                                                                                                    \
-      P.x = word_to_index(bin_mut_word<true>(a.key, cc, 0), L) | 0xFFFF0000u;                                   \
-    }                                                                                                           \
-    if (sparse && !elite) {                                                                                     \
-      K = binom_count(misc.w, lds_thr);                                                                         \
-      if (K > 0u) {                                                                                             \
-        const uint32_t kk = K < kRecPos ? K : kRecPos;                                                          \
-        const u32x4 m0 = draw<true>(a.key, ST_BMUT, cc, 0);                                                     \
-        const uint32_t c0 = word_to_index(m0.x, L), c1 = word_to_index(m0.y, L);                                \
-        const uint32_t c2 = word_to_index(m0.z, L), c3 = word_to_index(m0.w, L);                                \
-        /* common case: the first kk <= 4 candidates are distinct, hence the positions */                      \
-        const bool slow = kk > 4u || (kk > 1u && c0 == c1) || (kk > 2u && (c2 == c0 || c2 == c1)) ||            \
-                          (kk > 3u && (c3 == c0 || c3 == c1 || c3 == c2));                                      \
-        P = make_uint4(c0 | (c1 << 16), c2 | (c3 << 16), 0xFFFFFFFFu, 0xFFFFFFFFu);                             \
-        jn = kk;                                                                                                \
-        if (slow) P = sparse_seq<true>(a.key, cc, kk, L, jn);                                                   \
-      }                                                                                                         \
-    }                                                                                                           \
-    const uint32_t meta = (K > 255u ? 255u : K) | ((jn > 0xFFFFu ? 0xFFFFu : jn) << 8) | (elite ? 1u << 31 : 0u); \
-    uint4(*r)[2] = rec[(B) & 1u];                                                                               \
-    r[lane][0] = make_uint4(pa, pb, lo | (hi << 16), meta);                                                     \
-    r[lane][1] = P;                                                                                             \
-  }
-
-    // prologue: batch 0 resolved, rows of step 0 in flight
-    PGA_TP_RESOLVE(0u)
-    uint4 A0, B0, A1, B1;
-    {
-      const uint4 r = rec[0][g][0];
-      A0 = ROW(cur, r.x, qq);
-      B0 = ROW(cur, r.y, qq);
-    }
-
-    // one STEP: every vector-memory operation is unconditional (the tail of
-    // the last wave writes the padding rows past S)
-#define PGA_TP_STEP(t, XA, XB, YA, YB)                                                                      \
-  {                                                                                                         \
-    const uint32_t b = (t) / GS, i = (t) & (GS - 1);                                                        \
-    if ((((t) + 1) & (GS - 1)) == 0u && b + 1 < nbatch) PGA_TP_RESOLVE(b + 1)                               \
-    {                                                                                                       \
-      /* parent rows of step t+1 (the last step re-reads its own) */                                        \
-      const uint32_t tn = (t) + 1 < nsteps ? (t) + 1 : (t);                                                 \
-      const uint4 r = rec[(tn / GS) & 1u][(tn & (GS - 1)) * NG + g][0];                                     \
-      YA = ROW(cur, r.x, qq);                                                                               \
-      YB = ROW(cur, r.y, qq);                                                                               \
-    }                                                                                                       \
-    const uint32_t c = begin + (t) * NG + g;                                                                \
-    const uint4 r0 = rec[b & 1u][i * NG + g][0];                                                            \
-    const uint32_t meta = r0.w;                                                                             \
-    const uint4 m = range ? range_keep_a(q, r0.z & 0xFFFFu, r0.z >> 16) : PGA_TP_XOMASK(c, q);               \
-    uint4 v = mix4(XA, XB, m);                                                                              \
-    if (last) v = and4(v, lmask);                                                                           \
-    uint4 fm = make_uint4(0, 0, 0, 0);                                                                      \
-    if (DENSE) {                                                                                            \
-      if (bitflip && !(meta >> 31)) /* elites are not mutated */                                           \
-        fm = u4(chunk_flip_mask(a, c, q, clen, bin_chunk_mut_word<true>(a.key, c, q), lds_thr));            \
-    } else {                                                                                                \
-      const uint32_t K = meta & 0xFFu;                                                                      \
-      if (K > 0u) {                                                                                         \
-        const uint4 r1 = rec[b & 1u][i * NG + g][1];                                                        \
-        const uint32_t kk = K < kRecPos ? K : kRecPos;                                                      \
-        /* the first 4 unrolled (a loop here costs ~20 VGPRs of the whole kernel) */                       \
-        _Pragma("unroll") for (uint32_t k = 0; k < 4; ++k) {                                               \
-          const uint32_t p = pos16(r1, k);                                                                  \
-          if (k < kk && (p >> 7) == q) fm = xor4(fm, bit4(p & 127u));                                       \
-        }                                                                                                   \
-        if (kk > 4u)                                                                                        \
-          for (uint32_t k = 4; k < kk; ++k) {                                                               \
-            const uint32_t p = pos16(r1, k);                                                                \
-            if ((p >> 7) == q) fm = xor4(fm, bit4(p & 127u));                                              \
-          }                                                                                                 \
-        if (K > kRecPos) fm = sparse_continue<GS, true>(a, c, K, kRecPos, (meta >> 8) & 0xFFFFu, fm, q, gbase); \
-      }                                                                                                     \
-    }                                                                                                       \
-    v = xor4(v, fm);                                                                                        \
-    float sc;                                                                                               \
-    if constexpr (KMF) {                                                                                    \
-      sc = knap_mfma<GS>(a, have ? v : make_uint4(0, 0, 0, 0), lane, q, lds_kscr[wid], lds_ktab);            \
-    } else {                                                                                                \
-      BinObj<OBJ> acc;                                                                                      \
-      if (have) acc.add(a, v, q);                                                                           \
-      sc = acc.template finish<GS>(a);                                                                      \
-    }                                                                                                       \
-    if (have) ROW(nxt, c, q) = v;                                                                           \
-    if (EVALS) { /* every lane of the group stores the same score */                                        \
-      ELEM(float, a.score_next, c) = sc;                                                                    \
-      if (KEY) ELEM(uint16_t, a.key_next, c) = (uint16_t)sc;                                                \
-      const unsigned long long pk = c < S ? pack_best(sc, c) : 0ull;                                        \
-      my_best = pk > my_best ? pk : my_best;                                                                \
-      st.add_if(q == 0u && c < S, sc);                                                                      \
-    }                                                                                                       \
-  }
-
-    uint32_t t = 0;
-    for (; t + 1 < nsteps; t += 2) {  // static row-register rotation
-      PGA_TP_STEP(t, A0, B0, A1, B1)
-      PGA_TP_STEP(t + 1, A1, B1, A0, B0)
-    }
-    if (t < nsteps) PGA_TP_STEP(t, A0, B0, A1, B1)
-#undef PGA_TP_RESOLVE
-#undef PGA_TP_STEP
-#ifdef PGA_TP_TIMING
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this segment's stores issued and done
-    clk_b += clock64() - clkB;
-#endif
-  }
-#undef ROW
-#undef ELEM
-#ifdef PGA_TP_TIMING
-  if (lane == 0) {
-    const uint32_t wv = blockIdx.x * NW + wid;
-    pga_tp_clk[wv][0] = clk_t;
-    pga_tp_clk[wv][1] = clk_b;
-    pga_tp_clk[wv][2] = clock64() - clk0;
-    pga_tp_clk[wv][3] = wend - wbegin;
-    pga_tp_clk[wv][4] = rt0;
-    pga_tp_clk[wv][5] = wall_clock64();
-    pga_tp_clk[wv][6] = __builtin_amdgcn_s_getreg((3 << 11) | 20);  // HW_REG_XCC_ID[3:0]
-  }
-#endif
-  unsigned long long bb = block_max_u64(my_best, lds_red);
-  if (threadIdx.x == 0 && best_parts && EVALS) best_parts[blockIdx.x] = bb;
-  if (EVALS && best_parts && a.stats_parts) block_stats_store(st, a.stats_parts);
-}
 
 template <typename K>
 uint32_t go(K kernel, const GenArgs& a, unsigned long long* parts, uint32_t gpb, hipStream_t s) {
@@ -930,6 +191,20 @@ bool build_knap_table(const float* values, const float* weights, uint32_t L, uin
   digits = D;
   cols = NC;
   return true;
+}
+
+bool binary_tp_plan(const GenArgs& a, uint32_t& gs, bool& full, bool& dense) {
+  // the conditions launch_mode applies before choosing binary_gen_tp, for an
+  // objective that tournaments on f32 scores (a JIT objective)
+  gs = group_size(a.chunks);
+  const bool fast = ((a.selection == SEL_TOURNAMENT && a.tour_k == 2) || a.selection == SEL_RANDOM ||
+                     (a.selection == SEL_RANK && a.rank_order != nullptr) ||
+                     (a.selection == SEL_ROULETTE && a.cumfit != nullptr && a.roul_guide != nullptr)) &&
+                    !(a.n_elite > 1 && a.elite_idx == nullptr) && !force_generic_kernels();
+  const bool o32 = (a.S + kRowPad) * (uint64_t)a.row_words * 4u <= 0xFFFFFFFFull;
+  full = a.chunks == gs;
+  dense = a.mutation == MUT_BIT_FLIP && a.mut_rate > 0.f && !a.mut_sparse;
+  return a.chunks <= 64u && fast && o32 && a.n_elite <= kTpMaxElite;
 }
 
 uint32_t binary_launch(int mode, const GenArgs& a, unsigned long long* best_parts, hipStream_t s) {

@@ -102,6 +102,14 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("jit_compile", &pga::jit_compile, py::arg("encoding"), py::arg("source"), py::arg("name"),
         py::arg("options") = std::vector<std::string>{}, py::call_guard<py::gil_scoped_release>());
   m.def("jit_kernel_source", &pga::jit_kernel_source);
+  // several same-shape islands of one device as one launch per generation
+  // (Island::run_batched); False (nothing run) when they do not qualify
+  m.def("run_islands_batched", [](std::vector<Island*> isls, uint32_t n) {
+    if (isls.empty() || !isls[0] || !isls[0]->on_gpu()) return false;
+    hipStream_t s = c10::hip::getCurrentHIPStream(isls[0]->device()).stream();
+    return Island::run_batched(isls, n, s);
+  });
+  m.def("max_batched_islands", &pga::binary_max_batch);
   m.def("trace_level", &pga::trace_level);
   m.def("trace_push", [](const std::string& n) { pga::trace_push(n.c_str()); });
   m.def("trace_pop", &pga::trace_pop);
@@ -178,6 +186,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
              i.set_jit_objective(std::move(k));
            })
       .def_property_readonly("has_jit", &Island::has_jit)
+      .def_property_readonly("jit_fused_generations", &Island::jit_fused_generations)
+      .def_property_readonly("jit_fused_error", &Island::jit_fused_error)
       .def_property("graph_generations", &Island::graph_generations, &Island::set_graph_generations)
       .def_property_readonly("graph_replays", &Island::graph_replays)
       .def_property_readonly("knapsack_digits", &Island::knapsack_digits)

@@ -177,6 +177,16 @@ int pga_run_islands_until(pga_t *p, unsigned generations, unsigned m, float pct,
 /* the same over every rank of an InitAll / loopback group at once */
 int pga_run_islands_multi_until(pga_t **solvers, int n, unsigned generations, unsigned m, float pct, float target);
 
+/* ---- batched islands ----
+ * pga_run_islands / pga_run_islands_until run the populations of one solver
+ * as ONE kernel launch per generation (island = grid y) when they qualify:
+ * two to ten BINARY populations of the same size and length with a built-in
+ * integer objective (OneMax, LeadingOnes, Trap) and the hot kernel's
+ * operators; otherwise each population runs on its own stream.  On by
+ * default; pga_batched_generations counts the generations run batched. */
+int pga_set_batch_islands(pga_t *p, int on);
+unsigned long long pga_batched_generations(const pga_t *p);
+
 #ifdef __cplusplus
 }
 #endif

@@ -4,8 +4,10 @@ The single-device island model.  In the reference, up to 10
 populations share a context, ``*_all`` loops run them serially and migration
 is a stub (include/pga.h:44, src/pga.cu:272-276, :368-374, :393-395).  Here
 the islands are independent ``GeneticAlgorithm`` objects (distinct island ids,
-hence distinct Philox streams) whose generations are enqueued on separate
-streams, so small, latency-bound islands run side by side across the 256 CUs.
+hence distinct Philox streams).  Same-shape BINARY islands with a built-in
+integer objective run as ONE batched launch per generation (island = grid y,
+Island::run_batched); other islands are enqueued on separate streams, so
+small, latency-bound islands run side by side across the 256 CUs.
 Every ``migrate_every`` generations the streams join on the caller's stream
 and the top ``migrate_pct`` of each island replaces the worst of the next one
 (ring, or a seeded random ring) with device-to-device gather/scatter kernels —
@@ -38,7 +40,7 @@ def migration_policy(name: str) -> int:
 class LocalIslands:
     def __init__(self, problem: Problem, n_islands: int, pop_size: int, *, seed: Optional[int] = None,
                  device=None, migrate_every: int = 10, migrate_pct: float = 0.01, topology: str = "ring",
-                 first_island: int = 0, policy: str = "topk", **op_overrides):
+                 first_island: int = 0, policy: str = "topk", batched: bool = True, **op_overrides):
         if n_islands < 1:
             raise ValueError("n_islands must be >= 1")
         if topology not in ("ring", "random"):
@@ -58,6 +60,10 @@ class LocalIslands:
         self.streams = ([torch.cuda.Stream(self.device) for _ in range(n_islands)]
                         if self.device.type == "cuda" else None)
         self.migrations = 0
+        # batched launches (Island::run_batched) when the islands qualify:
+        # BINARY, same shape, built-in integer objective, <= 10 islands
+        self.batched = bool(batched)
+        self.batched_generations = 0
         self._epoch = 0
         self._staging = {}
 
@@ -77,6 +83,12 @@ class LocalIslands:
             for ga in self.islands:
                 ga.run(n)
             return
+        if self.batched and all(ga.torch_objective is None for ga in self.islands):
+            # same-shape islands: ONE launch per generation (island = grid y)
+            from .._ext import C
+            if C.run_islands_batched([ga.island for ga in self.islands], int(n)):
+                self.batched_generations += n
+                return
         main = torch.cuda.current_stream(self.device)
         for ga, s in zip(self.islands, self.streams):
             s.wait_stream(main)

@@ -53,10 +53,13 @@ def test_jit_cpu_uses_fallback():
 
 
 @pytest.mark.gpu
-def test_jit_onemax_bit_identical_to_builtin():
-    L, S = 1024, 1 << 16
-    a = pga.GeneticAlgorithm(M.OneMax(L), S, seed=4, device="cuda:0", elitism=1)
-    b = pga.GeneticAlgorithm(onemax_jit(L), S, seed=4, device="cuda:0", elitism=1)
+@pytest.mark.parametrize("L,kw", [(1024, {}), (777, {}), (1024, dict(mutation_rate=0.02)), (300, dict(selection="rank"))])
+def test_jit_onemax_bit_identical_to_builtin(L, kw):
+    # the objective is linked into the hot generation kernel (one launch per
+    # generation): rows, scores and best equal the built-in OneMax bit for bit
+    S = 1 << 16
+    a = pga.GeneticAlgorithm(M.OneMax(L), S, seed=4, device="cuda:0", elitism=1, **kw)
+    b = pga.GeneticAlgorithm(onemax_jit(L), S, seed=4, device="cuda:0", elitism=1, **kw)
     assert b.island.has_jit
     for _ in range(3):
         a.run(7)
@@ -65,6 +68,32 @@ def test_jit_onemax_bit_identical_to_builtin():
         assert torch.equal(a.rows, b.rows)
         assert torch.equal(a.scores, b.scores)
         assert a.best_score() == b.best_score()
+    assert b.island.jit_fused_error == ""
+    assert b.island.jit_fused_generations >= 20
+
+
+WEIGHTED_SRC = """
+__device__ float wsum(const unsigned int* w, unsigned int nbits, const float* data) {
+  float s = 0.f;
+  for (unsigned int i = 0; i < nbits; ++i) s += ((w[i >> 5] >> (i & 31)) & 1u) ? data[i] : 0.f;
+  return s;
+}
+"""
+
+
+@pytest.mark.gpu
+def test_jit_fused_objective_with_data_matches_oracle():
+    L = 200
+    wts = torch.randn(L, generator=torch.Generator().manual_seed(3))
+    p = M.JitObjective("binary", L, WEIGHTED_SRC, name="wsum", data=wts)
+    ga = pga.GeneticAlgorithm(p, 1 << 14, seed=5, device="cuda:0", elitism=1)
+    s0 = ga.best_score()
+    ga.run(15)
+    torch.cuda.synchronize()
+    assert ga.island.jit_fused_generations >= 15, ga.island.jit_fused_error
+    ref = (ga.genomes().float() * wts.to(ga.genomes().device)).sum(-1)
+    assert torch.allclose(ref, ga.scores, rtol=1e-4, atol=1e-3)
+    assert ga.best_score() > s0
 
 
 @pytest.mark.gpu

@@ -55,3 +55,30 @@ def test_local_islands_streams_match_serial_gpu():
     for x, y in zip(a.islands, b.islands):
         assert torch.equal(x.rows, y.rows) and torch.equal(x.scores, y.scores)
     assert a.migrations == b.migrations == 5
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("L,kw", [(256, {}), (1024, dict(selection="rank")), (700, dict(crossover="two_point"))])
+def test_local_islands_batched_launch_matches_streams_gpu(L, kw):
+    # one launch per generation for all islands (Island::run_batched, island =
+    # grid y) evolves every island exactly as its own launch on its own stream
+    common = dict(seed=11, device="cuda:0", migrate_every=5, migrate_pct=0.02, elitism=1, **kw)
+    a = LocalIslands(pga.models.OneMax(L), 8, 4096, **common)
+    b = LocalIslands(pga.models.OneMax(L), 8, 4096, batched=False, **common)
+    a.run(23)
+    b.run(23)
+    torch.cuda.synchronize()
+    assert a.batched_generations == 23 and b.batched_generations == 0
+    for x, y in zip(a.islands, b.islands):
+        assert torch.equal(x.rows, y.rows) and torch.equal(x.scores, y.scores)
+        assert x.best_score() == y.best_score()
+    assert a.migrations == b.migrations == 4
+
+
+@pytest.mark.gpu
+def test_local_islands_batched_falls_back_gpu():
+    # a float objective does not batch: the islands run on their streams
+    li = LocalIslands(pga.models.Rastrigin(8), 3, 2048, seed=1, device="cuda:0", migrate_every=0)
+    li.run(3)
+    torch.cuda.synchronize()
+    assert li.batched_generations == 0

@@ -29,7 +29,7 @@ ARCH = os.environ.get("PGA_ARCH", "gfx950")
 
 KERNELS = ["csrc/kernels/binary.hip", "csrc/kernels/real.hip", "csrc/kernels/perm.hip",
            "csrc/kernels/util.hip", "csrc/kernels/compat.hip", "csrc/kernels/qubo.hip",
-           "csrc/kernels/sort.hip"]
+           "csrc/kernels/sort.hip", "csrc/kernels/binary_batch.hip"]
 HOST = ["csrc/engine/island.cpp", "csrc/engine/trace.cpp", "csrc/engine/jit.cpp", "csrc/cpu/cpu_ops.cpp", "csrc/cpu/cpu_real.cpp", "csrc/cpu/cpu_perm.cpp", "csrc/cpu/parallel.cpp"]
 CAPI = ["csrc/capi/pga_capi.cpp", "csrc/capi/comm.cpp", "csrc/capi/comm_rccl.cpp"]
 COMPAT = []
@@ -76,6 +76,9 @@ def write_ninja(opt: str, with_torch: bool) -> str:
         "  depfile = $out.d",
         "  deps = gcc",
         "  description = HIP-RDC $in",
+        "rule jitbc",
+        "  command = $hipcc $hip_flags -Xclang -disable-llvm-passes -fgpu-rdc --cuda-device-only -emit-llvm $extra -c $in -o $out",
+        "  description = HIP-BC $out",
         "rule host",
         "  command = $hipcc $host_flags $extra -MD -MF $out.d -c $in -o $out",
         "  depfile = $out.d",
@@ -164,7 +167,20 @@ def write_ninja(opt: str, with_torch: bool) -> str:
         lines.append("  ldflags = ")
         ex.append("build/bench/refsem")
 
-    defaults = ["build/libpga.so", "build/libpga.a"] + ex
+    # the hot BINARY generation kernel as LLVM bitcode, one file per variant,
+    # for linking hipRTC-compiled user objectives into it at run time (jit.cpp)
+    jit_bc = []
+    for gs in (1, 2, 4, 8, 16, 32, 64):
+        for full in (0, 1):
+            for dense in (0, 1):
+                out = f"build/jit/gen_{gs}_{full}_{dense}.bc"
+                # no depfile from a device-only bitcode compile: the headers are listed
+                hdrs = " ".join(f"csrc/include/pga/{h}.hpp" for h in ("binary_dev", "tp", "core", "device", "ops"))
+                lines.append(f"build {out}: jitbc csrc/kernels/jitgen.hip | {hdrs}")
+                lines.append(f"  extra = -DPGA_JIT_GS={gs} -DPGA_JIT_FULL={full} -DPGA_JIT_DENSE={dense}")
+                jit_bc.append(out)
+
+    defaults = ["build/libpga.so", "build/libpga.a"] + ex + jit_bc
     if with_torch:
         inc, lib, abi = torch_paths()
         tflags = " ".join(f"-isystem {p}" for p in inc + pybind_includes())
@@ -183,6 +199,7 @@ def write_ninja(opt: str, with_torch: bool) -> str:
     path = os.path.join(BUILD, "build.ninja")
     os.makedirs(os.path.join(BUILD, "obj"), exist_ok=True)
     os.makedirs(os.path.join(BUILD, "examples"), exist_ok=True)
+    os.makedirs(os.path.join(BUILD, "jit"), exist_ok=True)
     with open(path, "w") as f:
         f.write("\n".join(lines) + "\n")
     return path
