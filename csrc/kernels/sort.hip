@@ -15,7 +15,9 @@
 //            popcount below the lane, and bump the wave's LDS digit counter
 //            once per group.  Stable by construction (rounds in key order,
 //            lanes in key order, waves in key order), no atomics, no look-back
-//            chain: every workgroup of a pass is independent.
+//            chain: every workgroup of a pass is independent.  The ranked tile
+//            is staged in LDS in digit order and written out from there, so a
+//            store instruction covers consecutive addresses of one digit run.
 // The previous onesweep design (decoupled look-back over 512 tiles of 2048
 // keys, 4-bit digits) serialised on the look-back: 28 us per pass at 1M keys
 // (profiles/rank_roulette_r03.md).
@@ -139,12 +141,24 @@ __global__ __launch_bounds__(kScanBlock) void scan_chunk_kernel(uint32_t* __rest
   const uint32_t t = threadIdx.x, lane = lane_id(), wid = t >> 6;
   const uint64_t base = (uint64_t)blockIdx.x * kScanChunk + (uint64_t)t * kScanPer;
   uint32_t v[kScanPer], s = 0;
+  if (base + kScanPer <= m && (m & 3u) == 0u) {  // whole 16-byte vectors (the usual case)
 #pragma unroll
-  for (uint32_t j = 0; j < kScanPer; ++j) {
-    const uint32_t y = x[base + j < m ? base + j : m - 1];  // unconditional load
-    v[j] = base + j < m ? y : 0u;
-    s += v[j];
+    for (uint32_t j = 0; j < kScanPer; j += 4) {
+      const uint4 y = *(const uint4*)(x + base + j);
+      v[j] = y.x;
+      v[j + 1] = y.y;
+      v[j + 2] = y.z;
+      v[j + 3] = y.w;
+    }
+  } else {
+#pragma unroll
+    for (uint32_t j = 0; j < kScanPer; ++j) {
+      const uint32_t y = x[base + j < m ? base + j : m - 1];  // unconditional load
+      v[j] = base + j < m ? y : 0u;
+    }
   }
+#pragma unroll
+  for (uint32_t j = 0; j < kScanPer; ++j) s += v[j];
   uint32_t incl = s;
 #pragma unroll
   for (int o = 1; o < 64; o <<= 1) {
@@ -158,10 +172,23 @@ __global__ __launch_bounds__(kScanBlock) void scan_chunk_kernel(uint32_t* __rest
     off += w < wid ? wsum[w] : 0u;
     tot += wsum[w];
   }
+  if (base + kScanPer <= m && (m & 3u) == 0u) {
 #pragma unroll
-  for (uint32_t j = 0; j < kScanPer; ++j) {
-    if (base + j < m) x[base + j] = off;
-    off += v[j];
+    for (uint32_t j = 0; j < kScanPer; j += 4) {
+      uint4 y;
+      y.x = off;
+      y.y = y.x + v[j];
+      y.z = y.y + v[j + 1];
+      y.w = y.z + v[j + 2];
+      off = y.w + v[j + 3];
+      *(uint4*)(x + base + j) = y;
+    }
+  } else {
+#pragma unroll
+    for (uint32_t j = 0; j < kScanPer; ++j) {
+      if (base + j < m) x[base + j] = off;
+      off += v[j];
+    }
   }
   if (sums && t == 0) sums[blockIdx.x] = tot;
 }
@@ -209,24 +236,54 @@ __global__ __launch_bounds__(kBlock) void radix_scatter_kernel(KeySrc src, const
     pos[r] = ok ? c + rk : 0xFFFFFFFFu;
   }
   __syncthreads();
-  // per digit: the tile's global base plus the keys of the earlier waves
-  for (uint32_t d = threadIdx.x; d < D; d += kBlock) {
-    uint32_t o = base[(uint64_t)d * tiles + blockIdx.x];
+  // Stage the tile in LDS in digit order, then write it out in that order:
+  // consecutive lanes store consecutive addresses of a digit's output run
+  // (scattering straight from the ranking spreads one store instruction
+  // over up to 64 runs).
+  __shared__ uint32_t sk[kTile], sv[kTile];
+  __shared__ uint32_t gofs[kMaxDigits], wsum[kBlock / 64];
+  const uint32_t t = threadIdx.x, d = t;
+  uint32_t tc = 0;  // keys of digit d in the tile; cnt[w][d] becomes the waves-before offset
+  if (d < D) {
 #pragma unroll
     for (uint32_t w = 0; w < kBlock / 64; ++w) {
       const uint32_t c = cnt[w][d];
-      cnt[w][d] = o;
-      o += c;
+      cnt[w][d] = tc;
+      tc += c;
     }
+  }
+  uint32_t incl = tc;  // block exclusive scan of tc over the digits -> the digit's local start
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = (uint32_t)__shfl_up((int)incl, o, 64);
+    if (lane >= (uint32_t)o) incl += y;
+  }
+  if (lane == 63) wsum[wid] = incl;
+  __syncthreads();
+  uint32_t ls = incl - tc;
+  for (uint32_t w = 0; w < wid; ++w) ls += wsum[w];
+  if (d < D) {
+#pragma unroll
+    for (uint32_t w = 0; w < kBlock / 64; ++w) cnt[w][d] += ls;  // local start of (wave w, digit d)
+    gofs[d] = base[(uint64_t)d * tiles + blockIdx.x] - ls;       // output index = gofs[d] + local index
   }
   __syncthreads();
 #pragma unroll
   for (uint32_t r = 0; r < kRounds; ++r) {
     if (pos[r] != 0xFFFFFFFFu) {
-      const uint32_t p = cnt[wid][(key[r] >> shift) & (D - 1)] + pos[r];
-      if (kout) kout[p] = key[r];
-      vout[p] = val[r];
+      const uint32_t lp = cnt[wid][(key[r] >> shift) & (D - 1)] + pos[r];
+      sk[lp] = key[r];
+      sv[lp] = val[r];
     }
+  }
+  __syncthreads();
+  const uint64_t t0 = (uint64_t)blockIdx.x * kTile;
+  const uint32_t nt = (uint32_t)(n - t0 < kTile ? n - t0 : kTile);
+  for (uint32_t i = t; i < nt; i += kBlock) {
+    const uint32_t k = sk[i];
+    const uint32_t o = gofs[(k >> shift) & (D - 1)] + i;
+    if (kout) kout[o] = k;
+    vout[o] = sv[i];
   }
 }
 
