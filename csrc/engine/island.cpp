@@ -367,13 +367,24 @@ void Island::prepare_generation() {
   if (real_qk()) {
     // the current generation's score range (fused partials when its kernel
     // stored them), and its quantized keys if anything rewrote the scores
-    if (!qk_ws_.ptr) qk_ws_ = alloc(4ull * (4 + 3 * 1024));
+    if (!qk_ws_.ptr) {
+      qk_ws_ = alloc(4ull * (4 + 3 * 1024));
+      qk_age_ = 0;
+    }
     const float* sc = (const float*)scores_[cur_].ptr;
-    if (stats_ok_[cur_])
-      stats_from_parts_launch((const float*)stats_parts_[cur_].ptr, (const unsigned long long*)best_[cur_].ptr,
-                              n_best_[cur_], cfg_.S, (float*)qk_ws_.ptr, stream);
-    else
-      score_stats_launch(sc, cfg_.S, (float*)qk_ws_.ptr, stream);
+    // The quantization range only has to be the same for every key of a
+    // generation: keys are monotonic in the score and equal keys fall back to
+    // the exact f32 compare, so any range gives the same tournaments.  It is
+    // refreshed every kQkRefresh generations (a stale range only costs more
+    // ties), not every generation: small populations are launch-bound.
+    constexpr uint32_t kQkRefresh = 8;
+    if (qk_age_++ % kQkRefresh == 0) {
+      if (stats_ok_[cur_])
+        stats_from_parts_launch((const float*)stats_parts_[cur_].ptr, (const unsigned long long*)best_[cur_].ptr,
+                                n_best_[cur_], cfg_.S, (float*)qk_ws_.ptr, stream);
+      else
+        score_stats_launch(sc, cfg_.S, (float*)qk_ws_.ptr, stream);
+    }
     if (!qk_valid_[cur_]) {
       scores_to_qkeys_launch(sc, cfg_.S, (const float*)qk_ws_.ptr, (uint16_t*)keys_[cur_].ptr, stream);
       qk_valid_[cur_] = true;

@@ -244,6 +244,7 @@ class Island {
   // JIT evaluation of `n` rows at `rows` -> scores, block bests -> parts; returns the grid
   uint32_t jit_eval(const void* rows, float* scores, uint64_t n, unsigned long long* parts);
   bool fused_jit_generation(GenArgs& a);
+  uint32_t qk_age_ = 0;  // REAL quantized keys: generations since the range was refreshed
   bool jit_fused_off_ = false;
   uint64_t jit_fused_gens_ = 0;
   u32x4 last_mask_{0, 0, 0, 0};
