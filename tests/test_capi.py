@@ -70,6 +70,9 @@ def lib():
     L.pga_set_migration_policy.argtypes = [vp, vp, C.c_int]
     L.pga_run_islands_until.argtypes = [vp, C.c_uint, C.c_uint, C.c_float, C.c_float]
     L.pga_set_stats_history.argtypes = [vp, vp, C.c_int]
+    L.pga_set_batch_islands.argtypes = [vp, C.c_int]
+    L.pga_batched_generations.restype = C.c_ulonglong
+    L.pga_batched_generations.argtypes = [vp]
     L.pga_get_stats_history.restype = C.c_long
     L.pga_get_stats_history.argtypes = [vp, vp, C.POINTER(C.c_float), C.c_ulong]
     L.free_ = C.CDLL(None).free
@@ -345,3 +348,32 @@ def test_objective_source_gpu(lib):
         best.append(list(scores))
         lib.pga_deinit(p)
     assert best[0] == best[1]
+
+
+@pytest.mark.gpu
+def test_run_islands_batched_launch_matches_streams(lib):
+    """pga_run_islands: same-shape BINARY populations run as ONE launch per
+    generation (island = grid y) and evolve exactly as on their own streams."""
+    def run(batched):
+        p = lib.pga_init_device(0)
+        lib.pga_set_seed(p, 5)
+        lib.pga_set_quiet(p, 1)
+        lib.pga_set_abort_on_error(p, 0)
+        assert lib.pga_set_batch_islands(p, batched) == 0
+        pops = [lib.pga_create_population_ext(p, 4096, 256, PGA_BINARY) for _ in range(4)]
+        for pop in pops:
+            assert lib.pga_set_objective_builtin(p, pop, 1, None, 0, None, 0, 0, 0.0, 0.0) == 0
+        lib.pga_run_islands(p, 25, 5, 0.02)
+        out = []
+        for pop in pops:
+            sc = (C.c_float * 4096)()
+            lib.pga_get_scores(p, pop, sc)
+            out.append(list(sc))
+        n = lib.pga_batched_generations(p)
+        lib.pga_deinit(p)
+        return out, n
+
+    a, na = run(1)
+    b, nb = run(0)
+    assert na == 25 and nb == 0
+    assert a == b
