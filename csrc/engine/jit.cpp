@@ -323,7 +323,9 @@ hipFunction_t JitKernel::gen_function(int device, uint32_t gs, bool full, bool d
     const std::string cc = "'" + rocm + "/bin/hipcc' -x hip --offload-arch=gfx950 -O3 -Xclang -disable-llvm-passes "
                            "-std=c++17 -ffp-contract=fast -fgpu-rdc --cuda-device-only -emit-llvm -c '" + base +
                            ".hip' -o '" + base + ".bc'";
-    const std::string ld = "'" + rocm + "/lib/llvm/bin/clang' --target=amdgcn-amd-amdhsa -mcpu=gfx950 -O3 '" + kbc +
+    // -flto: one LTO module, so the objective inlines into the kernel (without
+    // it each bitcode is compiled on its own and the objective is a call)
+    const std::string ld = "'" + rocm + "/lib/llvm/bin/clang' --target=amdgcn-amd-amdhsa -mcpu=gfx950 -O3 -flto '" + kbc +
                            "' '" + base + ".bc' -o '" + tmp + "' && mv '" + tmp + "' '" + co + "'";
     if (spawn_shell(cc, log) != 0) return fail("compiling the objective to bitcode failed:\n" + read_text(log));
     if (spawn_shell(ld, log) != 0) return fail("linking the fused generation kernel failed:\n" + read_text(log));

@@ -33,6 +33,9 @@ namespace {
 
 using namespace dev;
 
+#ifndef PGA_JIT_WAVES
+#define PGA_JIT_WAVES 4  // the fused-JIT variant's waves/SIMD (jitgen.hip): 107.2 us vs 111.9 at 5 (2 spills)
+#endif
 constexpr int kObjJit = 1001;  // launcher-only objective id: the linked user objective (jitgen.hip)
 
 // per-lane objective accumulator over the chunks a lane owns
@@ -798,7 +801,7 @@ __device__ __forceinline__ void binary_gen_tp_body(GenArgs a, unsigned long long
 }
 
 template <int GS, int OBJ, bool FULL, bool DENSE>
-__global__ __launch_bounds__(kBlock, (OBJ == kObjKnapMfma || OBJ == kObjJit) ? 4 : PGA_TP_WAVES) void binary_gen_tp(GenArgs a, unsigned long long* best_parts) {
+__global__ __launch_bounds__(kBlock, OBJ == kObjKnapMfma ? 4 : (OBJ == kObjJit ? PGA_JIT_WAVES : PGA_TP_WAVES)) void binary_gen_tp(GenArgs a, unsigned long long* best_parts) {
   binary_gen_tp_body<GS, OBJ, FULL, DENSE>(a, best_parts);
 }
 
