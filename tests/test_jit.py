@@ -114,3 +114,19 @@ def test_jit_rastrigin_and_tsp_match_oracles():
     ref = M.TSP(d).reference_fitness(t.genomes())
     assert torch.allclose(ref, t.scores, rtol=1e-4, atol=1e-3)
     assert t.best_score() > t0
+
+
+@pytest.mark.gpu
+def test_jit_fusion_unavailable_falls_back(monkeypatch):
+    # no generation-kernel bitcode: the island says why and evaluates with the
+    # separate hipRTC pass instead, with the same results
+    monkeypatch.setenv("PGA_JIT_DIR", "/nonexistent/pga_jit")
+    L, S = 512, 1 << 13
+    a = pga.GeneticAlgorithm(M.OneMax(L), S, seed=9, device="cuda:0", elitism=1)
+    b = pga.GeneticAlgorithm(onemax_jit(L), S, seed=9, device="cuda:0", elitism=1)
+    a.run(6)
+    b.run(6)
+    torch.cuda.synchronize()
+    assert b.island.jit_fused_generations == 0
+    assert "no generation-kernel bitcode" in b.island.jit_fused_error
+    assert torch.equal(a.rows, b.rows) and torch.equal(a.scores, b.scores)
