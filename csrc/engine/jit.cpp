@@ -283,19 +283,14 @@ std::string read_text(const std::string& path) {
 // process where another HIP runtime is already loaded (PyTorch bundles its own
 // HIP / COMGR) hipRTC links with that older LLVM, which cannot read bitcode
 // from this build's compiler.
-hipFunction_t JitKernel::gen_function(int device, uint32_t gs, bool full, bool dense, uint32_t L) {
-  if (encoding != ENC_BINARY || fused_failed_ || device < 0) return nullptr;
-  const uint64_t key = ((uint64_t)L << 8) | (gs * 4u + (full ? 2u : 0u) + (dense ? 1u : 0u));
-  for (const GenVariant& v : gen_)
-    if (v.device == device && v.key == key) return v.fn;
-  auto fail = [&](const std::string& why) -> hipFunction_t {
-    fused_failed_ = true;
-    fused_error_ = why;
-    return nullptr;
-  };
+std::string JitKernel::build_gen_object(uint32_t gs, bool full, bool dense, uint32_t L) {
+  if (encoding != ENC_BINARY) throw std::invalid_argument("fused generation kernels are BINARY only");
+  if (gs == 0 || gs > 64 || (gs & (gs - 1)) != 0) throw std::invalid_argument("group size must be a power of two <= 64");
   const std::string variant = std::to_string(gs) + "_" + (full ? "1" : "0") + "_" + (dense ? "1" : "0");
   const std::string kbc = jit_bitcode_dir() + "/gen_" + variant + ".bc";
-  if (read_file(kbc).empty()) return fail("no generation-kernel bitcode at " + kbc + " (tools/build.py builds it)");
+  const std::string kbc_text = read_text(kbc);
+  if (kbc_text.empty())
+    throw std::runtime_error("no generation-kernel bitcode at " + kbc + " (tools/build.py builds it)");
   const char* rp = std::getenv("ROCM_PATH");
   const std::string rocm = rp && *rp ? rp : "/opt/rocm";
   // the user's source + the external-linkage entry the kernel bitcode calls:
@@ -306,31 +301,51 @@ hipFunction_t JitKernel::gen_function(int device, uint32_t gs, bool full, bool d
                           "extern \"C\" __device__ float pga_user_objective(__attribute__((address_space(1))) "
                           "const unsigned int* w, unsigned int, const float* d) { return " + name +
                           "((const unsigned int*)w, " + std::to_string(L) + "u, d); }\n";
-  const std::string h = std::to_string(std::hash<std::string>{}(src + "|" + read_text(kbc)));
+  const std::string h = std::to_string(std::hash<std::string>{}(src + "|" + kbc_text));
   const std::string dir = jit_cache_dir();
   const std::string base = dir + "/obj_" + h;
   const std::string co = base + "_" + variant + ".co", log = base + "_" + variant + ".log";
-  std::vector<char> image = read_file(co);
-  if (image.empty()) {
-    if (spawn_shell("mkdir -p '" + dir + "'", "/dev/null") != 0) return fail("cannot create " + dir);
-    const std::string tmp = co + ".tmp" + std::to_string((unsigned)getpid());
-    FILE* f = std::fopen((base + ".hip").c_str(), "wb");
-    if (!f) return fail("cannot write " + base + ".hip");
-    std::fwrite(src.data(), 1, src.size(), f);
-    std::fclose(f);
-    // unoptimised bitcode on both sides: the link optimises the whole kernel
-    // once, with the objective inlined (optimising twice costs registers)
-    const std::string cc = "'" + rocm + "/bin/hipcc' -x hip --offload-arch=gfx950 -O3 -Xclang -disable-llvm-passes "
-                           "-std=c++17 -ffp-contract=fast -fgpu-rdc --cuda-device-only -emit-llvm -c '" + base +
-                           ".hip' -o '" + base + ".bc'";
-    // -flto: one LTO module, so the objective inlines into the kernel (without
-    // it each bitcode is compiled on its own and the objective is a call)
-    const std::string ld = "'" + rocm + "/lib/llvm/bin/clang' --target=amdgcn-amd-amdhsa -mcpu=gfx950 -O3 -flto '" + kbc +
-                           "' '" + base + ".bc' -o '" + tmp + "' && mv '" + tmp + "' '" + co + "'";
-    if (spawn_shell(cc, log) != 0) return fail("compiling the objective to bitcode failed:\n" + read_text(log));
-    if (spawn_shell(ld, log) != 0) return fail("linking the fused generation kernel failed:\n" + read_text(log));
-    image = read_file(co);
-    if (image.empty()) return fail("the linker produced no code object: " + co);
+  if (!read_file(co).empty()) return co;
+  if (spawn_shell("mkdir -p '" + dir + "'", "/dev/null") != 0) throw std::runtime_error("cannot create " + dir);
+  // per-process intermediates; the code object appears atomically (rename),
+  // so concurrent processes compiling the same objective never see a partial one
+  const std::string pid = std::to_string((unsigned)getpid());
+  const std::string tmp = co + ".tmp" + pid, work = base + "_" + variant + "_" + pid;
+  FILE* f = std::fopen((work + ".hip").c_str(), "wb");
+  if (!f) throw std::runtime_error("cannot write " + work + ".hip");
+  std::fwrite(src.data(), 1, src.size(), f);
+  std::fclose(f);
+  // unoptimised bitcode on both sides: the link optimises the whole kernel
+  // once, with the objective inlined (optimising twice costs registers)
+  const std::string cc = "'" + rocm + "/bin/hipcc' -x hip --offload-arch=gfx950 -O3 -Xclang -disable-llvm-passes "
+                         "-std=c++17 -ffp-contract=fast -fgpu-rdc --cuda-device-only -emit-llvm -c '" + work +
+                         ".hip' -o '" + work + ".bc'";
+  // -flto: one LTO module, so the objective inlines into the kernel (without
+  // it each bitcode is compiled on its own and the objective is a call)
+  const std::string ld = "'" + rocm + "/lib/llvm/bin/clang' --target=amdgcn-amd-amdhsa -mcpu=gfx950 -O3 -flto '" + kbc +
+                         "' '" + work + ".bc' -o '" + tmp + "' && mv '" + tmp + "' '" + co + "'";
+  const bool ok_cc = spawn_shell(cc, log) == 0;
+  const bool ok_ld = ok_cc && spawn_shell(ld, log) == 0;
+  (void)std::remove((work + ".hip").c_str());
+  (void)std::remove((work + ".bc").c_str());
+  if (!ok_cc) throw std::runtime_error("compiling the objective to bitcode failed:\n" + read_text(log));
+  if (!ok_ld) throw std::runtime_error("linking the fused generation kernel failed:\n" + read_text(log));
+  if (read_file(co).empty()) throw std::runtime_error("the linker produced no code object: " + co);
+  return co;
+}
+
+hipFunction_t JitKernel::gen_function(int device, uint32_t gs, bool full, bool dense, uint32_t L) {
+  if (encoding != ENC_BINARY || fused_failed_ || device < 0) return nullptr;
+  const uint64_t key = ((uint64_t)L << 8) | (gs * 4u + (full ? 2u : 0u) + (dense ? 1u : 0u));
+  for (const GenVariant& v : gen_)
+    if (v.device == device && v.key == key) return v.fn;
+  std::vector<char> image;
+  try {
+    image = read_file(build_gen_object(gs, full, dense, L));
+  } catch (const std::exception& e) {
+    fused_failed_ = true;
+    fused_error_ = e.what();
+    return nullptr;
   }
   PGA_HIP_CHECK(hipSetDevice(device));
   GenVariant v{device, key, nullptr, nullptr, 1, std::make_shared<std::vector<char>>(std::move(image))};
@@ -338,7 +353,9 @@ hipFunction_t JitKernel::gen_function(int device, uint32_t gs, bool full, bool d
   if (e == hipSuccess) e = hipModuleGetFunction(&v.fn, v.mod, gen_symbol(gs, full, dense).c_str());
   if (e != hipSuccess) {
     if (v.mod) (void)hipModuleUnload(v.mod);
-    return fail(std::string("loading the fused generation kernel: ") + hipGetErrorString(e));
+    fused_failed_ = true;
+    fused_error_ = std::string("loading the fused generation kernel: ") + hipGetErrorString(e);
+    return nullptr;
   }
   int occ = 0;
   if (hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&occ, v.fn, 256, 0) != hipSuccess || occ <= 0) occ = 1;

@@ -47,6 +47,9 @@ class JitKernel {
   // a link error: fused_error() says why) — the caller falls back to
   // generation + eval().
   hipFunction_t gen_function(int device, uint32_t gs, bool full, bool dense, uint32_t L);
+  // the linked code object of one variant (compiled / LTO-linked on first use,
+  // cached on disk; no GPU needed): its path.  Throws with the toolchain log.
+  std::string build_gen_object(uint32_t gs, bool full, bool dense, uint32_t L);
   // launches one fused generation; returns the grid (= best partials written)
   uint32_t gen_launch(hipFunction_t f, const void* args, size_t args_bytes, uint64_t S, unsigned long long* parts,
                       uint32_t max_grid, hipStream_t s);

@@ -98,7 +98,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def_readonly("name", &pga::JitKernel::name)
       .def_readonly("source", &pga::JitKernel::source)
       .def_readonly("log", &pga::JitKernel::log)
-      .def_property_readonly("code_size", [](const pga::JitKernel& k) { return k.code.size(); });
+      .def_property_readonly("code_size", [](const pga::JitKernel& k) { return k.code.size(); })
+      .def("build_generation_object", &pga::JitKernel::build_gen_object, py::arg("group_size"), py::arg("full"),
+           py::arg("dense"), py::arg("length"));
   m.def("jit_compile", &pga::jit_compile, py::arg("encoding"), py::arg("source"), py::arg("name"),
         py::arg("options") = std::vector<std::string>{}, py::call_guard<py::gil_scoped_release>());
   m.def("jit_kernel_source", &pga::jit_kernel_source);

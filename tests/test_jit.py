@@ -42,6 +42,21 @@ def test_jit_compiles_and_reports_errors():
         M.JitObjective("real", 4, "not c++", name="f").kernel()
 
 
+def test_jit_fused_generation_object_builds_without_gpu(tmp_path, monkeypatch):
+    # the fused-JIT toolchain path (user bitcode + jitgen.hip bitcode, LTO link)
+    # needs no GPU: the code object holds the kernel with the objective inlined
+    monkeypatch.setenv("PGA_JIT_CACHE", str(tmp_path))
+    k = onemax_jit(1024).kernel()
+    path = k.build_generation_object(8, True, False, 1024)
+    data = open(path, "rb").read()
+    assert data[:4] == b"\x7fELF"
+    assert b"_ZN3pga6jitgen13binary_gen_tpILi8ELi1001ELb1ELb0EEEvNS_7GenArgsEPy" in data
+    assert b"pga_user_objective" not in data  # inlined, no call left
+    assert k.build_generation_object(8, True, False, 1024) == path  # cached
+    with pytest.raises(ValueError, match="power of two"):
+        k.build_generation_object(3, True, False, 1024)
+
+
 def test_jit_cpu_uses_fallback():
     ga = pga.GeneticAlgorithm(onemax_jit(96), 200, seed=1, device="cpu")
     assert torch.equal(ga.scores, ga.genomes().float().sum(-1))
