@@ -395,3 +395,20 @@ def test_stripe_migration_gpu(S, k, prob):
     g.run(2)
     c.run(2)  # keys of the replaced individuals follow their scores
     same(g, c)
+
+
+@pytest.mark.gpu
+def test_rank_selection_u16_keys_partial_tile_bitexact():
+    """OneMax rank selection sorts the u16 tournament keys (2 passes, 6 + 5
+    bits for L = 1024) over a population that is not a multiple of the
+    4096-key tile: children equal the CPU backend's."""
+    p = pga.models.OneMax(1024)
+    kw = dict(seed=13, elitism=1, selection="rank")
+    g = pga.GeneticAlgorithm(p, 70_001, device="cuda:0", **kw)
+    c = pga.GeneticAlgorithm(p, 70_001, device="cpu", **kw)
+    for _ in range(3):
+        g.run(1)
+        c.run(1)
+        torch.cuda.synchronize()
+        assert torch.equal(g.rows.cpu(), c.rows)
+        assert torch.equal(g.scores.cpu(), c.scores)

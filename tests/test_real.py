@@ -271,3 +271,13 @@ def test_cpu_sparse_mutation_rate():
     changed = sum(1 for x in after.flatten().tolist() if x not in vals)
     mean = changed / 4000
     assert 0.9 < mean < 1.1  # E[K] = L p = 1
+
+
+@pytest.mark.gpu
+def test_gpu_rank_order_large_population_bitexact():
+    """Linear ranking on f32 scores at S = 300,007: the native radix sort runs
+    4 passes of 8-bit digits over 74 tiles (a (digit, tile) table of 18,944
+    entries: the two-level scan) and a partial last tile; the rank order, hence
+    every child, equals the CPU backend's stable sort."""
+    _exact_pair(M.Rosenbrock(30), 300_007, 2, seed=8, elitism=1, selection="rank", crossover="two_point",
+                mutation="gaussian")
