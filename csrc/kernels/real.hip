@@ -26,6 +26,8 @@
 // crossover / mutate kernels (src/pga.cu:250-347) become one launch.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include "pga/device.hpp"
 #include "pga/ops.hpp"
 #include "pga/real_ops.hpp"
@@ -814,8 +816,20 @@ uint32_t go_tp(K kernel, const GenArgs& a, unsigned long long* parts, hipStream_
   return grid;
 }
 
+// Below ~192 children per CU the transposed kernel has too few waves (one
+// 64-child batch each) to hide its GS dependent breed steps and the generic
+// kernel is faster (bench/real_size_sweep.py: SumGenes-100 at S = 40,000
+// 39.4 vs 35.3 us, Rastrigin-30 24.3 vs 20.9 us; from S = 100,000 the
+// transposed kernel wins, 43 vs 75 and 28 vs 39 us).  PGA_TP_MIN_S overrides
+// (the tests pin 0 to cover the transposed kernel at small sizes).
+uint64_t real_tp_min_population() {
+  if (const char* e = std::getenv("PGA_TP_MIN_S")) return std::strtoull(e, nullptr, 10);
+  return 192ull * (uint64_t)device_cu_count();
+}
+
 bool real_tp_eligible(const GenArgs& a, uint32_t GS, bool rot) {
   if (force_generic_kernels()) return false;
+  if (a.S < real_tp_min_population()) return false;
   if (a.objective == OBJ_USER_FNPTR || a.objective == OBJ_TSP_RANDOM_KEY) return false;
   if (rot && GS != 4 && GS != 8) return false;
   const bool sel_ok = (a.selection == SEL_TOURNAMENT && a.tour_k == 2) || a.selection == SEL_RANDOM ||

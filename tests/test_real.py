@@ -137,6 +137,14 @@ EXACT = {
 }
 
 
+@pytest.fixture(autouse=True)
+def _transposed_kernel_at_every_size(monkeypatch):
+    # the engine routes small REAL populations to the generic kernel
+    # (real_tp_min_population); the bit-exact tests below cover the transposed
+    # kernel at small sizes too
+    monkeypatch.setenv("PGA_TP_MIN_S", "0")
+
+
 def _exact_pair(p, S, gens, **kw):
     g = pga.GeneticAlgorithm(p, S, device="cuda:0", **kw)
     c = pga.GeneticAlgorithm(p, S, device="cpu", **kw)
@@ -281,3 +289,12 @@ def test_gpu_rank_order_large_population_bitexact():
     every child, equals the CPU backend's stable sort."""
     _exact_pair(M.Rosenbrock(30), 300_007, 2, seed=8, elitism=1, selection="rank", crossover="two_point",
                 mutation="gaussian")
+
+
+@pytest.mark.gpu
+def test_gpu_small_population_generic_route_bitexact(monkeypatch):
+    """The default route of a small REAL population (generic kernel) gives the
+    CPU backend's children too."""
+    monkeypatch.delenv("PGA_TP_MIN_S", raising=False)
+    _exact_pair(M.Sphere(30), 3000, 3, seed=31, elitism=1, crossover="blend", mutation="gaussian")
+    _exact_pair(M.SumGenes(100), 3000, 2, seed=32, crossover="uniform", mutation="reset_one")
