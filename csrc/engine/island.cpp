@@ -775,9 +775,11 @@ bool Island::fused_jit_generation(GenArgs& a) {
   uint32_t gs = 0;
   bool full = false, dense = false;
   if (!binary_tp_plan(a, gs, full, dense)) return false;
-  hipFunction_t f = jit_->gen_function(device_, gs, full, dense, cfg_.L);
+  // no compile / module load inside a graph capture: there only a variant
+  // loaded by an earlier plain generation is used
+  hipFunction_t f = jit_->gen_function(device_, gs, full, dense, cfg_.L, !capturing_);
   if (!f) {
-    jit_fused_off_ = true;  // fall back to generation + evaluation pass (jit_->fused_error() says why)
+    if (!capturing_) jit_fused_off_ = true;  // fall back to generation + evaluation pass (fused_error() says why)
     return false;
   }
   TraceRange tr("pga.jit_generation", 2);

@@ -334,11 +334,12 @@ std::string JitKernel::build_gen_object(uint32_t gs, bool full, bool dense, uint
   return co;
 }
 
-hipFunction_t JitKernel::gen_function(int device, uint32_t gs, bool full, bool dense, uint32_t L) {
+hipFunction_t JitKernel::gen_function(int device, uint32_t gs, bool full, bool dense, uint32_t L, bool build) {
   if (encoding != ENC_BINARY || fused_failed_ || device < 0) return nullptr;
   const uint64_t key = ((uint64_t)L << 8) | (gs * 4u + (full ? 2u : 0u) + (dense ? 1u : 0u));
   for (const GenVariant& v : gen_)
     if (v.device == device && v.key == key) return v.fn;
+  if (!build) return nullptr;
   std::vector<char> image;
   try {
     image = read_file(build_gen_object(gs, full, dense, L));

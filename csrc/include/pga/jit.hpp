@@ -46,7 +46,9 @@ class JitKernel {
   // nullptr when fusion is unavailable (another encoding, no kernel bitcode,
   // a link error: fused_error() says why) — the caller falls back to
   // generation + eval().
-  hipFunction_t gen_function(int device, uint32_t gs, bool full, bool dense, uint32_t L);
+  // build = false: only an already loaded variant (nothing is compiled or
+  // loaded, e.g. while a stream is being captured into a graph)
+  hipFunction_t gen_function(int device, uint32_t gs, bool full, bool dense, uint32_t L, bool build = true);
   // the linked code object of one variant (compiled / LTO-linked on first use,
   // cached on disk; no GPU needed): its path.  Throws with the toolchain log.
   std::string build_gen_object(uint32_t gs, bool full, bool dense, uint32_t L);

@@ -14,6 +14,14 @@ CASES = {
     "rastrigin_rot": (lambda: M.Rastrigin(20, rotate=True, seed=2), 4000, dict(elitism=1)),
     "sum_refops": (lambda: M.SumGenes(100), 40000, {}),
     "tsp_ox": (lambda: M.TSP(torch.rand(40, 40, generator=torch.Generator().manual_seed(1))), 2000, dict(elitism=1)),
+    # a source objective fused into the generation kernel: the variant loaded by
+    # the first plain generations is replayed inside the graph
+    "onemax_jit_fused": (lambda: M.JitObjective("binary", 256, """
+__device__ float ones(const unsigned int* w, unsigned int nbits, const float* data) {
+  float s = 0.f;
+  for (unsigned int i = 0; i < (nbits + 31) / 32; ++i) s += (float)__popc(w[i]);
+  return s;
+}""", name="ones"), 5000, dict(elitism=1)),
 }
 
 
