@@ -37,6 +37,10 @@ using namespace dev;
 
 constexpr uint32_t kMaxDigitBits = 8;
 constexpr uint32_t kMaxDigits = 1u << kMaxDigitBits;
+// single-pass mode for small key ranges (u16 keys of integer objectives,
+// key_range <= 2048): the digit is the whole key, D = key_range digits
+constexpr uint32_t kWideBits = 11;
+constexpr uint32_t kWideDigits = 1u << kWideBits;
 constexpr uint32_t kWaveKeys = 1024;                   // per wave: 16 rounds of 64
 constexpr uint32_t kRounds = kWaveKeys / 64;
 constexpr uint32_t kTile = kWaveKeys * (kBlock / 64);  // 4096 keys per workgroup
@@ -56,7 +60,7 @@ struct RadixWs {
 };
 
 RadixWs radix_ws(void* ws, uint64_t n) {
-  const uint64_t entries = (uint64_t)kMaxDigits * tiles_of(n);
+  const uint64_t entries = (uint64_t)kWideDigits * tiles_of(n);
   const uint64_t chunks = (entries + kScanChunk - 1) / kScanChunk;
   char* p = (char*)ws;
   RadixWs w;
@@ -107,11 +111,11 @@ __device__ __forceinline__ uint64_t match_digit(uint32_t dig, bool ok, uint32_t 
 // Per-tile digit counts (order-independent): one LDS atomic per group of
 // lanes sharing a digit (a skewed key distribution would otherwise serialise
 // up to 64 same-address atomics per instruction).
-template <int SRC>
+template <int SRC, uint32_t MAXD>
 __global__ __launch_bounds__(kBlock) void radix_count_kernel(KeySrc src, uint64_t n, uint32_t shift, uint32_t bits,
-                                                             uint64_t tiles, uint32_t* __restrict__ counts) {
-  __shared__ uint32_t h[kMaxDigits];
-  const uint32_t D = 1u << bits;
+                                                             uint32_t D, uint64_t tiles, uint32_t* __restrict__ counts) {
+  __shared__ uint32_t h[MAXD];
+  const uint32_t mask = (1u << bits) - 1u;
   for (uint32_t d = threadIdx.x; d < D; d += kBlock) h[d] = 0;
   __syncthreads();
   const uint64_t t0 = (uint64_t)blockIdx.x * kTile;
@@ -120,7 +124,7 @@ __global__ __launch_bounds__(kBlock) void radix_count_kernel(KeySrc src, uint64_
 #pragma unroll
   for (uint32_t i = 0; i < kTile / kBlock; ++i) {  // all loads first
     const uint64_t e = t0 + (uint64_t)i * kBlock + threadIdx.x;
-    const uint32_t d = (load_key<SRC>(src, e < n ? e : n - 1) >> shift) & (D - 1);  // unconditional load
+    const uint32_t d = min((load_key<SRC>(src, e < n ? e : n - 1) >> shift) & mask, D - 1);  // unconditional load
     dig[i] = e < n ? d : D;
   }
 #pragma unroll
@@ -201,13 +205,13 @@ __global__ __launch_bounds__(kBlock) void scan_add_kernel(uint32_t* __restrict__
 
 // Scatter one tile stably by digit.  Thread layout: wave w owns keys
 // [t0 + w * 1024, t0 + (w + 1) * 1024), round r lane l is key w * 1024 + r * 64 + l.
-template <int SRC, int VAL>  // VAL: 0 = the key's index, 1 = src.vals, 2 = vin
+template <int SRC, int VAL, uint32_t MAXD>  // VAL: 0 = the key's index, 1 = src.vals, 2 = vin
 __global__ __launch_bounds__(kBlock) void radix_scatter_kernel(KeySrc src, const uint32_t* __restrict__ vin, uint64_t n,
-                                                               uint32_t shift, uint32_t bits, uint64_t tiles,
+                                                               uint32_t shift, uint32_t bits, uint32_t D, uint64_t tiles,
                                                                const uint32_t* __restrict__ base,
                                                                uint32_t* __restrict__ kout, uint32_t* __restrict__ vout) {
-  __shared__ uint32_t cnt[kBlock / 64][kMaxDigits];  // per wave: running digit counts, then output bases
-  const uint32_t D = 1u << bits;
+  __shared__ uint32_t cnt[kBlock / 64][MAXD];  // per wave: running digit counts, then output bases
+  const uint32_t mask = (1u << bits) - 1u;
   const uint32_t lane = lane_id(), wid = threadIdx.x >> 6;
   for (uint32_t d = lane; d < D; d += 64) cnt[wid][d] = 0;
   const uint64_t w0 = (uint64_t)blockIdx.x * kTile + (uint64_t)wid * kWaveKeys;
@@ -224,7 +228,7 @@ __global__ __launch_bounds__(kBlock) void radix_scatter_kernel(KeySrc src, const
 #pragma unroll
   for (uint32_t r = 0; r < kRounds; ++r) {
     const bool ok = w0 + r * 64u + lane < n;
-    const uint32_t dig = ok ? (key[r] >> shift) & (D - 1) : D;
+    const uint32_t dig = ok ? min((key[r] >> shift) & mask, D - 1) : D;
     const uint64_t peers = match_digit(dig, ok, bits);
     const uint32_t rk = (uint32_t)__popcll(peers & below);
     // every lane of a group reads the counter, then the group's first lane bumps
@@ -241,18 +245,26 @@ __global__ __launch_bounds__(kBlock) void radix_scatter_kernel(KeySrc src, const
   // (scattering straight from the ranking spreads one store instruction
   // over up to 64 runs).
   __shared__ uint32_t sk[kTile], sv[kTile];
-  __shared__ uint32_t gofs[kMaxDigits], wsum[kBlock / 64];
-  const uint32_t t = threadIdx.x, d = t;
-  uint32_t tc = 0;  // keys of digit d in the tile; cnt[w][d] becomes the waves-before offset
-  if (d < D) {
+  __shared__ uint32_t gofs[MAXD], wsum[kBlock / 64];
+  constexpr uint32_t P = MAXD / kBlock;  // digits per thread: [t P, t P + P)
+  const uint32_t t = threadIdx.x;
+  uint32_t tcs[P], tsum = 0;  // keys of each digit in the tile; cnt[w][d] becomes the waves-before offset
 #pragma unroll
-    for (uint32_t w = 0; w < kBlock / 64; ++w) {
-      const uint32_t c = cnt[w][d];
-      cnt[w][d] = tc;
-      tc += c;
+  for (uint32_t j = 0; j < P; ++j) {
+    const uint32_t d = t * P + j;
+    uint32_t tc = 0;
+    if (d < D) {
+#pragma unroll
+      for (uint32_t w = 0; w < kBlock / 64; ++w) {
+        const uint32_t c = cnt[w][d];
+        cnt[w][d] = tc;
+        tc += c;
+      }
     }
+    tcs[j] = tc;
+    tsum += tc;
   }
-  uint32_t incl = tc;  // block exclusive scan of tc over the digits -> the digit's local start
+  uint32_t incl = tsum;  // block exclusive scan over the threads' digit ranges -> local digit starts
 #pragma unroll
   for (int o = 1; o < 64; o <<= 1) {
     const uint32_t y = (uint32_t)__shfl_up((int)incl, o, 64);
@@ -260,18 +272,23 @@ __global__ __launch_bounds__(kBlock) void radix_scatter_kernel(KeySrc src, const
   }
   if (lane == 63) wsum[wid] = incl;
   __syncthreads();
-  uint32_t ls = incl - tc;
+  uint32_t ls = incl - tsum;
   for (uint32_t w = 0; w < wid; ++w) ls += wsum[w];
-  if (d < D) {
 #pragma unroll
-    for (uint32_t w = 0; w < kBlock / 64; ++w) cnt[w][d] += ls;  // local start of (wave w, digit d)
-    gofs[d] = base[(uint64_t)d * tiles + blockIdx.x] - ls;       // output index = gofs[d] + local index
+  for (uint32_t j = 0; j < P; ++j) {
+    const uint32_t d = t * P + j;
+    if (d < D) {
+#pragma unroll
+      for (uint32_t w = 0; w < kBlock / 64; ++w) cnt[w][d] += ls;  // local start of (wave w, digit d)
+      gofs[d] = base[(uint64_t)d * tiles + blockIdx.x] - ls;       // output index = gofs[d] + local index
+    }
+    ls += tcs[j];
   }
   __syncthreads();
 #pragma unroll
   for (uint32_t r = 0; r < kRounds; ++r) {
     if (pos[r] != 0xFFFFFFFFu) {
-      const uint32_t lp = cnt[wid][(key[r] >> shift) & (D - 1)] + pos[r];
+      const uint32_t lp = cnt[wid][min((key[r] >> shift) & mask, D - 1)] + pos[r];
       sk[lp] = key[r];
       sv[lp] = val[r];
     }
@@ -281,7 +298,7 @@ __global__ __launch_bounds__(kBlock) void radix_scatter_kernel(KeySrc src, const
   const uint32_t nt = (uint32_t)(n - t0 < kTile ? n - t0 : kTile);
   for (uint32_t i = t; i < nt; i += kBlock) {
     const uint32_t k = sk[i];
-    const uint32_t o = gofs[(k >> shift) & (D - 1)] + i;
+    const uint32_t o = gofs[min((k >> shift) & mask, D - 1)] + i;
     if (kout) kout[o] = k;
     vout[o] = sv[i];
   }
@@ -311,11 +328,15 @@ void scan_exclusive(uint32_t* x, uint64_t m, const RadixWs& w, hipStream_t s) {
 // one sort: per pass count -> scan -> scatter.  The passes ping-pong between
 // the workspace staging (W) and the output (O); pass i writes O when an even
 // number of passes follows it, so the last one lands in O.
-void radix_run(const KeySrc& src0, uint64_t n, uint32_t bits, uint32_t* kout, uint32_t* vout, void* ws, hipStream_t s) {
+void radix_run(const KeySrc& src0, uint64_t n, uint32_t bits, uint32_t* kout, uint32_t* vout, void* ws, hipStream_t s,
+               uint32_t key_range = 0) {
   if (n == 0) return;
   if (n > 0xFFFFFFFFull) throw std::invalid_argument("radix sort: more than 2^32 - 1 keys");
   bits = bits < 1 ? 1 : (bits > 32 ? 32 : bits);
-  const uint32_t passes = (bits + kMaxDigitBits - 1) / kMaxDigitBits;
+  // keys below a known range of at most 2^11 values: ONE pass whose digit is the key
+  const bool wide = key_range >= 2 && key_range <= kWideDigits && bits > kMaxDigitBits && bits <= kWideBits &&
+                    (1u << bits) >= key_range;
+  const uint32_t passes = wide ? 1u : (bits + kMaxDigitBits - 1) / kMaxDigitBits;
   RadixWs w = radix_ws(ws, n);
   const uint64_t tiles = tiles_of(n);
   if (tiles > 0x7FFFFFFFull) throw std::invalid_argument("radix sort: too many tiles");
@@ -330,16 +351,26 @@ void radix_run(const KeySrc& src0, uint64_t n, uint32_t bits, uint32_t* kout, ui
     KeySrc src = p == 0 ? src0 : KeySrc{ck, nullptr, nullptr, nullptr, false};
     const int kind = p > 0 ? SRC_U32 : (src.k32 ? SRC_U32 : (src.k16 ? SRC_U16 : SRC_F32));
     const int vk = p > 0 ? 2 : (src.vals ? 1 : 0);
+    const uint32_t D = wide ? key_range : (1u << pb);
     const dim3 g((uint32_t)tiles);
-    if (kind == SRC_U32) hipLaunchKernelGGL(radix_count_kernel<SRC_U32>, g, kBlock, 0, s, src, n, shift, pb, tiles, w.counts);
-    if (kind == SRC_U16) hipLaunchKernelGGL(radix_count_kernel<SRC_U16>, g, kBlock, 0, s, src, n, shift, pb, tiles, w.counts);
-    if (kind == SRC_F32) hipLaunchKernelGGL(radix_count_kernel<SRC_F32>, g, kBlock, 0, s, src, n, shift, pb, tiles, w.counts);
-    scan_exclusive(w.counts, (uint64_t)(1u << pb) * tiles, w, s);
-#define PGA_SCATTER(K, V) hipLaunchKernelGGL((radix_scatter_kernel<K, V>), g, kBlock, 0, s, src, cv, n, shift, pb, tiles, w.counts, dk, dv)
-    if (vk == 2) PGA_SCATTER(SRC_U32, 2);
-    else if (kind == SRC_U32) { if (vk) PGA_SCATTER(SRC_U32, 1); else PGA_SCATTER(SRC_U32, 0); }
-    else if (kind == SRC_U16) { if (vk) PGA_SCATTER(SRC_U16, 1); else PGA_SCATTER(SRC_U16, 0); }
-    else { if (vk) PGA_SCATTER(SRC_F32, 1); else PGA_SCATTER(SRC_F32, 0); }
+#define PGA_COUNT(K, MD) hipLaunchKernelGGL((radix_count_kernel<K, MD>), g, kBlock, 0, s, src, n, shift, pb, D, tiles, w.counts)
+#define PGA_SCATTER(K, V, MD) hipLaunchKernelGGL((radix_scatter_kernel<K, V, MD>), g, kBlock, 0, s, src, cv, n, shift, pb, D, tiles, w.counts, dk, dv)
+    if (wide) {  // one pass over u16 keys (rank order of an integer objective)
+      if (kind != SRC_U16 || vk != 0) throw std::logic_error("radix sort: single-pass mode is for u16 keys");
+      PGA_COUNT(SRC_U16, kWideDigits);
+      scan_exclusive(w.counts, (uint64_t)D * tiles, w, s);
+      PGA_SCATTER(SRC_U16, 0, kWideDigits);
+    } else {
+      if (kind == SRC_U32) PGA_COUNT(SRC_U32, kMaxDigits);
+      if (kind == SRC_U16) PGA_COUNT(SRC_U16, kMaxDigits);
+      if (kind == SRC_F32) PGA_COUNT(SRC_F32, kMaxDigits);
+      scan_exclusive(w.counts, (uint64_t)D * tiles, w, s);
+      if (vk == 2) PGA_SCATTER(SRC_U32, 2, kMaxDigits);
+      else if (kind == SRC_U32) { if (vk) PGA_SCATTER(SRC_U32, 1, kMaxDigits); else PGA_SCATTER(SRC_U32, 0, kMaxDigits); }
+      else if (kind == SRC_U16) { if (vk) PGA_SCATTER(SRC_U16, 1, kMaxDigits); else PGA_SCATTER(SRC_U16, 0, kMaxDigits); }
+      else { if (vk) PGA_SCATTER(SRC_F32, 1, kMaxDigits); else PGA_SCATTER(SRC_F32, 0, kMaxDigits); }
+    }
+#undef PGA_COUNT
 #undef PGA_SCATTER
     ck = dk;
     cv = dv;
@@ -351,7 +382,7 @@ void radix_run(const KeySrc& src0, uint64_t n, uint32_t bits, uint32_t* kout, ui
 }  // namespace
 
 size_t radix_sort_workspace_bytes(uint64_t n) {
-  const uint64_t entries = (uint64_t)kMaxDigits * tiles_of(n);
+  const uint64_t entries = (uint64_t)kWideDigits * tiles_of(n);
   const uint64_t chunks = (entries + kScanChunk - 1) / kScanChunk;
   return al(4ull * entries) + al(4ull * chunks) + al(4ull * ((chunks + kScanChunk - 1) / kScanChunk)) + 2 * al(4ull * n);
 }
@@ -378,7 +409,7 @@ void rank_order16_launch(const uint16_t* keys16, uint64_t S, uint32_t key_range,
   uint32_t bits = 1;
   while (bits < 16 && (1u << bits) < key_range) ++bits;
   uint32_t* keys_out = (uint32_t*)((char*)ws + radix_sort_workspace_bytes(S));
-  radix_run(KeySrc{nullptr, keys16, nullptr, nullptr, false}, S, bits, keys_out, order, ws, s);
+  radix_run(KeySrc{nullptr, keys16, nullptr, nullptr, false}, S, bits, keys_out, order, ws, s, key_range);
 }
 
 }  // namespace pga
