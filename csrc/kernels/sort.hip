@@ -127,11 +127,19 @@ __global__ __launch_bounds__(kBlock) void radix_count_kernel(KeySrc src, uint64_
     const uint32_t d = min((load_key<SRC>(src, e < n ? e : n - 1) >> shift) & mask, D - 1);  // unconditional load
     dig[i] = e < n ? d : D;
   }
+  if (MAXD > kMaxDigits) {
+    // the whole key as digit: spread over many bins, plain LDS atomics beat
+    // an 11-ballot match per key
 #pragma unroll
-  for (uint32_t i = 0; i < kTile / kBlock; ++i) {
-    const bool ok = dig[i] < D;
-    const uint64_t peers = match_digit(dig[i], ok, bits);
-    if (ok && (peers & below) == 0ull) atomicAdd(&h[dig[i]], (uint32_t)__popcll(peers));
+    for (uint32_t i = 0; i < kTile / kBlock; ++i)
+      if (dig[i] < D) atomicAdd(&h[dig[i]], 1u);
+  } else {
+#pragma unroll
+    for (uint32_t i = 0; i < kTile / kBlock; ++i) {
+      const bool ok = dig[i] < D;
+      const uint64_t peers = match_digit(dig[i], ok, bits);
+      if (ok && (peers & below) == 0ull) atomicAdd(&h[dig[i]], (uint32_t)__popcll(peers));
+    }
   }
   __syncthreads();
   for (uint32_t d = threadIdx.x; d < D; d += kBlock) counts[(uint64_t)d * tiles + blockIdx.x] = h[d];
