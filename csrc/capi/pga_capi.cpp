@@ -552,10 +552,12 @@ gene** pga_get_best_top_all(pga_t* p, unsigned length) {
       isl.stream = p->stream;
       const uint32_t k = (uint32_t)std::min<uint64_t>(length, isl.config().S);
       const size_t rb = isl.row_bytes();
-      char* buf = (char*)isl.scratch(4ull * k + rb * k + 4ull * k);
+      // rows at a 16-byte boundary: the gather kernel stores them as uint4
+      const size_t roff = (4ull * k + 15) & ~(size_t)15, soff = roff + ((rb * k + 15) & ~(size_t)15);
+      char* buf = (char*)isl.scratch(soff + 4ull * k);
       uint32_t* idx = (uint32_t*)buf;
-      void* rdev = buf + 4ull * k;
-      float* sdev = (float*)(buf + 4ull * k + rb * k);
+      void* rdev = buf + roff;
+      float* sdev = (float*)(buf + soff);
       isl.topk(k, true, idx, /*sorted=*/true);
       isl.gather(idx, k, rdev, sdev);
       rows[i].resize(rb / 4 * k);

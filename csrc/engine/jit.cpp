@@ -3,6 +3,7 @@
 
 #include <dlfcn.h>
 #include <spawn.h>
+#include <sys/stat.h>
 #include <sys/wait.h>
 #include <unistd.h>
 
@@ -149,6 +150,7 @@ std::shared_ptr<JitKernel> jit_compile(int encoding, const std::string& source, 
   k->name = name;
   k->source = jit_kernel_source(encoding, source, name);
   k->user_source = source;
+  k->options = extra_options;
   rtc_program prog = nullptr;
   if (r.create(&prog, k->source.c_str(), "pga_jit_objective.hip", 0, nullptr, nullptr) != 0)
     throw std::runtime_error("hiprtcCreateProgram failed");
@@ -266,9 +268,42 @@ int spawn_shell(const std::string& cmd, const std::string& log) {
   return WIFEXITED(st) ? WEXITSTATUS(st) : -1;
 }
 
+// The code-object cache: $PGA_JIT_CACHE, else $XDG_CACHE_HOME/pga_jit, else
+// ~/.cache/pga_jit.  Code objects found there are loaded and launched, so the
+// directory must be private: it is created 0700 and used only if it is a real
+// directory (not a symlink) owned by this user and not group/world-writable.
 std::string jit_cache_dir() {
-  if (const char* e = std::getenv("PGA_JIT_CACHE")) return e;
-  return "/tmp/pga_jit_cache_" + std::to_string((unsigned)getuid());
+  std::string dir;
+  if (const char* e = std::getenv("PGA_JIT_CACHE")) {
+    dir = e;
+  } else if (const char* x = std::getenv("XDG_CACHE_HOME"); x && *x) {
+    dir = std::string(x) + "/pga_jit";
+  } else if (const char* h = std::getenv("HOME"); h && *h) {
+    dir = std::string(h) + "/.cache/pga_jit";
+  } else {
+    throw std::runtime_error("no private JIT cache directory: set PGA_JIT_CACHE, XDG_CACHE_HOME or HOME");
+  }
+  while (dir.size() > 1 && dir.back() == '/') dir.pop_back();
+  // parents as needed (0700), then the directory itself
+  for (size_t k = dir.find('/', 1); k != std::string::npos; k = dir.find('/', k + 1))
+    (void)mkdir(dir.substr(0, k).c_str(), 0700);
+  (void)mkdir(dir.c_str(), 0700);
+  struct stat st;
+  if (lstat(dir.c_str(), &st) != 0 || !S_ISDIR(st.st_mode))
+    throw std::runtime_error("JIT cache " + dir + " is not a directory");
+  if (st.st_uid != getuid() || (st.st_mode & (S_IWGRP | S_IWOTH)) != 0)
+    throw std::runtime_error("JIT cache " + dir + " is not private (owner " + std::to_string(st.st_uid) +
+                             ", mode " + std::to_string(st.st_mode & 0777) + "): refusing to load code from it");
+  return dir;
+}
+
+std::string shell_quote(const std::string& v) {
+  std::string r = "'";
+  for (char ch : v) {
+    if (ch == '\'') r += "'\\''";
+    else r += ch;
+  }
+  return r + "'";
 }
 
 std::string read_text(const std::string& path) {
@@ -301,12 +336,15 @@ std::string JitKernel::build_gen_object(uint32_t gs, bool full, bool dense, uint
                           "extern \"C\" __device__ float pga_user_objective(__attribute__((address_space(1))) "
                           "const unsigned int* w, unsigned int, const float* d) { return " + name +
                           "((const unsigned int*)w, " + std::to_string(L) + "u, d); }\n";
-  const std::string h = std::to_string(std::hash<std::string>{}(src + "|" + kbc_text));
+  // the user's compile options (-D, -I, ...) apply to the fused objective as
+  // they do to the evaluation kernel, and are part of the cache key
+  std::string uopts;
+  for (const std::string& o : options) uopts += " " + shell_quote(o);
+  const std::string h = std::to_string(std::hash<std::string>{}(src + "|" + uopts + "|" + kbc_text));
   const std::string dir = jit_cache_dir();
   const std::string base = dir + "/obj_" + h;
   const std::string co = base + "_" + variant + ".co", log = base + "_" + variant + ".log";
   if (!read_file(co).empty()) return co;
-  if (spawn_shell("mkdir -p '" + dir + "'", "/dev/null") != 0) throw std::runtime_error("cannot create " + dir);
   // per-process intermediates; the code object appears atomically (rename),
   // so concurrent processes compiling the same objective never see a partial one
   const std::string pid = std::to_string((unsigned)getpid());
@@ -318,8 +356,8 @@ std::string JitKernel::build_gen_object(uint32_t gs, bool full, bool dense, uint
   // unoptimised bitcode on both sides: the link optimises the whole kernel
   // once, with the objective inlined (optimising twice costs registers)
   const std::string cc = "'" + rocm + "/bin/hipcc' -x hip --offload-arch=gfx950 -O3 -Xclang -disable-llvm-passes "
-                         "-std=c++17 -ffp-contract=fast -fgpu-rdc --cuda-device-only -emit-llvm -c '" + work +
-                         ".hip' -o '" + work + ".bc'";
+                         "-std=c++17 -ffp-contract=fast -fgpu-rdc --cuda-device-only -emit-llvm" + uopts + " -c '" +
+                         work + ".hip' -o '" + work + ".bc'";
   // -flto: one LTO module, so the objective inlines into the kernel (without
   // it each bitcode is compiled on its own and the objective is a call)
   const std::string ld = "'" + rocm + "/lib/llvm/bin/clang' --target=amdgcn-amd-amdhsa -mcpu=gfx950 -O3 -flto '" + kbc +
@@ -336,7 +374,8 @@ std::string JitKernel::build_gen_object(uint32_t gs, bool full, bool dense, uint
 
 hipFunction_t JitKernel::gen_function(int device, uint32_t gs, bool full, bool dense, uint32_t L, bool build) {
   if (encoding != ENC_BINARY || fused_failed_ || device < 0) return nullptr;
-  const uint64_t key = ((uint64_t)L << 8) | (gs * 4u + (full ? 2u : 0u) + (dense ? 1u : 0u));
+  // (L, gs, full, dense) in disjoint fields: gs * 4 + 3 < 2^16
+  const uint64_t key = ((uint64_t)L << 16) | (gs * 4u + (full ? 2u : 0u) + (dense ? 1u : 0u));
   for (const GenVariant& v : gen_)
     if (v.device == device && v.key == key) return v.fn;
   if (!build) return nullptr;
@@ -358,8 +397,10 @@ hipFunction_t JitKernel::gen_function(int device, uint32_t gs, bool full, bool d
     fused_error_ = std::string("loading the fused generation kernel: ") + hipGetErrorString(e);
     return nullptr;
   }
-  int occ = 0;
-  if (hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&occ, v.fn, 256, 0) != hipSuccess || occ <= 0) occ = 1;
+  int occ = 0;  // resident 4-wave blocks per CU (tp_geometry_occ)
+  if (hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&occ, v.fn, 256, tp_dyn_lds_bytes(4)) != hipSuccess ||
+      occ <= 0)
+    occ = 1;
   v.occ = (uint32_t)occ;
   gen_.push_back(v);
   return v.fn;
@@ -370,19 +411,22 @@ uint32_t JitKernel::gen_launch(hipFunction_t f, const void* args, size_t args_by
   uint32_t occ = 1;
   for (const GenVariant& v : gen_)
     if (v.fn == f) occ = v.occ;
-  // the same grid launch_grid_occ gives the built-in kernels: resident blocks x CUs
-  uint64_t need = (S + 255) / 256, cap = (uint64_t)device_cu_count() * occ;
-  if (cap > max_grid) cap = max_grid;
-  const uint32_t grid = (uint32_t)std::max<uint64_t>(1, std::min(need, cap));
+  // the geometry the built-in kernels get (tp_geometry)
+  if (args_bytes != sizeof(GenArgs)) throw std::invalid_argument("fused generation: kernel arguments are not a GenArgs");
+  GenArgs a;
+  std::memcpy(&a, args, sizeof(a));
+  const TpGeom t = tp_geometry_occ(S, 1, occ, 64 / group_size(a.chunks));
+  a.tp_unit = t.unit;
+  const uint32_t grid = std::min(t.grid, max_grid);
   // kernel arguments as one packed buffer: (GenArgs a, unsigned long long* parts)
   std::vector<char> buf(args_bytes + 16);
-  std::memcpy(buf.data(), args, args_bytes);
+  std::memcpy(buf.data(), &a, args_bytes);
   size_t off = (args_bytes + 7) & ~(size_t)7;
   std::memcpy(buf.data() + off, &parts, sizeof(parts));
   size_t total = off + sizeof(parts);
   void* cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, buf.data(), HIP_LAUNCH_PARAM_BUFFER_SIZE, &total,
                  HIP_LAUNCH_PARAM_END};
-  PGA_HIP_CHECK(hipModuleLaunchKernel(f, grid, 1, 1, 256, 1, 1, 0, s, nullptr, cfg));
+  PGA_HIP_CHECK(hipModuleLaunchKernel(f, grid, 1, 1, t.block, 1, 1, t.lds, s, nullptr, cfg));
   return grid;
 }
 

@@ -33,9 +33,6 @@ namespace {
 
 using namespace dev;
 
-#ifndef PGA_JIT_WAVES
-#define PGA_JIT_WAVES 4  // the fused-JIT variant's waves/SIMD (jitgen.hip): 107.2 us vs 111.9 at 5 (2 spills)
-#endif
 constexpr int kObjJit = 1001;  // launcher-only objective id: the linked user objective (jitgen.hip)
 
 // per-lane objective accumulator over the chunks a lane owns
@@ -375,18 +372,23 @@ __global__ __launch_bounds__(kBlock) void binary_kernel(GenArgs a, unsigned long
 // ---------------------------------------------------------------------------
 // The hot generation kernel: transposed tournaments.
 //
-// A wave owns a contiguous range of children and breeds NG = 64/GS of them per
-// STEP (group g: child begin + t*NG + g).  Steps come in BATCHES of GS steps =
-// 64 children, and the per-child work that does not touch the genome runs
-// transposed, one lane per child of a whole batch.  The range is cut into
-// SEGMENTS of up to kSegBatches batches, each in two phases:
-//   TOURNAMENTS  every batch of the segment at once: one Philox block = the 4
+// A wave breeds NG = 64/GS children per STEP (group g: child bs + i*NG + g).
+// Steps come in BATCHES of GS steps = 64 children, and the per-child work
+// that does not touch the genome runs transposed, one lane per child of a
+// whole batch.  A block owns a contiguous share of the population
+// (tp_block_range), in ROUNDS of at most tp_par_cap children, each in two
+// phases:
+//   TOURNAMENTS  SEGMENTS of up to kSegBatches batches pulled from an LDS
+//                counter, one per wave at a time: one Philox block = the 4
 //                contestants of a child, all 4 x kSegBatches key loads in
-//                flight together, compare -> (parent A, parent B) in LDS
+//                flight together, compare -> (parent A, parent B) of every
+//                child of the segment in LDS, then the segment's ready flag
 //                (linear ranking: two rank picks, two rank-order loads)
-//   BREED        per batch, RESOLVE: the misc block (crossover test, cut
-//                points, mutation count K) and the sparse bit-flip positions
-//                (one more block, first K distinct by a pairwise check) -> a
+//   BREED        UNITS of U <= 64 children pulled from a second counter once
+//                no segment is left (a unit waits for its segment's flag):
+//                RESOLVE the misc block (crossover test, cut points,
+//                mutation count K) and the sparse bit-flip positions (one
+//                more block, first K distinct by a pairwise check) -> a
 //                32-byte child RECORD in the wave's LDS ring (2 batches);
 //                per step: XO mask Philox (one block per chunk), mix, flips,
 //                popcount, group butterfly, stores.
@@ -399,12 +401,9 @@ __global__ __launch_bounds__(kBlock) void binary_kernel(GenArgs a, unsigned long
 // A child costs 3/64 of a Philox per lane for its child-level words, and
 // mutation is a short loop over the record's positions instead of a
 // divergent geometric search in every chunk.
-//
-// Breed pipeline (per step t): RESOLVE batch (t+1)/GS if (t+1)%GS==0; load
-// the parent rows of step t+1; breed step t from the rows loaded one step
-// earlier.  Every vector memory operation is unconditional (s_waitcnt vmcnt
-// retires in order and hipcc assumes the fewest outstanding loads over all
-// paths, so a conditionally issued load would make the next wait drain it).
+// Why a counter: equal static shares per wave left the CU's youngest waves
+// breeding alone for the last ~20 us (oldest-first issue, tp.hpp); pulled
+// batches end every wave of a CU within about one batch of each other.
 // ---------------------------------------------------------------------------
 
 #ifdef PGA_TP_TIMING
@@ -416,12 +415,6 @@ __device__ unsigned long long pga_tp_clk[kMaxGrid * 4][8];
 // kTpMaxElite (elites the fast kernel routes through its records),
 // kSegBatches and the work units: tp.hpp
 
-// 5 waves/SIMD: 4, 5 and 6 measured alike for the breed phase alone (the
-// fabric, not occupancy, is the bound); 5 gives the tournament phase its
-// 16 key loads in flight without spilling (6: 23 spilled VGPRs, +8%)
-#ifndef PGA_TP_WAVES
-#define PGA_TP_WAVES 5
-#endif
 #ifndef PGA_TP_NOKEYS
 #define PGA_TP_NOKEYS 0
 #endif
@@ -443,22 +436,28 @@ __device__ __forceinline__ uint32_t pos16(uint4 r1, uint32_t k) {  // k-th packe
 template <int GS, int OBJ, bool FULL, bool DENSE>
 __device__ __forceinline__ void binary_gen_tp_body(GenArgs a, unsigned long long* best_parts) {
   resolve_gen(a);
-  constexpr uint32_t NW = kBlock / 64;
-  constexpr uint32_t NG = 64 / GS;  // children per wave per step
+  const uint32_t NW = blockDim.x >> 6;  // 4 or 16 waves (tp_dyn_lds of the launch)
+  constexpr uint32_t NG = 64 / GS;      // children per wave per step
+  constexpr uint32_t PD = tp_prefetch_depth(GS);  // steps of parent rows in flight (tp.hpp)
   constexpr bool EVALS = OBJ != OBJ_NONE;
   // integer objectives tournament on their exact u16 keys (L2-resident)
   constexpr bool KEY = OBJ == OBJ_ONEMAX || OBJ == OBJ_LEADING_ONES || OBJ == OBJ_TRAP;
-  __shared__ uint4 lds_rec[NW][2][64][2];           // per wave: 2 batches x 64 records x 32 B
-  __shared__ uint2 lds_par[NW][kSegBatches * 64];  // per wave: the segment's (parent A, parent B)
+  // dynamic LDS: per wave 2 batches x 64 records x 32 B, then the round's
+  // (parent A, parent B) of every child
+  uint4(*lds_rec)[2][64][2] = (uint4(*)[2][64][2])pga_dyn_lds;
+  uint2* lds_par = (uint2*)(pga_dyn_lds + NW * 4096u);
   __shared__ uint32_t lds_thr[kMutCap];
   __shared__ uint32_t lds_el[kTpMaxElite];  // elite sources
-  __shared__ unsigned long long lds_red[NW];
+  __shared__ unsigned long long lds_red[kTpMaxWaves];
+  __shared__ uint32_t lds_next;   // the round's next unbred unit
+  __shared__ uint32_t lds_tnext;  // the round's next tournament segment
+  __shared__ uint32_t lds_ready[kTpMaxSegs];  // per segment: its parents are in LDS
   constexpr bool KMF = OBJ == kObjKnapMfma;
-  __shared__ uint4 lds_kscr[KMF ? NW : 1][kKnapScratch];             // knapsack: per-wave chunk / C scratch
+  __shared__ uint4 lds_kscr[KMF ? kTpMaxWaves : 1][kKnapScratch];      // knapsack: per-wave chunk / C scratch
   __shared__ uint4 lds_ktab[KMF ? kKnapSlices * 4 * kKnapMaxCols : 1];  // knapsack: digit table
   // JIT (a linked user objective): the steps only store the children; after
-  // each segment every lane evaluates its children of the segment from the
-  // rows just stored (L2), one child per lane
+  // each batch's last step every lane evaluates one child of the batch from
+  // the rows just stored (8 KB per wave, still in the L2)
   constexpr bool JIT = OBJ == kObjJit;
 
   const uint32_t lane = lane_id(), wid = threadIdx.x >> 6;
@@ -487,47 +486,61 @@ __device__ __forceinline__ void binary_gen_tp_body(GenArgs a, unsigned long long
 #define ELEM(T, base, i) (*(T*)((char*)(base) + (uint32_t)(i) * (uint32_t)sizeof(T)))
 #define ROW(base, row, ch) (*(uint4*)((char*)(base) + ((uint32_t)(row) * rb + (uint32_t)(ch) * 16u)))
 
-  // this wave's children [wbegin, wend): contiguous, a multiple of NG long
-  uint32_t wbegin, wend, bfirst;
-  tp_wave_range(S, NG, wbegin, wend, bfirst);
+  // this block's children [bbegin, bend) (tp.hpp)
+  const uint32_t U = tp_unit(a, NG);  // children per breed unit (tp.hpp)
+  uint32_t bbegin, bend;
+  tp_block_range(S, U, bbegin, bend);
+  const uint32_t pcap = tp_par_cap(NW);
 
   // elite sources of children [0, n_elite) (n_elite <= kTpMaxElite), for the
-  // blocks that hold any of them
-  if (a.n_elite > 0 && bfirst < a.n_elite) {
+  // block that holds any of them
+  if (a.n_elite > 0 && bbegin < a.n_elite) {
     if (a.elite_idx) {
-      for (uint32_t i = threadIdx.x; i < a.n_elite; i += kBlock) lds_el[i] = a.elite_idx[i];
+      for (uint32_t i = threadIdx.x; i < a.n_elite; i += blockDim.x) lds_el[i] = a.elite_idx[i];
     } else {
-      unsigned long long b = block_reduce_parts(a.best_cur, a.n_best_cur, lds_red);
+      unsigned long long b = block_reduce_parts_n(a.best_cur, a.n_best_cur, lds_red, NW);
       if (threadIdx.x == 0) lds_el[0] = (uint32_t)best_index(b);
     }
   }
   if (bitflip)
-    for (uint32_t i = threadIdx.x; i < kMutCap; i += kBlock) lds_thr[i] = a.mut_thr[i];
+    for (uint32_t i = threadIdx.x; i < kMutCap; i += blockDim.x) lds_thr[i] = a.mut_thr[i];
   if (KMF)
-    for (uint32_t i = threadIdx.x; i < kKnapSlices * 4 * kKnapMaxCols; i += kBlock)
+    for (uint32_t i = threadIdx.x; i < kKnapSlices * 4 * kKnapMaxCols; i += blockDim.x)
       lds_ktab[i] = ((const uint4*)a.knap_tab)[i];
-  __syncthreads();
+  if (threadIdx.x == 0) lds_next = lds_tnext = 0;
+  if (threadIdx.x < kTpMaxSegs) lds_ready[threadIdx.x] = 0;
 
   unsigned long long my_best = 0;
   ScoreStats st;
   uint4(*rec)[64][2] = lds_rec[wid];
-  uint2* par = lds_par[wid];
   static_assert(sizeof(lds_rec[0]) >= kSegBatches * 64 * sizeof(uint4), "contestant staging");
 #ifdef PGA_TP_TIMING
   const unsigned long long clk0 = clock64(), rt0 = wall_clock64();
-  unsigned long long clk_t = 0, clk_b = 0;
+  unsigned long long clk_t = 0, clk_b = 0, n_bred = 0;
 #endif
-  for (uint32_t begin = wbegin; begin < wend; begin += kSegBatches * 64u) {  // wave-uniform
-    const uint32_t end = begin + kSegBatches * 64u < wend ? begin + kSegBatches * 64u : wend;
-    const uint32_t nsteps = (end - begin + NG - 1) / NG;
-    const uint32_t nbatch = (end - begin + 63) / 64;
+  for (uint32_t rbeg = bbegin; rbeg < bend; rbeg += pcap) {  // block-uniform rounds
+    const uint32_t rend = rbeg + pcap < bend ? rbeg + pcap : bend;
+    const uint32_t nb = (rend - rbeg + U - 1) / U;                          // the round's units
+    const uint32_t nseg = (rend - rbeg + kSegBatches * 64 - 1) / (kSegBatches * 64);  // its tournament segments
+    __syncthreads();  // tables / elites / counter visible; the previous round's records and parents released
 #ifdef PGA_TP_TIMING
     const unsigned long long clkA = clock64();
 #endif
 
-    // TOURNAMENTS of the whole segment: all key loads in flight at once; the
-    // contestants wait in the record ring (free until the first RESOLVE)
-    {
+    // TOURNAMENTS of the round, one segment of <= kSegBatches batches at a
+    // time per wave, segments pulled from a counter: all key loads of a
+    // segment in flight at once; the contestants wait in the wave's record
+    // ring (free until it breeds).  A wave breeds as soon as no segment is
+    // left; a unit's RESOLVE waits for its segment's flag (no block barrier)
+    for (;;) {
+      uint32_t ts = 0;
+      if (lane == 0) ts = __hip_atomic_fetch_add(&lds_tnext, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      const uint32_t sg = __builtin_amdgcn_readfirstlane(ts);
+      if (sg >= nseg) break;
+      const uint32_t begin = rbeg + sg * kSegBatches * 64u;
+      const uint32_t end = begin + kSegBatches * 64u < rend ? begin + kSegBatches * 64u : rend;
+      const uint32_t nbatch = (end - begin + 63) / 64;
+      uint2* par = lds_par + sg * kSegBatches * 64u;
       uint4* ixs = &rec[0][0][0];  // [B * 64 + lane]: 4 x 64 x 16 B = the ring's 4 KiB
       // raw keys (u16 zero-extended, or f32 scores), compared only after every
       // load of the segment is issued: a conversion here would make hipcc wait
@@ -571,7 +584,8 @@ __device__ __forceinline__ void binary_gen_tp_body(GenArgs a, unsigned long long
         }
         // no early exit past the segment's last batch: straight-line loads keep
         // every key in a register (a wave-uniform break spilled the last four);
-        // the extra batches skip the Philox draw and are never resolved
+        // the extra batches skip the Philox draw and are never bred (their
+        // parents land inside the round's slots: tp_par_cap holds whole segments)
       }
       if (roul) {
         // fitness-proportional, by the guide table: the pick is the smallest i
@@ -584,28 +598,28 @@ __device__ __forceinline__ void binary_gen_tp_body(GenArgs a, unsigned long long
         const float scale = *a.roul_scale;
         uint32_t ix[NS];
         float tg[NS];
-        #pragma unroll
+#pragma unroll
         for (uint32_t i = 0; i < NS; ++i) {
           const uint32_t w = __builtin_bit_cast(uint32_t, (i & 1u) ? k1[i >> 1] : k0[i >> 1]);
           tg[i] = word_to_unit(w) * total;
           ix[i] = total > 0.f ? ELEM(const uint32_t, a.roul_guide, roulette_bucket(tg[i], scale, S)) : word_to_index(w, S);
         }
         float v[NS];
-        #pragma unroll
+#pragma unroll
         for (uint32_t i = 0; i < NS; ++i) v[i] = ELEM(const float, a.cumfit, ix[i]);
         for (uint32_t it = 0; it < S; ++it) {  // wave-uniform: until every pick of every lane is resolved
           bool more = false;
-          #pragma unroll
+#pragma unroll
           for (uint32_t i = 0; i < NS; ++i) more |= total > 0.f && v[i] < tg[i];
           if (!__any(more)) break;
-          #pragma unroll
+#pragma unroll
           for (uint32_t i = 0; i < NS; ++i) {
             const bool adv = total > 0.f && v[i] < tg[i];
             ix[i] += adv ? 1u : 0u;
             v[i] = ELEM(const float, a.cumfit, ix[i]);
           }
         }
-        #pragma unroll
+#pragma unroll
         for (uint32_t B = 0; B < kSegBatches; ++B) {
           k0[B] = __builtin_bit_cast(KT, ix[2 * B]);
           k1[B] = __builtin_bit_cast(KT, ix[2 * B + 1]);
@@ -624,18 +638,31 @@ __device__ __forceinline__ void binary_gen_tp_body(GenArgs a, unsigned long long
         }
         par[B * 64u + lane] = make_uint2(pa, pb);
       }
+      // publish: the segment's parents (this wave's LDS stores, in order)
+      // before its flag
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+      if (lane == 0) __hip_atomic_store(&lds_ready[sg], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
 #ifdef PGA_TP_TIMING
     const unsigned long long clkB = clock64();
     clk_t += clkB - clkA;
 #endif
 
-    // RESOLVE: parents, crossover plan and flip positions of batch B -> records
-#define PGA_TP_RESOLVE(B)                                                                                       \
+    // RESOLVE: parents, crossover plan and flip positions of the round's unit
+    // BI -> the records of ring slot SL (lanes past the unit: unused copies)
+#define PGA_TP_RESOLVE(BI, SL)                                                                                  \
   {                                                                                                             \
-    const uint32_t tc = begin + (B) * 64u + lane;                                                               \
-    const uint32_t cc = tc < end ? tc : end - 1;                                                                \
-    const uint2 pp = par[(B) * 64u + lane];                                                                     \
+    {  /* the unit's tournament segment is done (wave-uniform spin, rare) */                                    \
+      const uint32_t sg_ = (BI) * U / (kSegBatches * 64u);                                                      \
+      while (__hip_atomic_load(&lds_ready[sg_], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == 0u)          \
+        __builtin_amdgcn_s_sleep(1);                                                                            \
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");                                                    \
+    }                                                                                                           \
+    const uint32_t bs_ = rbeg + (BI) * U;                                                                       \
+    const uint32_t be_ = bs_ + U < rend ? bs_ + U : rend;                                                       \
+    const uint32_t tc = bs_ + lane;                                                                             \
+    const uint32_t cc = tc < be_ ? tc : be_ - 1;                                                                \
+    const uint2 pp = lds_par[cc - rbeg];                                                                        \
     uint32_t pa = pp.x, pb = pp.y;                                                                              \
     const u32x4 misc = bin_misc<true>(a.key, cc);                                                               \
     const bool elite = tc < a.n_elite;                                                                          \
@@ -676,35 +703,69 @@ __device__ __forceinline__ void binary_gen_tp_body(GenArgs a, unsigned long long
       }                                                                                                         \
     }                                                                                                           \
     const uint32_t meta = (K > 255u ? 255u : K) | ((jn > 0xFFFFu ? 0xFFFFu : jn) << 8) | (elite ? 1u << 31 : 0u); \
-    uint4(*r)[2] = rec[(B) & 1u];                                                                               \
+    uint4(*r)[2] = rec[(SL)];                                                                                   \
     r[lane][0] = make_uint4(pa, pb, lo | (hi << 16), meta);                                                     \
     r[lane][1] = P;                                                                                             \
   }
 
-    // prologue: batch 0 resolved, rows of step 0 in flight
-    PGA_TP_RESOLVE(0u)
-    uint4 A0, B0, A1, B1;
-    {
-      const uint4 r = rec[0][g][0];
-      A0 = ROW(cur, r.x, qq);
-      B0 = ROW(cur, r.y, qq);
-    }
+    // BREED: the round's units in ticket order from the block's counter, as
+    // two cursors over the wave's sequence of steps: the LOAD cursor issues
+    // the parent-row loads of the step PD steps ahead of the BREED cursor
+    // (PD register sets in flight: the row gathers are latency-bound, so the
+    // bytes in flight per wave set the throughput) and RESOLVEs a unit into
+    // the other ring slot when it enters it (a full unit has U / NG >= PD
+    // steps, so the breed cursor has left that slot by then).  Every vector
+    // memory operation is unconditional (s_waitcnt vmcnt retires in order and
+    // hipcc assumes the fewest outstanding loads over all paths, so a
+    // conditionally issued load would make the next wait drain it): an
+    // exhausted load cursor re-reads the breed cursor's rows.
+    uint32_t tk = 0;
+    if (lane == 0) tk = __hip_atomic_fetch_add(&lds_next, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    const uint32_t b0 = __builtin_amdgcn_readfirstlane(tk);  // the wave's first unit
+    if (b0 < nb) {
+      if (lane == 0) tk = __hip_atomic_fetch_add(&lds_next, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      uint32_t bn = __builtin_amdgcn_readfirstlane(tk);  // the next ticket (>= nb: none)
+      PGA_TP_RESOLVE(b0, 0u)
+      // breed cursor: ring slot, step, first child and steps of its unit
+      uint32_t slot = 0, i = 0, bs = rbeg + b0 * U;
+      uint32_t nst = ((bs + U < rend ? bs + U : rend) - bs + NG - 1) / NG;
+      // load cursor; lpend: at the end of its unit with ticket bn next;
+      // lmore = false: past the wave's last step
+      uint32_t lslot = 0, li = 0, lbs = bs, lnst = nst;
+      bool lpend = false, lmore = true, done = false;
 
-    // one STEP: every vector-memory operation is unconditional (the tail of
-    // the last wave writes the padding rows past S)
-#define PGA_TP_STEP(t, XA, XB, YA, YB)                                                                      \
+      // LOAD the parent rows of the load cursor's step into (YA, YB) and
+      // advance it
+#define PGA_TP_LOAD(YA, YB)                                                                                 \
   {                                                                                                         \
-    const uint32_t b = (t) / GS, i = (t) & (GS - 1);                                                        \
-    if ((((t) + 1) & (GS - 1)) == 0u && b + 1 < nbatch) PGA_TP_RESOLVE(b + 1)                               \
-    {                                                                                                       \
-      /* parent rows of step t+1 (the last step re-reads its own) */                                        \
-      const uint32_t tn = (t) + 1 < nsteps ? (t) + 1 : (t);                                                 \
-      const uint4 r = rec[(tn / GS) & 1u][(tn & (GS - 1)) * NG + g][0];                                     \
-      YA = ROW(cur, r.x, qq);                                                                               \
-      YB = ROW(cur, r.y, qq);                                                                               \
+    if (lpend) { /* entering the next unit */                                                               \
+      PGA_TP_RESOLVE(bn, lslot ^ 1u)                                                                        \
+      lslot ^= 1u;                                                                                          \
+      li = 0;                                                                                               \
+      lbs = rbeg + bn * U;                                                                                  \
+      lnst = ((lbs + U < rend ? lbs + U : rend) - lbs + NG - 1) / NG;                                       \
+      lpend = false;                                                                                        \
+      if (lane == 0)                                                                                        \
+        tk = __hip_atomic_fetch_add(&lds_next, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);         \
+      bn = __builtin_amdgcn_readfirstlane(tk);                                                              \
     }                                                                                                       \
-    const uint32_t c = begin + (t) * NG + g;                                                                \
-    const uint4 r0 = rec[b & 1u][i * NG + g][0];                                                            \
+    const uint4 r = rec[lmore ? lslot : slot][(lmore ? li : i) * NG + g][0];                                \
+    YA = ROW(cur, r.x, qq);                                                                                 \
+    YB = ROW(cur, r.y, qq);                                                                                 \
+    if (lmore && ++li == lnst) {                                                                            \
+      lpend = bn < nb;                                                                                      \
+      lmore = lpend;                                                                                        \
+    }                                                                                                       \
+  }
+
+      // one STEP: load PD steps ahead into (YA, YB), breed the breed cursor's
+      // step i from (XA, XB) (its children past S, at the population's end
+      // only, write the padding rows), advance the breed cursor
+#define PGA_TP_STEP(XA, XB, YA, YB)                                                                         \
+  {                                                                                                         \
+    PGA_TP_LOAD(YA, YB)                                                                                     \
+    const uint32_t c = bs + i * NG + g;                                                                     \
+    const uint4 r0 = rec[slot][i * NG + g][0];                                                              \
     const uint32_t meta = r0.w;                                                                             \
     const uint4 m = range ? range_keep_a(q, r0.z & 0xFFFFu, r0.z >> 16) : PGA_TP_XOMASK(c, q);               \
     uint4 v = mix4(XA, XB, m);                                                                              \
@@ -716,7 +777,7 @@ __device__ __forceinline__ void binary_gen_tp_body(GenArgs a, unsigned long long
     } else {                                                                                                \
       const uint32_t K = meta & 0xFFu;                                                                      \
       if (K > 0u) {                                                                                         \
-        const uint4 r1 = rec[b & 1u][i * NG + g][1];                                                        \
+        const uint4 r1 = rec[slot][i * NG + g][1];                                                          \
         const uint32_t kk = K < kRecPos ? K : kRecPos;                                                      \
         /* the first 4 unrolled (a loop here costs ~20 VGPRs of the whole kernel) */                       \
         _Pragma("unroll") for (uint32_t k = 0; k < 4; ++k) {                                               \
@@ -736,7 +797,7 @@ __device__ __forceinline__ void binary_gen_tp_body(GenArgs a, unsigned long long
     if constexpr (KMF) {                                                                                    \
       sc = knap_mfma<GS>(a, have ? v : make_uint4(0, 0, 0, 0), lane, q, lds_kscr[wid], lds_ktab);            \
     } else if constexpr (JIT) {                                                                             \
-      sc = 0.f; /* evaluated after the segment */                                                           \
+      sc = 0.f; /* evaluated after the unit */                                                              \
     } else {                                                                                                \
       BinObj<OBJ> acc;                                                                                      \
       if (have) acc.add(a, v, q);                                                                           \
@@ -750,58 +811,116 @@ __device__ __forceinline__ void binary_gen_tp_body(GenArgs a, unsigned long long
       my_best = pk > my_best ? pk : my_best;                                                                \
       st.add_if(q == 0u && c < S, sc);                                                                      \
     }                                                                                                       \
+    if (++i == nst) {                                                                                       \
+      if constexpr (JIT) PGA_TP_JIT_EVAL                                                                    \
+      PGA_TP_COUNT                                                                                          \
+      if (lbs == bs) { /* the load cursor never left this unit: it was the wave's last */                   \
+        done = true;                                                                                        \
+      } else {                                                                                              \
+        slot ^= 1u;                                                                                         \
+        i = 0;                                                                                              \
+        bs = lbs;                                                                                           \
+        nst = lnst;                                                                                         \
+      }                                                                                                     \
+    }                                                                                                       \
   }
 
-    uint32_t t = 0;
-    for (; t + 1 < nsteps; t += 2) {  // static row-register rotation
-      PGA_TP_STEP(t, A0, B0, A1, B1)
-      PGA_TP_STEP(t + 1, A1, B1, A0, B0)
-    }
-    if (t < nsteps) PGA_TP_STEP(t, A0, B0, A1, B1)
-#undef PGA_TP_RESOLVE
-#undef PGA_TP_STEP
-    if constexpr (JIT) {
-      // this wave's stores of the segment's rows complete before its lanes read
-      // them back (no other CU wrote them, so no stale L1 line can exist)
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-      for (uint32_t B = 0; B < nbatch; ++B) {  // wave-uniform
-        const uint32_t c = begin + B * 64u + lane;
-        if (c < end) {
-          const float sc = pga_user_objective((pga_global_words)((const char*)nxt + c * rb), L, a.obj_data);
-          ELEM(float, a.score_next, c) = sc;
-          const unsigned long long pk = c < S ? pack_best(sc, c) : 0ull;
-          my_best = pk > my_best ? pk : my_best;
-          st.add_if(c < S, sc);
+      // JIT: this wave's stores of the unit's rows complete before its lanes
+      // read them back (no other CU wrote them, so no stale L1 line can exist)
+#define PGA_TP_JIT_EVAL                                                                                     \
+  {                                                                                                         \
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");                                                  \
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");                                                  \
+    const uint32_t cj = bs + lane;                                                                          \
+    if (lane < U && cj < rend) {                                                                            \
+      const float sj = pga_user_objective((pga_global_words)((const char*)nxt + cj * rb), L, a.obj_data);   \
+      ELEM(float, a.score_next, cj) = sj;                                                                   \
+      my_best = pack_best(sj, cj) > my_best ? pack_best(sj, cj) : my_best;                                  \
+      st.add(sj);                                                                                           \
+    }                                                                                                       \
+  }
+#ifdef PGA_TP_TIMING
+#define PGA_TP_COUNT n_bred += (bs + U < rend ? bs + U : rend) - bs;
+#else
+#define PGA_TP_COUNT
+#endif
+
+      uint4 A0, B0, A1, B1, A2, B2, A3, B3;  // PD + 1 register sets, rotated statically
+      (void)A2; (void)B2; (void)A3; (void)B3;
+      if constexpr (PD == 1) {
+        PGA_TP_LOAD(A0, B0)
+        for (;;) {
+          PGA_TP_STEP(A0, B0, A1, B1)
+          if (done) break;
+          PGA_TP_STEP(A1, B1, A0, B0)
+          if (done) break;
+        }
+      } else if constexpr (PD == 2) {
+        PGA_TP_LOAD(A0, B0)
+        PGA_TP_LOAD(A1, B1)
+        for (;;) {
+          PGA_TP_STEP(A0, B0, A2, B2)
+          if (done) break;
+          PGA_TP_STEP(A1, B1, A0, B0)
+          if (done) break;
+          PGA_TP_STEP(A2, B2, A1, B1)
+          if (done) break;
+        }
+      } else {
+        PGA_TP_LOAD(A0, B0)
+        PGA_TP_LOAD(A1, B1)
+        PGA_TP_LOAD(A2, B2)
+        for (;;) {
+          PGA_TP_STEP(A0, B0, A3, B3)
+          if (done) break;
+          PGA_TP_STEP(A1, B1, A0, B0)
+          if (done) break;
+          PGA_TP_STEP(A2, B2, A1, B1)
+          if (done) break;
+          PGA_TP_STEP(A3, B3, A2, B2)
+          if (done) break;
         }
       }
+#undef PGA_TP_STEP
+#undef PGA_TP_LOAD
+#undef PGA_TP_JIT_EVAL
+#undef PGA_TP_COUNT
     }
+#undef PGA_TP_RESOLVE
 #ifdef PGA_TP_TIMING
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this segment's stores issued and done
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this round's stores issued and done
     clk_b += clock64() - clkB;
 #endif
+    __syncthreads();  // every wave out of the round's counters before they are reset
+    if (threadIdx.x == 0) lds_next = lds_tnext = 0;
+    if (threadIdx.x < kTpMaxSegs) lds_ready[threadIdx.x] = 0;
   }
 #undef ROW
 #undef ELEM
 #ifdef PGA_TP_TIMING
-  if (lane == 0) {
+  if (lane == 0 && blockIdx.x * NW + wid < kMaxGrid * 4) {
     const uint32_t wv = blockIdx.x * NW + wid;
     pga_tp_clk[wv][0] = clk_t;
     pga_tp_clk[wv][1] = clk_b;
     pga_tp_clk[wv][2] = clock64() - clk0;
-    pga_tp_clk[wv][3] = wend - wbegin;
+    pga_tp_clk[wv][3] = n_bred;
     pga_tp_clk[wv][4] = rt0;
     pga_tp_clk[wv][5] = wall_clock64();
     pga_tp_clk[wv][6] = __builtin_amdgcn_s_getreg((3 << 11) | 20);  // HW_REG_XCC_ID[3:0]
   }
 #endif
-  unsigned long long bb = block_max_u64(my_best, lds_red);
-  if (threadIdx.x == 0 && best_parts && EVALS) best_parts[blockIdx.x] = bb;
-  if (EVALS && best_parts && a.stats_parts) block_stats_store(st, a.stats_parts);
+  if (EVALS && best_parts) {  // block-uniform
+    unsigned long long bb = block_max_u64_n(my_best, lds_red, NW);
+    if (threadIdx.x == 0) best_parts[blockIdx.x] = bb;
+    if (a.stats_parts) block_stats_store_n(st, a.stats_parts, NW);
+  }
 }
 
+// 16-wave blocks (one per CU) for the headline launch and 4-wave blocks for
+// small populations; 128 VGPRs either way (the breed phase measured alike at
+// 4 and 5 waves per SIMD: the fabric is the bound)
 template <int GS, int OBJ, bool FULL, bool DENSE>
-__global__ __launch_bounds__(kBlock, OBJ == kObjKnapMfma ? 4 : (OBJ == kObjJit ? PGA_JIT_WAVES : PGA_TP_WAVES)) void binary_gen_tp(GenArgs a, unsigned long long* best_parts) {
+__global__ __launch_bounds__(kTpMaxWaves * 64) void binary_gen_tp(GenArgs a, unsigned long long* best_parts) {
   binary_gen_tp_body<GS, OBJ, FULL, DENSE>(a, best_parts);
 }
 
@@ -821,7 +940,7 @@ struct GenBatch {
 };
 
 template <int GS, int OBJ, bool FULL, bool DENSE>
-__global__ __launch_bounds__(kBlock, PGA_TP_WAVES) void binary_gen_tp_batch(GenBatch b) {
+__global__ __launch_bounds__(kTpMaxWaves * 64) void binary_gen_tp_batch(GenBatch b) {
   binary_gen_tp_body<GS, OBJ, FULL, DENSE>(b.a[blockIdx.y], b.parts[blockIdx.y]);
 }
 

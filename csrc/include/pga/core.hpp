@@ -350,6 +350,10 @@ struct GenArgs {
   // BINARY bit-flip: 1 = sparse sampler (mut_thr is the Binomial CDF table),
   // 0 = per-chunk geometric skips (mut_thr is the geometric table)
   uint32_t mut_sparse;
+
+  // two-phase kernels (tp.hpp): children per dynamically assigned breed unit,
+  // a power of two in [64 / GS, 64] set by the launcher (0 = 64)
+  uint32_t tp_unit;
 };
 
 PGA_HD uint32_t sel_words(const GenArgs& a) {

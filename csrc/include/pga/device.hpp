@@ -70,6 +70,29 @@ __device__ __forceinline__ unsigned long long block_reduce_parts(const unsigned 
   return block_max_u64<BLK>(v, lds4);
 }
 
+// the same two for a block of `nw` waves chosen at launch (nw <= 16; lds:
+// nw entries)
+__device__ __forceinline__ unsigned long long block_max_u64_n(unsigned long long v, unsigned long long* lds,
+                                                              uint32_t nw) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    unsigned long long w = shfl_xor_u64(v, o);
+    v = w > v ? w : v;
+  }
+  __syncthreads();
+  if (lane_id() == 0) lds[threadIdx.x >> 6] = v;
+  __syncthreads();
+  unsigned long long r = lds[0];
+  for (uint32_t i = 1; i < nw; ++i) r = lds[i] > r ? lds[i] : r;
+  return r;
+}
+__device__ __forceinline__ unsigned long long block_reduce_parts_n(const unsigned long long* parts, uint32_t n,
+                                                                   unsigned long long* lds, uint32_t nw) {
+  unsigned long long v = 0;
+  for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) v = parts[i] > v ? parts[i] : v;
+  return block_max_u64_n(v, lds, nw);
+}
+
 // Fused per-generation statistics: every evaluating kernel keeps a running
 // {min, sum} of the scores its lanes produce and, when GenArgs::stats_parts is
 // set, stores one {min, sum} pair per block next to its packed best (the max),
@@ -111,6 +134,33 @@ __device__ __forceinline__ void block_stats_store(ScoreStats st, float* parts) {
       mn = fminf(mn, lds_st[0][i]);
       sm += lds_st[1][i];
     }
+  }
+  if (threadIdx.x == 0) {
+    parts[2 * blockIdx.x] = mn;
+    parts[2 * blockIdx.x + 1] = sm;
+  }
+}
+
+// block_stats_store for a block of `nw` waves chosen at launch (nw <= 16)
+__device__ __forceinline__ void block_stats_store_n(ScoreStats st, float* parts, uint32_t nw) {
+  __shared__ float lds_stn[2][16];
+  float mn = st.mn, sm = st.sm;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    mn = fminf(mn, __shfl_xor(mn, o, 64));
+    sm += __shfl_xor(sm, o, 64);
+  }
+  __syncthreads();
+  if (lane_id() == 0) {
+    lds_stn[0][threadIdx.x >> 6] = mn;
+    lds_stn[1][threadIdx.x >> 6] = sm;
+  }
+  __syncthreads();
+  mn = lds_stn[0][0];
+  sm = lds_stn[1][0];
+  for (uint32_t i = 1; i < nw; ++i) {
+    mn = fminf(mn, lds_stn[0][i]);
+    sm += lds_stn[1][i];
   }
   if (threadIdx.x == 0) {
     parts[2 * blockIdx.x] = mn;

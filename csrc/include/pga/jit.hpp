@@ -32,6 +32,7 @@ class JitKernel {
   int encoding = 0;
   std::string name, source, log;
   std::string user_source;  // the objective as the user wrote it
+  std::vector<std::string> options;  // the user's extra compile options (hipRTC and the fused build alike)
   std::vector<char> code;  // gfx950 code object
   // per-device loaded module / function (lazily, on first launch)
   hipFunction_t function(int device);

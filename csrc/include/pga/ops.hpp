@@ -38,7 +38,21 @@ uint32_t launch_grid(uint64_t S, uint32_t per_block);
 // same, capped at the kernel's resident blocks per CU (hipOccupancy...) so a
 // persistent grid-stride launch never leaves a partial second wave
 uint32_t launch_grid_occ(uint64_t S, uint32_t per_block, const void* kernel);
-uint32_t occupancy_blocks(const void* kernel, int block);
+uint32_t occupancy_blocks(const void* kernel, int block, size_t dyn_lds = 0);
+// Launch geometry of the two-phase kernels (binary_gen_tp, tp.hpp
+// tp_block_range): one 16-wave block per CU of an island's share of the
+// device when every wave breeds at least one 64-child unit, else 4-wave
+// blocks on an occupancy-sized grid with breed units of `unit` children (a
+// power of two >= ng = children per step) small enough to reach every
+// resident wave; `lds` = the dynamic LDS bytes.  Launchers store `unit` in
+// GenArgs::tp_unit.
+struct TpGeom {
+  uint32_t grid, block, lds, unit;
+};
+TpGeom tp_geometry(uint64_t S, uint32_t islands, const void* kernel, uint32_t ng, uint32_t pseg = 7);
+// the same from the resident 4-wave blocks per CU (occ4; module kernels)
+TpGeom tp_geometry_occ(uint64_t S, uint32_t islands, uint32_t occ4, uint32_t ng, uint32_t pseg = 7);
+uint32_t tp_dyn_lds_bytes(uint32_t nw, uint32_t pseg = 7);
 int device_cu_count();
 // raise a kernel's dynamic-LDS limit to what its static LDS leaves of the
 // CU's 160 KiB; returns that many bytes

@@ -151,29 +151,55 @@ __device__ __forceinline__ void tp_select_segment(const GenArgs& a, uint32_t beg
   }
 }
 
-// Work distribution of the transposed kernels: wave w of the grid breeds the
-// contiguous children [w per, (w + 1) per), per = ceil(S / W) rounded up to
-// a multiple of the children per step (NG).  Equal static shares leave a
-// tail: a SIMD issues oldest-wave-first, so the first-dispatched eighth of
-// the waves ends at ~54 us on average and the last at ~74 (phase clocks,
-// round 3), and the kernel's last ~20 us run on a thinning grid.  Two ways
-// to balance it were measured and dropped (tools/gpu_exp3.sh, gpu_exp4.sh):
-//   - dynamic units of 128 children pulled from 64 ticket heads, each on its
-//     own 128-B line: +14 us per generation of device-scope atomic latency
-//     (one shared line for every ticket: 10x the kernel);
-//   - shares skewed by dispatch order (1 +- s): the young waves still ended
-//     last (s = 0.15 moved the first eighth's mean end 54 -> 58 us, the last
-//     eighth's not at all); +3 us on the headline, +4 us on Rastrigin.
-__device__ __forceinline__ void tp_wave_range(uint32_t S, uint32_t NG, uint32_t& wbegin, uint32_t& wend,
-                                              uint32_t& first) {
-  constexpr uint32_t NW = kBlock / 64;
-  const uint64_t W = (uint64_t)gridDim.x * NW, w = (uint64_t)blockIdx.x * NW + (threadIdx.x >> 6);
-  uint64_t per = (S + W - 1) / W;
-  per = (per + NG - 1) / NG * NG;
-  wbegin = (uint32_t)(w * per < S ? w * per : S);
-  wend = (uint32_t)(wbegin + per < S ? wbegin + per : S);
-  const uint64_t f = (uint64_t)blockIdx.x * NW * per;
-  first = (uint32_t)(f < S ? f : S);
+// Work distribution of the two-phase kernels (binary_gen_tp, real_gen_tp):
+// BLOCK shares with CU-local dynamic breed units.  Block b owns the contiguous children
+// [b per, (b + 1) per), per = ceil(S / grid) rounded up to whole UNITS of
+// U = GenArgs::tp_unit children (64: one batch; small populations use fewer,
+// so that every wave gets a unit), processed in ROUNDS of at most
+// tp_par_cap(nw) children: the waves pull the round's 256-child tournament
+// segments from one LDS counter, then its units from another until none is
+// left; a unit waits for its segment's ready flag (binary_gen_tp: no block
+// barrier between the phases; real_gen_tp: one barrier).  The headline launch is one
+// 16-wave block per CU (its LDS admits no second), so the counter balances
+// every wave slot of the CU: the oldest-first issue order only decides WHICH
+// wave breeds a unit, and the last ~20 us of thinning grid that equal static
+// shares left (phase clocks, round 3) shrink to the last unit of each CU.
+// The RNG is keyed per child, so any assignment is bit-identical.  (Round 3
+// measured two device-scope balancers and dropped both: 128-child units from
+// 64 global ticket heads cost +14 us of atomic latency; shares skewed by
+// dispatch order did not move the young waves.)
+constexpr uint32_t kTpMaxWaves = 16;
+// parents per round: pseg tournament segments per 4 waves (7; 6 for kernels
+// with more static LDS)
+__host__ __device__ constexpr uint32_t tp_par_cap(uint32_t nw, uint32_t pseg = 7) {
+  return nw / 4u * pseg * kSegBatches * 64u;
+}
+// dynamic LDS of a block of nw waves: records [nw][2][64][2] uint4, the
+// round's parents [tp_par_cap] uint2
+__host__ __device__ constexpr uint32_t tp_dyn_lds(uint32_t nw, uint32_t pseg = 7) {
+  return nw * 4096u + tp_par_cap(nw, pseg) * 8u;
+}
+static_assert(tp_par_cap(4) % (kSegBatches * 64) == 0, "rounds hold whole segments");
+constexpr uint32_t kTpMaxSegs = tp_par_cap(kTpMaxWaves) / (kSegBatches * 64);  // tournament segments per round
+
+// Breed prefetch depth: parent rows are loaded PD steps ahead (<= 3; a unit
+// must hold at least PD steps, so PD <= GS = the steps of a 64-child unit)
+#ifndef PGA_TP_PD
+#define PGA_TP_PD 2
+#endif
+__host__ __device__ constexpr uint32_t tp_prefetch_depth(uint32_t gs) { return gs < PGA_TP_PD ? gs : PGA_TP_PD; }
+
+__device__ __forceinline__ uint32_t tp_unit(const GenArgs& a, uint32_t NG) {
+  const uint32_t u = a.tp_unit, lo = NG * tp_prefetch_depth(64u / NG);
+  return u >= lo && u <= 64u && (u & (u - 1u)) == 0u ? u : 64u;
+}
+
+__device__ __forceinline__ void tp_block_range(uint32_t S, uint32_t U, uint32_t& bbegin, uint32_t& bend) {
+  uint64_t per = (S + (uint64_t)gridDim.x - 1) / gridDim.x;
+  per = (per + U - 1) / U * U;
+  const uint64_t b = (uint64_t)blockIdx.x * per;
+  bbegin = (uint32_t)(b < S ? b : S);
+  bend = (uint32_t)(bbegin + per < S ? bbegin + per : S);
 }
 
 }  // namespace dev

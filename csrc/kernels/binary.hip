@@ -43,6 +43,15 @@ uint32_t go(K kernel, const GenArgs& a, unsigned long long* parts, uint32_t gpb,
   return grid;
 }
 
+template <typename K>
+uint32_t go_tp(K kernel, const GenArgs& a0, unsigned long long* parts, hipStream_t s) {
+  const TpGeom t = tp_geometry(a0.S, 1, (const void*)kernel, 64 / group_size(a0.chunks));
+  GenArgs a = a0;
+  a.tp_unit = t.unit;
+  hipLaunchKernelGGL(kernel, t.grid, t.block, t.lds, s, a, parts);
+  return t.grid;
+}
+
 template <int GS, int OBJ>
 uint32_t launch_mode(int mode, const GenArgs& a, unsigned long long* parts, hipStream_t s) {
   constexpr uint32_t gpb = kBlock / GS;
@@ -68,20 +77,19 @@ uint32_t launch_mode(int mode, const GenArgs& a, unsigned long long* parts, hipS
         if constexpr (OBJ == OBJ_KNAPSACK && GS >= 4 && GS <= 32) {
           if (a.knap_tab != nullptr) {  // integer-exact instance: the matrix-core evaluation
             if (full) {
-              if (dense) return go(binary_gen_tp<GS, kObjKnapMfma, true, true>, a, parts, kBlock, s);
-              return go(binary_gen_tp<GS, kObjKnapMfma, true, false>, a, parts, kBlock, s);
+              if (dense) return go_tp(binary_gen_tp<GS, kObjKnapMfma, true, true>, a, parts, s);
+              return go_tp(binary_gen_tp<GS, kObjKnapMfma, true, false>, a, parts, s);
             }
-            if (dense) return go(binary_gen_tp<GS, kObjKnapMfma, false, true>, a, parts, kBlock, s);
-            return go(binary_gen_tp<GS, kObjKnapMfma, false, false>, a, parts, kBlock, s);
+            if (dense) return go_tp(binary_gen_tp<GS, kObjKnapMfma, false, true>, a, parts, s);
+            return go_tp(binary_gen_tp<GS, kObjKnapMfma, false, false>, a, parts, s);
           }
         }
-        // one block = 4 waves x 64 children per batch
         if (full) {
-          if (dense) return go(binary_gen_tp<GS, OBJ, true, true>, a, parts, kBlock, s);
-          return go(binary_gen_tp<GS, OBJ, true, false>, a, parts, kBlock, s);
+          if (dense) return go_tp(binary_gen_tp<GS, OBJ, true, true>, a, parts, s);
+          return go_tp(binary_gen_tp<GS, OBJ, true, false>, a, parts, s);
         }
-        if (dense) return go(binary_gen_tp<GS, OBJ, false, true>, a, parts, kBlock, s);
-        return go(binary_gen_tp<GS, OBJ, false, false>, a, parts, kBlock, s);
+        if (dense) return go_tp(binary_gen_tp<GS, OBJ, false, true>, a, parts, s);
+        return go_tp(binary_gen_tp<GS, OBJ, false, false>, a, parts, s);
       }
       return go(binary_kernel<GS, OBJ, MODE_GEN>, a, parts, gpb, s);
     }
@@ -109,7 +117,7 @@ uint32_t launch_obj(int mode, const GenArgs& a, unsigned long long* parts, hipSt
 // experiment builds: mean per-wave cycles of the tournament / breed phases of
 // the last binary_gen_tp launch (bench/gen_bench.cpp prints it)
 extern "C" void pga_tp_timing_dump(uint32_t nwaves) {
-  static unsigned long long h[kMaxGrid * 4][8];
+  static unsigned long long h[kMaxGrid * 4][8];  // per wave: blockIdx.x * waves + wave
   PGA_HIP_CHECK(hipMemcpyFromSymbol(h, HIP_SYMBOL(pga_tp_clk), sizeof(h)));
   double t = 0, b = 0, tot = 0, n = 0, mx = 0;
   unsigned long long rt_min = ~0ull, rt_max = 0, st_max = 0;

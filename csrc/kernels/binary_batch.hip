@@ -16,31 +16,28 @@ namespace pga {
 namespace {
 
 template <int GS, int OBJ>
-uint32_t batch_go(const GenBatch& b, uint32_t n, uint64_t S, bool full, bool dense, hipStream_t s) {
+uint32_t batch_go(GenBatch& b, uint32_t n, uint64_t S, bool full, bool dense, hipStream_t s) {
   const void* k = full ? (dense ? (const void*)binary_gen_tp_batch<GS, OBJ, true, true>
                                 : (const void*)binary_gen_tp_batch<GS, OBJ, true, false>)
                        : (dense ? (const void*)binary_gen_tp_batch<GS, OBJ, false, true>
                                 : (const void*)binary_gen_tp_batch<GS, OBJ, false, false>);
-  // the device's resident blocks split between the islands
-  const uint64_t need = (S + kBlock - 1) / kBlock;
-  uint64_t cap = (uint64_t)device_cu_count() * occupancy_blocks(k, kBlock) / n;
-  if (cap < 1) cap = 1;
-  if (cap > kMaxGrid) cap = kMaxGrid;
-  const uint32_t gx = (uint32_t)(need < cap ? need : cap);
-  const dim3 grid(gx, n);
+  // the device split between the islands (tp_geometry)
+  const TpGeom t = tp_geometry(S, n, k, 64 / GS);
+  for (uint32_t i = 0; i < n; ++i) b.a[i].tp_unit = t.unit;
+  const dim3 grid(t.grid, n);
   if (full) {
-    if (dense) hipLaunchKernelGGL((binary_gen_tp_batch<GS, OBJ, true, true>), grid, kBlock, 0, s, b);
-    else hipLaunchKernelGGL((binary_gen_tp_batch<GS, OBJ, true, false>), grid, kBlock, 0, s, b);
+    if (dense) hipLaunchKernelGGL((binary_gen_tp_batch<GS, OBJ, true, true>), grid, t.block, t.lds, s, b);
+    else hipLaunchKernelGGL((binary_gen_tp_batch<GS, OBJ, true, false>), grid, t.block, t.lds, s, b);
   } else {
-    if (dense) hipLaunchKernelGGL((binary_gen_tp_batch<GS, OBJ, false, true>), grid, kBlock, 0, s, b);
-    else hipLaunchKernelGGL((binary_gen_tp_batch<GS, OBJ, false, false>), grid, kBlock, 0, s, b);
+    if (dense) hipLaunchKernelGGL((binary_gen_tp_batch<GS, OBJ, false, true>), grid, t.block, t.lds, s, b);
+    else hipLaunchKernelGGL((binary_gen_tp_batch<GS, OBJ, false, false>), grid, t.block, t.lds, s, b);
   }
   PGA_HIP_CHECK(hipGetLastError());
-  return gx;
+  return t.grid;
 }
 
 template <int GS>
-uint32_t batch_obj(int obj, const GenBatch& b, uint32_t n, uint64_t S, bool full, bool dense, hipStream_t s) {
+uint32_t batch_obj(int obj, GenBatch& b, uint32_t n, uint64_t S, bool full, bool dense, hipStream_t s) {
   switch (obj) {
     case OBJ_ONEMAX: return batch_go<GS, OBJ_ONEMAX>(b, n, S, full, dense, s);
     case OBJ_LEADING_ONES: return batch_go<GS, OBJ_LEADING_ONES>(b, n, S, full, dense, s);

@@ -506,16 +506,17 @@ uint32_t go(const GenArgs& a, unsigned long long* parts, hipStream_t s) {
 
 // ---------------------------------------------------------------------------
 // The hot generation kernel: transposed tournaments (the binary_gen_tp design,
-// binary.hip).  A wave owns a contiguous range of children and breeds
-// NG = 64/GS of them per STEP; steps come in BATCHES of GS steps = 64
-// children.  The range is cut into SEGMENTS of up to kSegBatches batches:
+// binary_dev.hpp).  A wave breeds NG = 64/GS children per STEP; a block owns
+// a contiguous share of the population, in rounds (tp.hpp tp_block_range):
 //   TOURNAMENTS  tp_select_segment (tp.hpp): one lane per child, every f32
-//                score load of the segment in flight together
-//   BREED        per batch, RESOLVE (one lane per child): the misc block
+//                score load of a 256-child segment in flight together
+//   BREED        after one block barrier, UNITS of U <= 64 children pulled
+//                from the block's LDS counter; per unit, RESOLVE (one lane
+//                per child): the misc block
 //                (crossover test, cut points / arithmetic u, mutation count
 //                K), the first min(K, 3) distinct mutation positions and
 //                their values (gaussian z by gauss_z) -> a 32-byte child
-//                RECORD in the wave's LDS ring (2 batches); per step: parent
+//                RECORD in the wave's LDS ring (2 units); per step: parent
 //                rows loaded one step ahead, crossover (BLX: one Philox block
 //                per lane), the record's mutations (K > 3: the group
 //                continues the sequence), objective, group butterfly, stores.
@@ -575,25 +576,24 @@ __device__ __forceinline__ void rot_tile4(float* xw, const float* ms, float z[4]
   rot_tile4_sync();
 }
 
-#ifndef PGA_RTP_WAVES
-#define PGA_RTP_WAVES 4
-#endif
-
-
 template <int GS, int OBJ, bool ROT>
-__global__ __launch_bounds__(kBlock, PGA_RTP_WAVES) void real_gen_tp(GenArgs a, unsigned long long* best_parts) {
+__global__ __launch_bounds__(kTpMaxWaves * 64) void real_gen_tp(GenArgs a, unsigned long long* best_parts) {
   static_assert(!ROT || GS == 4 || GS == 8, "wave-local rotation: 16 or 32 padded dims");
   resolve_gen(a);
   a.objective = OBJ;  // compile-time objective: the term switches fold away
-  constexpr uint32_t NW = kBlock / 64;
-  constexpr uint32_t NG = 64 / GS;  // children per wave per step
+  const uint32_t NW = blockDim.x >> 6;  // 4 or 16 waves (tp_geometry)
+  constexpr uint32_t NG = 64 / GS;      // children per wave per step
+  constexpr uint32_t PD = tp_prefetch_depth(GS);  // steps of parent rows in flight (tp.hpp)
+  constexpr uint32_t PSEG = ROT ? 6 : 7;  // tp_par_cap segments: the rotation tiles take static LDS
   constexpr bool EVALS = OBJ != OBJ_NONE;
-  __shared__ uint4 lds_rec[NW][2][64][2];           // per wave: 2 batches x 64 records x 32 B
-  __shared__ uint2 lds_par[NW][kSegBatches * 64];  // per wave: the segment's (parent A, parent B)
+  // dynamic LDS: per wave 2 units x 64 records x 32 B, then the round's parents
+  uint4(*lds_rec)[2][64][2] = (uint4(*)[2][64][2])pga_dyn_lds;
+  uint2* lds_par = (uint2*)(pga_dyn_lds + NW * 4096u);
   __shared__ uint32_t lds_thr[kMutCap];
   __shared__ uint32_t lds_el[kTpMaxElite];  // elite sources
-  __shared__ unsigned long long lds_red[NW];
-  __shared__ __attribute__((aligned(16))) float lds_rot[ROT ? (NW + 2) * 16 * kRotTW : 1];  // wave tiles + M
+  __shared__ unsigned long long lds_red[kTpMaxWaves];
+  __shared__ uint32_t lds_next;  // the round's next unbred unit
+  __shared__ __attribute__((aligned(16))) float lds_rot[ROT ? (kTpMaxWaves + 2) * 16 * kRotTW : 1];  // wave tiles + M
 
   const uint32_t lane = lane_id(), wid = threadIdx.x >> 6;
   const uint32_t q = lane & (GS - 1), gbase = lane & ~(uint32_t)(GS - 1), g = lane / GS;
@@ -629,49 +629,60 @@ __global__ __launch_bounds__(kBlock, PGA_RTP_WAVES) void real_gen_tp(GenArgs a, 
 #define RROW(base, row, ch) (*(float4*)((char*)(base) + ((uint32_t)(row) * rb + (uint32_t)(ch) * 16u)))
 #define RELEM(T, base, i) (*(T*)((char*)(base) + (uint32_t)(i) * (uint32_t)sizeof(T)))
 
-  uint32_t wbegin, wend, bfirst;  // this wave's children (tp.hpp)
-  tp_wave_range(S, NG, wbegin, wend, bfirst);
+  const uint32_t U = tp_unit(a, NG);  // children per breed unit (tp.hpp)
+  uint32_t bbegin, bend;              // this block's children
+  tp_block_range(S, U, bbegin, bend);
+  const uint32_t pcap = tp_par_cap(NW, PSEG);
 
-  float* xw = lds_rot + (ROT ? wid * 16 * kRotTW : 0);  // this wave's X/Z tile
-  float* ms = lds_rot + (ROT ? NW * 16 * kRotTW : 0);   // M[n][k], block-shared
+  float* xw = lds_rot + (ROT ? wid * 16 * kRotTW : 0);          // this wave's X/Z tile
+  float* ms = lds_rot + (ROT ? kTpMaxWaves * 16 * kRotTW : 0);  // M[n][k], block-shared
   if (ROT)
-    for (uint32_t i = threadIdx.x; i < 32 * kRotTW; i += kBlock) {
+    for (uint32_t i = threadIdx.x; i < 32 * kRotTW; i += blockDim.x) {
       const uint32_t n = i / kRotTW, k = i % kRotTW;
       ms[i] = (n < L && k < L) ? a.obj_data[n * L + k] : 0.f;
     }
-  // elite sources of children [0, n_elite), for the blocks that hold any of them
-  if (a.n_elite > 0 && bfirst < a.n_elite) {
+  // elite sources of children [0, n_elite), for the block that holds any of them
+  if (a.n_elite > 0 && bbegin < a.n_elite) {
     if (a.elite_idx) {
-      for (uint32_t i = threadIdx.x; i < a.n_elite; i += kBlock) lds_el[i] = a.elite_idx[i];
+      for (uint32_t i = threadIdx.x; i < a.n_elite; i += blockDim.x) lds_el[i] = a.elite_idx[i];
     } else {
-      unsigned long long b = block_reduce_parts(a.best_cur, a.n_best_cur, lds_red);
+      unsigned long long b = block_reduce_parts_n(a.best_cur, a.n_best_cur, lds_red, NW);
       if (threadIdx.x == 0) lds_el[0] = (uint32_t)best_index(b);
     }
   }
   if (per_gene)
-    for (uint32_t i = threadIdx.x; i < kMutCap; i += kBlock) lds_thr[i] = a.mut_thr[i];
-  __syncthreads();
+    for (uint32_t i = threadIdx.x; i < kMutCap; i += blockDim.x) lds_thr[i] = a.mut_thr[i];
+  if (threadIdx.x == 0) lds_next = 0;
 
   unsigned long long my_best = 0;
   ScoreStats st;
   uint4(*rec)[64][2] = lds_rec[wid];
-  uint2* par = lds_par[wid];
   static_assert(sizeof(lds_rec[0]) >= kSegBatches * 64 * sizeof(uint4), "contestant staging");
-  for (uint32_t begin = wbegin; begin < wend; begin += kSegBatches * 64u) {  // wave-uniform
-    const uint32_t end = begin + kSegBatches * 64u < wend ? begin + kSegBatches * 64u : wend;
-    const uint32_t nsteps = (end - begin + NG - 1) / NG;
-    const uint32_t nbatch = (end - begin + 63) / 64;
+  for (uint32_t rbeg = bbegin; rbeg < bend; rbeg += pcap) {  // block-uniform rounds
+    const uint32_t rend = rbeg + pcap < bend ? rbeg + pcap : bend;
+    const uint32_t nb = (rend - rbeg + U - 1) / U;                                  // the round's units
+    const uint32_t nseg = (rend - rbeg + kSegBatches * 64 - 1) / (kSegBatches * 64);  // its tournament segments
+    __syncthreads();  // tables / elites / M / counter visible; the previous round's records and parents released
 
-    // TOURNAMENTS of the whole segment (contestants wait in the record ring),
+    // TOURNAMENTS of the round (contestants wait in the wave's record ring),
     // on the quantized u16 keys when the objective scores the children here
-    tp_select_segment<EVALS ? TP_QKEY16 : TP_F32>(a, begin, end, lane, &rec[0][0][0], par);
+    for (uint32_t sg = wid; sg < nseg; sg += NW) {
+      const uint32_t begin = rbeg + sg * kSegBatches * 64u;
+      const uint32_t end = begin + kSegBatches * 64u < rend ? begin + kSegBatches * 64u : rend;
+      tp_select_segment<EVALS ? TP_QKEY16 : TP_F32>(a, begin, end, lane, &rec[0][0][0],
+                                                    lds_par + sg * kSegBatches * 64u);
+    }
+    __syncthreads();  // every parent of the round in LDS
 
-    // RESOLVE: parents, crossover plan, mutation positions and draws of batch B -> records
-#define PGA_RTP_RESOLVE(B)                                                                                   \
+    // RESOLVE: parents, crossover plan, mutation positions and draws of the
+    // round's unit BI -> the records of ring slot SL
+#define PGA_RTP_RESOLVE(BI, SL)                                                                              \
   {                                                                                                          \
-    const uint32_t tc = begin + (B) * 64u + lane;                                                            \
-    const uint32_t cc = tc < end ? tc : end - 1;                                                             \
-    const uint2 pp = par[(B) * 64u + lane];                                                                  \
+    const uint32_t bs_ = rbeg + (BI) * U;                                                                    \
+    const uint32_t be_ = bs_ + U < rend ? bs_ + U : rend;                                                    \
+    const uint32_t tc = bs_ + lane;                                                                          \
+    const uint32_t cc = tc < be_ ? tc : be_ - 1;                                                             \
+    const uint2 pp = lds_par[cc - rbeg];                                                                     \
     uint32_t pa = pp.x;                                                                                      \
     const u32x4 misc = real_misc<true>(a.key, cc);                                                           \
     const bool elite = tc < a.n_elite;                                                                       \
@@ -712,35 +723,56 @@ __global__ __launch_bounds__(kBlock, PGA_RTP_WAVES) void real_gen_tp(GenArgs a, 
     }                                                                                                        \
     const uint32_t meta =                                                                                    \
         (K > 255u ? 255u : K) | ((jn > 0xFFFFu ? 0xFFFFu : jn) << 8) | (xo ? 1u << 30 : 0u) | (elite ? 1u << 31 : 0u); \
-    uint4(*r)[2] = rec[(B) & 1u];                                                                            \
+    uint4(*r)[2] = rec[(SL)];                                                                                \
     r[lane][0] = make_uint4(pa, pb, cut, meta);                                                              \
     r[lane][1] = make_uint4(posw, d0, d1, d2);                                                               \
   }
 
-    // prologue: batch 0 resolved, rows of step 0 in flight
-    PGA_RTP_RESOLVE(0u)
-    float4 A0, B0, A1, B1;
-    {
-      const uint4 r = rec[0][g][0];
-      A0 = RROW(cur, r.x, qq);
-      B0 = RROW(cur, r.y, qq);
-    }
+    // BREED: the round's units in ticket order from the block's counter, as
+    // two cursors (binary_dev.hpp binary_gen_tp_body): the LOAD cursor
+    // issues the parent rows PD steps ahead of the BREED cursor and RESOLVEs
+    // a unit into the other ring slot when it enters it; every vector memory
+    // operation is unconditional (an exhausted load cursor re-reads the breed
+    // cursor's rows; the children past S, at the end only, write the padding)
+    uint32_t tk = 0;
+    if (lane == 0) tk = __hip_atomic_fetch_add(&lds_next, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    const uint32_t b0 = __builtin_amdgcn_readfirstlane(tk);  // the wave's first unit
+    if (b0 < nb) {
+      if (lane == 0) tk = __hip_atomic_fetch_add(&lds_next, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      uint32_t bn = __builtin_amdgcn_readfirstlane(tk);  // the next ticket (>= nb: none)
+      PGA_RTP_RESOLVE(b0, 0u)
+      uint32_t slot = 0, i = 0, bs = rbeg + b0 * U;  // breed cursor
+      uint32_t nst = ((bs + U < rend ? bs + U : rend) - bs + NG - 1) / NG;
+      uint32_t lslot = 0, li = 0, lbs = bs, lnst = nst;  // load cursor
+      bool lpend = false, lmore = true, done = false;
 
-    // one STEP: every vector-memory operation is unconditional (the tail of
-    // the last wave writes the padding rows past S)
-#define PGA_RTP_STEP(t, XA, XB, YA, YB)                                                                     \
+#define PGA_RTP_LOAD(YA, YB)                                                                                \
   {                                                                                                         \
-    const uint32_t b = (t) / GS, i = (t) & (GS - 1);                                                        \
-    if ((((t) + 1) & (GS - 1)) == 0u && b + 1 < nbatch) PGA_RTP_RESOLVE(b + 1)                              \
-    {                                                                                                       \
-      /* parent rows of step t+1 (the last step re-reads its own) */                                        \
-      const uint32_t tn = (t) + 1 < nsteps ? (t) + 1 : (t);                                                 \
-      const uint4 r = rec[(tn / GS) & 1u][(tn & (GS - 1)) * NG + g][0];                                     \
-      YA = RROW(cur, r.x, qq);                                                                              \
-      YB = RROW(cur, r.y, qq);                                                                              \
+    if (lpend) { /* entering the next unit */                                                               \
+      PGA_RTP_RESOLVE(bn, lslot ^ 1u)                                                                       \
+      lslot ^= 1u;                                                                                          \
+      li = 0;                                                                                               \
+      lbs = rbeg + bn * U;                                                                                  \
+      lnst = ((lbs + U < rend ? lbs + U : rend) - lbs + NG - 1) / NG;                                       \
+      lpend = false;                                                                                        \
+      if (lane == 0)                                                                                        \
+        tk = __hip_atomic_fetch_add(&lds_next, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);         \
+      bn = __builtin_amdgcn_readfirstlane(tk);                                                              \
     }                                                                                                       \
-    const uint32_t c = begin + (t) * NG + g;                                                                \
-    const uint4 r0 = rec[b & 1u][i * NG + g][0];                                                            \
+    const uint4 r = rec[lmore ? lslot : slot][(lmore ? li : i) * NG + g][0];                                \
+    YA = RROW(cur, r.x, qq);                                                                                \
+    YB = RROW(cur, r.y, qq);                                                                                \
+    if (lmore && ++li == lnst) {                                                                            \
+      lpend = bn < nb;                                                                                      \
+      lmore = lpend;                                                                                        \
+    }                                                                                                       \
+  }
+
+#define PGA_RTP_STEP(XA, XB, YA, YB)                                                                        \
+  {                                                                                                         \
+    PGA_RTP_LOAD(YA, YB)                                                                                    \
+    const uint32_t c = bs + i * NG + g;                                                                     \
+    const uint4 r0 = rec[slot][i * NG + g][0];                                                              \
     const uint32_t meta = r0.w;                                                                             \
     const float A_[4] = {XA.x, XA.y, XA.z, XA.w}, B_[4] = {XB.x, XB.y, XB.z, XB.w};                         \
     float v[4];                                                                                             \
@@ -751,7 +783,7 @@ __global__ __launch_bounds__(kBlock, PGA_RTP_WAVES) void real_gen_tp(GenArgs a, 
     }                                                                                                       \
     const uint32_t K = meta & 0xFFu;                                                                        \
     if (K > 0u) { /* group-uniform */                                                                       \
-      const uint4 r1 = rec[b & 1u][i * NG + g][1];                                                          \
+      const uint4 r1 = rec[slot][i * NG + g][1];                                                            \
       uint32_t mm = 0;                                                                                      \
       _Pragma("unroll") for (uint32_t k = 0; k < 3; ++k) {                                                  \
         const uint32_t p = (r1.x >> (8u * k)) & 0xFFu;                                                      \
@@ -789,42 +821,88 @@ __global__ __launch_bounds__(kBlock, PGA_RTP_WAVES) void real_gen_tp(GenArgs a, 
       my_best = pk > my_best ? pk : my_best;                                                                \
       st.add_if(q == 0u && c < S, sc);                                                                      \
     }                                                                                                       \
+    if (++i == nst) {                                                                                       \
+      if (lbs == bs) { /* the load cursor never left this unit: it was the wave's last */                   \
+        done = true;                                                                                        \
+      } else {                                                                                              \
+        slot ^= 1u;                                                                                         \
+        i = 0;                                                                                              \
+        bs = lbs;                                                                                           \
+        nst = lnst;                                                                                         \
+      }                                                                                                     \
+    }                                                                                                       \
   }
 
-    uint32_t t = 0;
-    for (; t + 1 < nsteps; t += 2) {  // static row-register rotation
-      PGA_RTP_STEP(t, A0, B0, A1, B1)
-      PGA_RTP_STEP(t + 1, A1, B1, A0, B0)
-    }
-    if (t < nsteps) PGA_RTP_STEP(t, A0, B0, A1, B1)
-#undef PGA_RTP_RESOLVE
+      float4 A0, B0, A1, B1, A2, B2, A3, B3;  // PD + 1 register sets, rotated statically
+      (void)A2; (void)B2; (void)A3; (void)B3;
+      if constexpr (PD == 1) {
+        PGA_RTP_LOAD(A0, B0)
+        for (;;) {
+          PGA_RTP_STEP(A0, B0, A1, B1)
+          if (done) break;
+          PGA_RTP_STEP(A1, B1, A0, B0)
+          if (done) break;
+        }
+      } else if constexpr (PD == 2) {
+        PGA_RTP_LOAD(A0, B0)
+        PGA_RTP_LOAD(A1, B1)
+        for (;;) {
+          PGA_RTP_STEP(A0, B0, A2, B2)
+          if (done) break;
+          PGA_RTP_STEP(A1, B1, A0, B0)
+          if (done) break;
+          PGA_RTP_STEP(A2, B2, A1, B1)
+          if (done) break;
+        }
+      } else {
+        PGA_RTP_LOAD(A0, B0)
+        PGA_RTP_LOAD(A1, B1)
+        PGA_RTP_LOAD(A2, B2)
+        for (;;) {
+          PGA_RTP_STEP(A0, B0, A3, B3)
+          if (done) break;
+          PGA_RTP_STEP(A1, B1, A0, B0)
+          if (done) break;
+          PGA_RTP_STEP(A2, B2, A1, B1)
+          if (done) break;
+          PGA_RTP_STEP(A3, B3, A2, B2)
+          if (done) break;
+        }
+      }
 #undef PGA_RTP_STEP
+#undef PGA_RTP_LOAD
+    }
+#undef PGA_RTP_RESOLVE
+    __syncthreads();  // every wave out of the round's counter before it is reset
+    if (threadIdx.x == 0) lds_next = 0;
   }
 #undef RROW
 #undef RELEM
-  if constexpr (EVALS) {
-    unsigned long long bb = block_max_u64(my_best, lds_red);
-    if (threadIdx.x == 0 && best_parts) best_parts[blockIdx.x] = bb;
-    if (best_parts && a.stats_parts) block_stats_store(st, a.stats_parts);
+  if (EVALS && best_parts) {  // block-uniform
+    unsigned long long bb = block_max_u64_n(my_best, lds_red, NW);
+    if (threadIdx.x == 0) best_parts[blockIdx.x] = bb;
+    if (a.stats_parts) block_stats_store_n(st, a.stats_parts, NW);
   }
 }
 
 template <typename K>
-uint32_t go_tp(K kernel, const GenArgs& a, unsigned long long* parts, hipStream_t s) {
-  const uint32_t grid = launch_grid_occ(a.S, kBlock, (const void*)kernel);
-  hipLaunchKernelGGL(kernel, grid, kBlock, 0, s, a, parts);
-  return grid;
+uint32_t go_tp(K kernel, const GenArgs& a0, unsigned long long* parts, hipStream_t s, bool rot) {
+  const TpGeom t = tp_geometry(a0.S, 1, (const void*)kernel, 64 / group_size(a0.chunks), rot ? 6 : 7);
+  GenArgs a = a0;
+  a.tp_unit = t.unit;
+  hipLaunchKernelGGL(kernel, t.grid, t.block, t.lds, s, a, parts);
+  return t.grid;
 }
 
-// Below ~192 children per CU the transposed kernel has too few waves (one
-// 64-child batch each) to hide its GS dependent breed steps and the generic
-// kernel is faster (bench/real_size_sweep.py: SumGenes-100 at S = 40,000
-// 39.4 vs 35.3 us, Rastrigin-30 24.3 vs 20.9 us; from S = 100,000 the
-// transposed kernel wins, 43 vs 75 and 28 vs 39 us).  PGA_TP_MIN_S overrides
-// (the tests pin 0 to cover the transposed kernel at small sizes).
+// Below ~64 children per CU the two-phase kernel has too few units to fill
+// the device and the generic kernel is as fast (bench/real_size_sweep.py,
+// round 4, breed units of U < 64 children: SumGenes-100 at S = 40,000 20.8 vs
+// 35.2 us generic, Rastrigin-30 18.8 vs 20.6; at S = 10,000 14.2 vs 15.2 and
+// 14.2 vs 13.0).  PGA_TP_MIN_S overrides (the tests pin 0 to cover the
+// two-phase kernel at small sizes).
 uint64_t real_tp_min_population() {
   if (const char* e = std::getenv("PGA_TP_MIN_S")) return std::strtoull(e, nullptr, 10);
-  return 192ull * (uint64_t)device_cu_count();
+  return 64ull * (uint64_t)device_cu_count();
 }
 
 bool real_tp_eligible(const GenArgs& a, uint32_t GS, bool rot) {
@@ -848,26 +926,26 @@ uint32_t launch_tp(const GenArgs& a, unsigned long long* parts, hipStream_t s) {
   if constexpr (ROT) {
     if constexpr (GS == 4 || GS == 8) {
       switch (a.objective) {
-        case OBJ_SPHERE: return go_tp(real_gen_tp<GS, OBJ_SPHERE, true>, a, parts, s);
-        case OBJ_RASTRIGIN: return go_tp(real_gen_tp<GS, OBJ_RASTRIGIN, true>, a, parts, s);
-        case OBJ_ROSENBROCK: return go_tp(real_gen_tp<GS, OBJ_ROSENBROCK, true>, a, parts, s);
-        case OBJ_ACKLEY: return go_tp(real_gen_tp<GS, OBJ_ACKLEY, true>, a, parts, s);
-        case OBJ_GRIEWANK: return go_tp(real_gen_tp<GS, OBJ_GRIEWANK, true>, a, parts, s);
-        default: return go_tp(real_gen_tp<GS, OBJ_SCHWEFEL, true>, a, parts, s);
+        case OBJ_SPHERE: return go_tp(real_gen_tp<GS, OBJ_SPHERE, true>, a, parts, s, ROT);
+        case OBJ_RASTRIGIN: return go_tp(real_gen_tp<GS, OBJ_RASTRIGIN, true>, a, parts, s, ROT);
+        case OBJ_ROSENBROCK: return go_tp(real_gen_tp<GS, OBJ_ROSENBROCK, true>, a, parts, s, ROT);
+        case OBJ_ACKLEY: return go_tp(real_gen_tp<GS, OBJ_ACKLEY, true>, a, parts, s, ROT);
+        case OBJ_GRIEWANK: return go_tp(real_gen_tp<GS, OBJ_GRIEWANK, true>, a, parts, s, ROT);
+        default: return go_tp(real_gen_tp<GS, OBJ_SCHWEFEL, true>, a, parts, s, ROT);
       }
     }
     return 0;
   } else {
     switch (a.objective) {
-      case OBJ_SPHERE: return go_tp(real_gen_tp<GS, OBJ_SPHERE, false>, a, parts, s);
-      case OBJ_RASTRIGIN: return go_tp(real_gen_tp<GS, OBJ_RASTRIGIN, false>, a, parts, s);
-      case OBJ_ROSENBROCK: return go_tp(real_gen_tp<GS, OBJ_ROSENBROCK, false>, a, parts, s);
-      case OBJ_ACKLEY: return go_tp(real_gen_tp<GS, OBJ_ACKLEY, false>, a, parts, s);
-      case OBJ_GRIEWANK: return go_tp(real_gen_tp<GS, OBJ_GRIEWANK, false>, a, parts, s);
-      case OBJ_SCHWEFEL: return go_tp(real_gen_tp<GS, OBJ_SCHWEFEL, false>, a, parts, s);
-      case OBJ_LINEAR: return go_tp(real_gen_tp<GS, OBJ_LINEAR, false>, a, parts, s);
-      case OBJ_KNAPSACK_REAL: return go_tp(real_gen_tp<GS, OBJ_KNAPSACK_REAL, false>, a, parts, s);
-      default: return go_tp(real_gen_tp<GS, OBJ_NONE, false>, a, parts, s);
+      case OBJ_SPHERE: return go_tp(real_gen_tp<GS, OBJ_SPHERE, false>, a, parts, s, ROT);
+      case OBJ_RASTRIGIN: return go_tp(real_gen_tp<GS, OBJ_RASTRIGIN, false>, a, parts, s, ROT);
+      case OBJ_ROSENBROCK: return go_tp(real_gen_tp<GS, OBJ_ROSENBROCK, false>, a, parts, s, ROT);
+      case OBJ_ACKLEY: return go_tp(real_gen_tp<GS, OBJ_ACKLEY, false>, a, parts, s, ROT);
+      case OBJ_GRIEWANK: return go_tp(real_gen_tp<GS, OBJ_GRIEWANK, false>, a, parts, s, ROT);
+      case OBJ_SCHWEFEL: return go_tp(real_gen_tp<GS, OBJ_SCHWEFEL, false>, a, parts, s, ROT);
+      case OBJ_LINEAR: return go_tp(real_gen_tp<GS, OBJ_LINEAR, false>, a, parts, s, ROT);
+      case OBJ_KNAPSACK_REAL: return go_tp(real_gen_tp<GS, OBJ_KNAPSACK_REAL, false>, a, parts, s, ROT);
+      default: return go_tp(real_gen_tp<GS, OBJ_NONE, false>, a, parts, s, ROT);
     }
   }
 }

@@ -7,11 +7,15 @@
 #include <hip/hip_runtime.h>
 
 #include <cmath>
+#include <map>
 #include <mutex>
+#include <set>
+#include <tuple>
 #include <unordered_map>
 
 #include "pga/device.hpp"
 #include "pga/ops.hpp"
+#include "pga/tp.hpp"
 
 namespace pga {
 
@@ -36,17 +40,17 @@ uint32_t launch_grid(uint64_t S, uint32_t per_block) {
   return (uint32_t)(g == 0 ? 1 : g);
 }
 
-uint32_t occupancy_blocks(const void* kernel, int block) {
+uint32_t occupancy_blocks(const void* kernel, int block, size_t dyn_lds) {
   static std::mutex mu;
-  static std::unordered_map<uint64_t, int> cache;
+  static std::map<std::tuple<const void*, int, int, size_t>, int> cache;
   int dev = 0;
   PGA_HIP_CHECK(hipGetDevice(&dev));
-  const uint64_t key = (uint64_t)(uintptr_t)kernel * 64 + (uint64_t)dev;
+  const auto key = std::make_tuple(kernel, dev, block, dyn_lds);
   std::lock_guard<std::mutex> g(mu);
   auto it = cache.find(key);
   if (it != cache.end()) return (uint32_t)it->second;
   int n = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, kernel, block, 0) != hipSuccess || n <= 0) n = 1;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, kernel, block, dyn_lds) != hipSuccess || n <= 0) n = 1;
   cache[key] = n;
   return (uint32_t)n;
 }
@@ -65,6 +69,41 @@ size_t allow_dynamic_lds(const void* kernel) {
   const size_t avail = 160 * 1024 - at.sharedSizeBytes;
   PGA_HIP_CHECK(hipFuncSetAttribute(kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)avail));
   return avail;
+}
+
+TpGeom tp_geometry(uint64_t S, uint32_t islands, const void* kernel, uint32_t ng, uint32_t pseg) {
+  {  // the 16-wave launch's dynamic LDS is above the default limit
+    static std::mutex mu;
+    static std::set<std::pair<const void*, int>> raised;
+    int dev = 0;
+    PGA_HIP_CHECK(hipGetDevice(&dev));
+    std::lock_guard<std::mutex> g(mu);
+    if (raised.insert({kernel, dev}).second) (void)allow_dynamic_lds(kernel);
+  }
+  return tp_geometry_occ(S, islands, occupancy_blocks(kernel, 256, dev::tp_dyn_lds(4, pseg)), ng, pseg);
+}
+
+uint32_t tp_dyn_lds_bytes(uint32_t nw, uint32_t pseg) { return dev::tp_dyn_lds(nw, pseg); }
+
+TpGeom tp_geometry_occ(uint64_t S, uint32_t islands, uint32_t occ4, uint32_t ng, uint32_t pseg) {
+  if (islands == 0) islands = 1;
+  if (ng == 0 || ng > 64) ng = 64;
+  const uint32_t cus = (uint32_t)device_cu_count();
+  const uint32_t share = cus / islands > 0 ? cus / islands : 1;
+  // one 16-wave block per CU when every wave breeds at least one 64-child unit
+  if ((S + 63) / 64 >= (uint64_t)dev::kTpMaxWaves * share)
+    return {share, dev::kTpMaxWaves * 64, dev::tp_dyn_lds(dev::kTpMaxWaves, pseg), 64};
+  // else 4-wave blocks on the occupancy grid, with units small enough that
+  // every resident wave gets one (each unit costs U / ng dependent steps)
+  uint64_t cap = (uint64_t)cus * (occ4 > 0 ? occ4 : 1) / islands;
+  if (cap < 1) cap = 1;
+  if (cap > kMaxGrid) cap = kMaxGrid;
+  const uint64_t per_wave = (S + 4 * cap - 1) / (4 * cap);
+  uint32_t u = ng * dev::tp_prefetch_depth(64 / ng);  // a unit holds >= PD steps
+  while (u < 64 && u < per_wave) u *= 2;
+  const uint64_t need = (S + 4ull * u - 1) / (4ull * u);
+  const uint64_t g = need < cap ? need : cap;
+  return {(uint32_t)(g == 0 ? 1 : g), 256u, dev::tp_dyn_lds(4, pseg), u};
 }
 
 uint32_t launch_grid_occ(uint64_t S, uint32_t per_block, const void* kernel) {

@@ -89,6 +89,26 @@ def test_knapsack_matrix_cores_bitexact(L, scale, digits):
     assert torch.allclose(ref, g.scores.cpu(), rtol=1e-6, atol=1e-2)
 
 
+@pytest.mark.parametrize("S,L,sel,elitism", [(1048576, 1024, "tournament", 1), (1048576, 1024, "rank", 3),
+                                              (1600000, 1024, "tournament", 3), (1600000, 1024, "rank", 1),
+                                              (1900000, 256, "tournament", 1), (300000, 64, "roulette", 1),
+                                              (200000, 1024, "tournament", 2)])
+def test_headline_geometry_bitexact(S, L, sel, elitism):
+    """The hot kernel at the headline geometry, rows and scores against the
+    CPU backend over 2 generations: one 16-wave block per CU with ~16 batches
+    pulled per block (1M), 24 batches per block (1.6M), a block share above
+    one round's parent capacity (1.9M x 256 bits: two tournament / breed
+    rounds per block), and the 4-wave occupancy grid (200K).  Roulette runs
+    OneMax-64 so that the f32 prefix sums stay exact (< 2^24)."""
+    kw = dict(rank_pressure=1.7) if sel == "rank" else {}
+    g, c = pair(pga.models.OneMax(L), S, seed=5, selection=sel, elitism=elitism, **kw)
+    for _ in range(2):
+        g.run(1)
+        c.run(1)
+        same(g, c)
+    assert g.best_score() == c.best_score()
+
+
 @pytest.mark.parametrize("mut", [("bit_flip", 0.0), ("bit_flip", 0.05), ("bit_flip", 1.0), ("reset_one", 0.3)])
 def test_mutation_modes_bitexact(mut):
     name, rate = mut
@@ -202,7 +222,7 @@ def test_gpu_topk_matches_cpu(problem, sorted_):
 
 @pytest.mark.parametrize("sp", [1.25, 2.0])
 def test_rank_selection_bitexact(sp):
-    """Device rank order (hipcub stable radix sort of score keys) + integer
+    """Device rank order (native stable LSD radix sort of score keys) + integer
     rank sampling reproduce the CPU backend bit for bit, ties included."""
     g, c = pair(pga.models.OneMax(300), 5000, selection="rank", rank_pressure=sp, elitism=2)
     g.run(4)
