@@ -53,6 +53,10 @@ Island::Island(const Config& cfg, int device) : cfg_(cfg), device_(device) {
   }
   out_best_ = alloc(64);
   stats_ = alloc(4ull * (4 + 3 * 1024));
+  if (on_gpu() && cfg_.encoding == ENC_BINARY) {  // binary_gen_tp's pair-pool counters (stamp 0 = stale)
+    tp_pool_ = alloc(tp_pool_bytes(kMaxGrid));
+    PGA_HIP_CHECK(hipMemset(tp_pool_.ptr, 0, tp_pool_.bytes));
+  }
   if (cfg_.encoding == ENC_BINARY) {
     const uint32_t rem = cfg_.L - 128 * (chunks_ - 1);
     uint32_t m[4];
@@ -69,7 +73,7 @@ Island::~Island() {
   Buffer* all[] = {&rows_[0],   &rows_[1],     &scores_[0],   &scores_[1],  &best_[0],  &best_[1],   &mut_thr_,
                    &obj_data_[0], &obj_data_[1], &keys_[0], &keys_[1], &elite_idx_, &cumfit_, &cum_ws_, &roul_guide_, &topk_ws_, &stats_,
                    &out_best_,  &scratch_, &compat_rand_, &ev_parts_, &gen_dev_, &rank_order_, &rank_ws_, &qubo_qt_,
-                   &knap_tab_, &stats_parts_[0], &stats_parts_[1], &hist_, &qk_ws_};
+                   &knap_tab_, &stats_parts_[0], &stats_parts_[1], &hist_, &qk_ws_, &tp_pool_};
   drop_graph();
   if (cap_stream_) (void)hipStreamDestroy(cap_stream_);
   for (Buffer* b : all) {
@@ -294,6 +298,13 @@ GenArgs Island::make_args(int mode) {
   a.compat_rand = (float*)compat_rand_.ptr;
   a.n_elite = cfg_.n_elite;
   a.elite_idx = cfg_.n_elite > 1 ? (const uint32_t*)elite_idx_.ptr : nullptr;
+  if (mode == MODE_GEN && tp_pool_.ptr && !capturing_) {
+    // a stamp per launch (never 0: zeroed counters are stale); a graph
+    // replay would repeat its stamp, so captured generations run without
+    a.tp_pool = (unsigned long long*)tp_pool_.ptr;
+    if (++tp_seq_ == 0) ++tp_seq_;
+    a.tp_seq = tp_seq_;
+  }
   a.best_cur = (const unsigned long long*)best_[cur_].ptr;
   a.n_best_cur = n_best_[cur_];
   a.last_mask = last_mask_;
@@ -360,7 +371,10 @@ void Island::rebest() {
 }
 
 bool Island::real_qk() const {
-  return on_gpu() && cfg_.encoding == ENC_REAL && cfg_.objective != OBJ_NONE && !jit_;
+  // quantized tournament keys feed only the two-phase kernel (real_gen_tp),
+  // which small populations do not take: there they would cost a launch
+  return on_gpu() && cfg_.encoding == ENC_REAL && cfg_.objective != OBJ_NONE && !jit_ &&
+         cfg_.S >= real_tp_min_population();
 }
 
 void Island::prepare_generation() {
@@ -462,6 +476,18 @@ bool Island::run_batched(const std::vector<Island*>& isls, uint32_t n, hipStream
       return false;
     for (const Island* j : isls)
       if (j != i && j->rows_[0].ptr == i->rows_[0].ptr) return false;  // the same island twice
+  }
+  {  // binary_launch_batch's conditions from the configuration alone, before
+     // any launch (an island that cannot qualify pays no extra prepare pass)
+    const Config& c = i0->cfg_;
+    const bool obj_ok = c.objective == OBJ_ONEMAX || c.objective == OBJ_LEADING_ONES || c.objective == OBJ_TRAP;
+    const bool sel_ok = (c.selection == SEL_TOURNAMENT && c.tour_k == 2) || c.selection == SEL_RANDOM ||
+                        c.selection == SEL_RANK || c.selection == SEL_ROULETTE;
+    const bool o32 = (c.S + kRowPad) * (uint64_t)i0->row_words_ * 4u <= 0xFFFFFFFFull;
+    if (!obj_ok || !sel_ok || !o32 || i0->chunks_ > 64 || c.n_elite > 64 || force_generic_kernels()) return false;
+    for (const Island* i : isls)
+      if (!integer_objective(i->cfg_.objective, i->cfg_.L) || !i->keys_[0].ptr || i->cfg_.objective != c.objective)
+        return false;
   }
   TraceRange tr("pga.run_batched");
   std::vector<GenArgs> args(N);
@@ -771,10 +797,10 @@ void Island::set_jit_objective(std::shared_ptr<JitKernel> k) {
 }
 
 bool Island::fused_jit_generation(GenArgs& a) {
-  if (!on_gpu() || cfg_.encoding != ENC_BINARY || jit_fused_off_) return false;
+  if (!on_gpu() || (cfg_.encoding != ENC_BINARY && cfg_.encoding != ENC_REAL) || jit_fused_off_) return false;
   uint32_t gs = 0;
   bool full = false, dense = false;
-  if (!binary_tp_plan(a, gs, full, dense)) return false;
+  if (cfg_.encoding == ENC_REAL ? !real_tp_plan(a, gs) : !binary_tp_plan(a, gs, full, dense)) return false;
   // no compile / module load inside a graph capture: there only a variant
   // loaded by an earlier plain generation is used
   hipFunction_t f = jit_->gen_function(device_, gs, full, dense, cfg_.L, !capturing_);

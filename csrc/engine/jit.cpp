@@ -239,8 +239,10 @@ std::string jit_bitcode_dir() {
 }
 
 namespace {
-// the jitgen.hip symbol of binary_gen_tp<GS, kObjJit = 1001, FULL, DENSE>
-std::string gen_symbol(uint32_t gs, bool full, bool dense) {
+// the jitgen.hip symbol of binary_gen_tp<GS, kObjJit = 1001, FULL, DENSE>, or
+// jitgen_real.hip's real_gen_tp<GS, kObjJit, false>
+std::string gen_symbol(int encoding, uint32_t gs, bool full, bool dense) {
+  if (encoding == ENC_REAL) return "_ZN3pga6jitgen11real_gen_tpILi" + std::to_string(gs) + "ELi1001ELb0EEEvNS_7GenArgsEPy";
   return "_ZN3pga6jitgen13binary_gen_tpILi" + std::to_string(gs) + "ELi1001ELb" + (full ? "1" : "0") + "ELb" +
          (dense ? "1" : "0") + "EEEvNS_7GenArgsEPy";
 }
@@ -319,9 +321,12 @@ std::string read_text(const std::string& path) {
 // HIP / COMGR) hipRTC links with that older LLVM, which cannot read bitcode
 // from this build's compiler.
 std::string JitKernel::build_gen_object(uint32_t gs, bool full, bool dense, uint32_t L) {
-  if (encoding != ENC_BINARY) throw std::invalid_argument("fused generation kernels are BINARY only");
+  if (encoding != ENC_BINARY && encoding != ENC_REAL)
+    throw std::invalid_argument("fused generation kernels are BINARY and REAL only");
   if (gs == 0 || gs > 64 || (gs & (gs - 1)) != 0) throw std::invalid_argument("group size must be a power of two <= 64");
-  const std::string variant = std::to_string(gs) + "_" + (full ? "1" : "0") + "_" + (dense ? "1" : "0");
+  const bool real = encoding == ENC_REAL;
+  const std::string variant =
+      real ? "real_" + std::to_string(gs) : std::to_string(gs) + "_" + (full ? "1" : "0") + "_" + (dense ? "1" : "0");
   const std::string kbc = jit_bitcode_dir() + "/gen_" + variant + ".bc";
   const std::string kbc_text = read_text(kbc);
   if (kbc_text.empty())
@@ -332,10 +337,11 @@ std::string JitKernel::build_gen_object(uint32_t gs, bool full, bool dense, uint
   // the row arrives as a global pointer (global loads, not flat) and the
   // genome length as a constant, so fixed-trip loops over the row unroll with
   // every load in flight (the length is part of the cache key)
+  const std::string T = real ? "float" : "unsigned int";
   const std::string src = "#include <hip/hip_runtime.h>\n#line 1 \"user_objective\"\n" + user_source + "\n" +
-                          "extern \"C\" __device__ float pga_user_objective(__attribute__((address_space(1))) "
-                          "const unsigned int* w, unsigned int, const float* d) { return " + name +
-                          "((const unsigned int*)w, " + std::to_string(L) + "u, d); }\n";
+                          "extern \"C\" __device__ float " + (real ? "pga_user_objective_f32" : "pga_user_objective") +
+                          "(__attribute__((address_space(1))) const " + T + "* w, unsigned int, const float* d) { return " +
+                          name + "((const " + T + "*)w, " + std::to_string(L) + "u, d); }\n";
   // the user's compile options (-D, -I, ...) apply to the fused objective as
   // they do to the evaluation kernel, and are part of the cache key
   std::string uopts;
@@ -373,7 +379,7 @@ std::string JitKernel::build_gen_object(uint32_t gs, bool full, bool dense, uint
 }
 
 hipFunction_t JitKernel::gen_function(int device, uint32_t gs, bool full, bool dense, uint32_t L, bool build) {
-  if (encoding != ENC_BINARY || fused_failed_ || device < 0) return nullptr;
+  if ((encoding != ENC_BINARY && encoding != ENC_REAL) || fused_failed_ || device < 0) return nullptr;
   // (L, gs, full, dense) in disjoint fields: gs * 4 + 3 < 2^16
   const uint64_t key = ((uint64_t)L << 16) | (gs * 4u + (full ? 2u : 0u) + (dense ? 1u : 0u));
   for (const GenVariant& v : gen_)
@@ -390,7 +396,7 @@ hipFunction_t JitKernel::gen_function(int device, uint32_t gs, bool full, bool d
   PGA_HIP_CHECK(hipSetDevice(device));
   GenVariant v{device, key, nullptr, nullptr, 1, std::make_shared<std::vector<char>>(std::move(image))};
   hipError_t e = hipModuleLoadData(&v.mod, v.image->data());
-  if (e == hipSuccess) e = hipModuleGetFunction(&v.fn, v.mod, gen_symbol(gs, full, dense).c_str());
+  if (e == hipSuccess) e = hipModuleGetFunction(&v.fn, v.mod, gen_symbol(encoding, gs, full, dense).c_str());
   if (e != hipSuccess) {
     if (v.mod) (void)hipModuleUnload(v.mod);
     fused_failed_ = true;
@@ -418,6 +424,7 @@ uint32_t JitKernel::gen_launch(hipFunction_t f, const void* args, size_t args_by
   const TpGeom t = tp_geometry_occ(S, 1, occ, 64 / group_size(a.chunks));
   a.tp_unit = t.unit;
   const uint32_t grid = std::min(t.grid, max_grid);
+  a.tp_pool_units = a.tp_pool && grid == t.grid ? tp_pool_units(t, S) : 0u;
   // kernel arguments as one packed buffer: (GenArgs a, unsigned long long* parts)
   std::vector<char> buf(args_bytes + 16);
   std::memcpy(buf.data(), &a, args_bytes);

@@ -33,7 +33,6 @@ namespace {
 
 using namespace dev;
 
-constexpr int kObjJit = 1001;  // launcher-only objective id: the linked user objective (jitgen.hip)
 
 // per-lane objective accumulator over the chunks a lane owns
 template <int OBJ>
@@ -491,6 +490,17 @@ __device__ __forceinline__ void binary_gen_tp_body(GenArgs a, unsigned long long
   uint32_t bbegin, bend;
   tp_block_range(S, U, bbegin, bend);
   const uint32_t pcap = tp_par_cap(NW);
+  // the pair pool (tp.hpp): one round, tournament or random selection; the
+  // block's own units end at own_end, the last P units are the pair's
+  const uint32_t P = a.tp_pool_units;
+  bool pool_on = a.tp_pool != nullptr && P > 0u && bend - bbegin <= pcap && (tourn || a.selection == SEL_RANDOM);
+  if (pool_on && a.n_elite > 0) {  // elites stay in block 0's own units (their sources are in its LDS)
+    uint32_t b0b, b0e;
+    tp_share(S, U, 0, b0b, b0e);
+    pool_on = tp_pool_start(b0b, b0e, U, P) >= a.n_elite;
+  }
+  const uint32_t own_end = pool_on ? tp_pool_start(bbegin, bend, U, P) : bend;
+  const uint32_t pair = blockIdx.x & ~1u, npair = pair + 1u < gridDim.x ? 2u : 1u;
 
   // elite sources of children [0, n_elite) (n_elite <= kTpMaxElite), for the
   // block that holds any of them
@@ -519,7 +529,8 @@ __device__ __forceinline__ void binary_gen_tp_body(GenArgs a, unsigned long long
   unsigned long long clk_t = 0, clk_b = 0, n_bred = 0;
 #endif
   for (uint32_t rbeg = bbegin; rbeg < bend; rbeg += pcap) {  // block-uniform rounds
-    const uint32_t rend = rbeg + pcap < bend ? rbeg + pcap : bend;
+    const uint32_t rend0 = rbeg + pcap < bend ? rbeg + pcap : bend;
+    const uint32_t rend = rend0 < own_end ? rend0 : own_end;                // the round's own children
     const uint32_t nb = (rend - rbeg + U - 1) / U;                          // the round's units
     const uint32_t nseg = (rend - rbeg + kSegBatches * 64 - 1) / (kSegBatches * 64);  // its tournament segments
     __syncthreads();  // tables / elites / counter visible; the previous round's records and parents released
@@ -650,20 +661,40 @@ __device__ __forceinline__ void binary_gen_tp_body(GenArgs a, unsigned long long
 
     // RESOLVE: parents, crossover plan and flip positions of the round's unit
     // BI -> the records of ring slot SL (lanes past the unit: unused copies)
-#define PGA_TP_RESOLVE(BI, SL)                                                                                  \
+#define PGA_TP_RESOLVE(US, UE, SL)                                                                              \
   {                                                                                                             \
-    {  /* the unit's tournament segment is done (wave-uniform spin, rare) */                                    \
-      const uint32_t sg_ = (BI) * U / (kSegBatches * 64u);                                                      \
+    const uint32_t tc = (US) + lane;                                                                            \
+    const uint32_t cc = tc < (UE) ? tc : (UE) - 1;                                                              \
+    uint32_t pa, pb;                                                                                            \
+    if ((US) - rbeg < rend - rbeg) { /* an own unit: parents from the round's tournaments */                    \
+      /* its segment is done (wave-uniform spin, rare) */                                                       \
+      const uint32_t sg_ = ((US) - rbeg) / (kSegBatches * 64u);                                                 \
       while (__hip_atomic_load(&lds_ready[sg_], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == 0u)          \
         __builtin_amdgcn_s_sleep(1);                                                                            \
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");                                                    \
+      const uint2 pp = lds_par[cc - rbeg];                                                                      \
+      pa = pp.x;                                                                                                \
+      pb = pp.y;                                                                                                \
+    } else { /* a pool unit: its tournaments here, one lane per child (same words) */                           \
+      const u32x4 sb = draw<true>(a.key, ST_SEL, cc, 0);                                                        \
+      const uint32_t i0 = word_to_index(sb.x, S), i1 = word_to_index(sb.y, S);                                  \
+      const uint32_t i2 = word_to_index(sb.z, S), i3 = word_to_index(sb.w, S);                                  \
+      pa = i0;                                                                                                  \
+      pb = i1;                                                                                                  \
+      if (tourn) {                                                                                              \
+        if constexpr (KEY) {                                                                                    \
+          const uint32_t q0 = ELEM(const uint16_t, a.key_cur, i0), q1 = ELEM(const uint16_t, a.key_cur, i1);    \
+          const uint32_t q2 = ELEM(const uint16_t, a.key_cur, i2), q3 = ELEM(const uint16_t, a.key_cur, i3);    \
+          pa = q0 < q1 ? i1 : i0;                                                                               \
+          pb = q2 < q3 ? i3 : i2;                                                                               \
+        } else {                                                                                                \
+          const float f0 = ELEM(const float, a.score_cur, i0), f1 = ELEM(const float, a.score_cur, i1);         \
+          const float f2 = ELEM(const float, a.score_cur, i2), f3 = ELEM(const float, a.score_cur, i3);         \
+          pa = f0 < f1 ? i1 : i0;                                                                               \
+          pb = f2 < f3 ? i3 : i2;                                                                               \
+        }                                                                                                       \
+      }                                                                                                         \
     }                                                                                                           \
-    const uint32_t bs_ = rbeg + (BI) * U;                                                                       \
-    const uint32_t be_ = bs_ + U < rend ? bs_ + U : rend;                                                       \
-    const uint32_t tc = bs_ + lane;                                                                             \
-    const uint32_t cc = tc < be_ ? tc : be_ - 1;                                                                \
-    const uint2 pp = lds_par[cc - rbeg];                                                                        \
-    uint32_t pa = pp.x, pb = pp.y;                                                                              \
     const u32x4 misc = bin_misc<true>(a.key, cc);                                                               \
     const bool elite = tc < a.n_elite;                                                                          \
     const bool xo = !elite && xo_on && do_crossover(a, misc.x);                                                 \
@@ -719,19 +750,54 @@ __device__ __forceinline__ void binary_gen_tp_body(GenArgs a, unsigned long long
     // hipcc assumes the fewest outstanding loads over all paths, so a
     // conditionally issued load would make the next wait drain it): an
     // exhausted load cursor re-reads the breed cursor's rows.
-    uint32_t tk = 0;
-    if (lane == 0) tk = __hip_atomic_fetch_add(&lds_next, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    const uint32_t b0 = __builtin_amdgcn_readfirstlane(tk);  // the wave's first unit
-    if (b0 < nb) {
-      if (lane == 0) tk = __hip_atomic_fetch_add(&lds_next, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      uint32_t bn = __builtin_amdgcn_readfirstlane(tk);  // the next ticket (>= nb: none)
-      PGA_TP_RESOLVE(b0, 0u)
-      // breed cursor: ring slot, step, first child and steps of its unit
-      uint32_t slot = 0, i = 0, bs = rbeg + b0 * U;
-      uint32_t nst = ((bs + U < rend ? bs + U : rend) - bs + NG - 1) / NG;
-      // load cursor; lpend: at the end of its unit with ticket bn next;
+    // NEXT unit [US, UE) of this wave (US = kNoUnit: none): the block's own
+    // units from its LDS counter, then pool units from the pair's counter
+    constexpr uint32_t kNoUnit = 0xFFFFFFFFu;
+    bool steal = false;  // wave-uniform: own units exhausted, pulling pool units
+#define PGA_TP_NEXT(US, UE)                                                                                 \
+  {                                                                                                         \
+    US = kNoUnit;                                                                                           \
+    if (!steal) {                                                                                           \
+      uint32_t tk_ = 0;                                                                                     \
+      if (lane == 0) tk_ = __hip_atomic_fetch_add(&lds_next, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); \
+      tk_ = __builtin_amdgcn_readfirstlane(tk_);                                                            \
+      if (tk_ < nb) {                                                                                       \
+        US = rbeg + tk_ * U;                                                                                \
+        UE = US + U < rend ? US + U : rend;                                                                 \
+      } else {                                                                                              \
+        steal = pool_on;                                                                                    \
+      }                                                                                                     \
+    }                                                                                                       \
+    while (steal && US == kNoUnit) { /* ticket t: block pair + t % npair, its pool unit t / npair */       \
+      const uint32_t t_ = tp_pool_grab(a.tp_pool + (pair >> 1) * kTpPoolStride, a.tp_seq, lane);            \
+      if (t_ / npair >= P) {                                                                                \
+        steal = false;                                                                                      \
+      } else {                                                                                              \
+        uint32_t pb_, pe_;                                                                                  \
+        tp_share(S, U, pair + t_ % npair, pb_, pe_);                                                        \
+        const uint32_t ps_ = tp_pool_start(pb_, pe_, U, P) + (t_ / npair) * U;                             \
+        if (ps_ < pe_) {                                                                                    \
+          US = ps_;                                                                                         \
+          UE = ps_ + U < pe_ ? ps_ + U : pe_;                                                               \
+        }                                                                                                   \
+      }                                                                                                     \
+    }                                                                                                       \
+  }
+
+    uint32_t ns, ne = 0;  // the wave's next unit (prefetched ticket)
+    PGA_TP_NEXT(ns, ne)
+    if (ns != kNoUnit) {
+      // breed cursor: ring slot, step, its unit [bs, be) and steps.  Every
+      // unit takes U / NG steps, a partial one (only ever at S) too: its
+      // children past S write the padding rows, and a unit never holds fewer
+      // steps than the PD the load cursor runs ahead
+      const uint32_t nst = U / NG;
+      uint32_t slot = 0, i = 0, bs = ns, be = ne;
+      PGA_TP_NEXT(ns, ne)
+      PGA_TP_RESOLVE(bs, be, 0u)
+      // load cursor; lpend: at the end of its unit with unit ns next;
       // lmore = false: past the wave's last step
-      uint32_t lslot = 0, li = 0, lbs = bs, lnst = nst;
+      uint32_t lslot = 0, li = 0, lbs = bs, lbe = be;
       bool lpend = false, lmore = true, done = false;
 
       // LOAD the parent rows of the load cursor's step into (YA, YB) and
@@ -739,21 +805,19 @@ __device__ __forceinline__ void binary_gen_tp_body(GenArgs a, unsigned long long
 #define PGA_TP_LOAD(YA, YB)                                                                                 \
   {                                                                                                         \
     if (lpend) { /* entering the next unit */                                                               \
-      PGA_TP_RESOLVE(bn, lslot ^ 1u)                                                                        \
+      PGA_TP_RESOLVE(ns, ne, lslot ^ 1u)                                                                    \
       lslot ^= 1u;                                                                                          \
       li = 0;                                                                                               \
-      lbs = rbeg + bn * U;                                                                                  \
-      lnst = ((lbs + U < rend ? lbs + U : rend) - lbs + NG - 1) / NG;                                       \
+      lbs = ns;                                                                                             \
+      lbe = ne;                                                                                             \
       lpend = false;                                                                                        \
-      if (lane == 0)                                                                                        \
-        tk = __hip_atomic_fetch_add(&lds_next, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);         \
-      bn = __builtin_amdgcn_readfirstlane(tk);                                                              \
+      PGA_TP_NEXT(ns, ne)                                                                                   \
     }                                                                                                       \
     const uint4 r = rec[lmore ? lslot : slot][(lmore ? li : i) * NG + g][0];                                \
     YA = ROW(cur, r.x, qq);                                                                                 \
     YB = ROW(cur, r.y, qq);                                                                                 \
-    if (lmore && ++li == lnst) {                                                                            \
-      lpend = bn < nb;                                                                                      \
+    if (lmore && ++li == nst) {                                                                             \
+      lpend = ns != kNoUnit;                                                                                \
       lmore = lpend;                                                                                        \
     }                                                                                                       \
   }
@@ -820,7 +884,7 @@ __device__ __forceinline__ void binary_gen_tp_body(GenArgs a, unsigned long long
         slot ^= 1u;                                                                                         \
         i = 0;                                                                                              \
         bs = lbs;                                                                                           \
-        nst = lnst;                                                                                         \
+        be = lbe;                                                                                           \
       }                                                                                                     \
     }                                                                                                       \
   }
@@ -832,7 +896,7 @@ __device__ __forceinline__ void binary_gen_tp_body(GenArgs a, unsigned long long
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");                                                  \
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");                                                  \
     const uint32_t cj = bs + lane;                                                                          \
-    if (lane < U && cj < rend) {                                                                            \
+    if (cj < be) {                                                                                          \
       const float sj = pga_user_objective((pga_global_words)((const char*)nxt + cj * rb), L, a.obj_data);   \
       ELEM(float, a.score_next, cj) = sj;                                                                   \
       my_best = pack_best(sj, cj) > my_best ? pack_best(sj, cj) : my_best;                                  \
@@ -840,7 +904,7 @@ __device__ __forceinline__ void binary_gen_tp_body(GenArgs a, unsigned long long
     }                                                                                                       \
   }
 #ifdef PGA_TP_TIMING
-#define PGA_TP_COUNT n_bred += (bs + U < rend ? bs + U : rend) - bs;
+#define PGA_TP_COUNT n_bred += be - bs;
 #else
 #define PGA_TP_COUNT
 #endif
@@ -883,6 +947,7 @@ __device__ __forceinline__ void binary_gen_tp_body(GenArgs a, unsigned long long
       }
 #undef PGA_TP_STEP
 #undef PGA_TP_LOAD
+#undef PGA_TP_NEXT
 #undef PGA_TP_JIT_EVAL
 #undef PGA_TP_COUNT
     }

@@ -354,6 +354,11 @@ struct GenArgs {
   // two-phase kernels (tp.hpp): children per dynamically assigned breed unit,
   // a power of two in [64 / GS, 64] set by the launcher (0 = 64)
   uint32_t tp_unit;
+  // pair pool of binary_gen_tp (tp.hpp): per block pair one 64-bit counter
+  // (kTpPoolStride apart), this launch's stamp, the units per block in the
+  // pool (0 / nullptr: no pool)
+  unsigned long long* tp_pool;
+  uint32_t tp_seq, tp_pool_units;
 };
 
 PGA_HD uint32_t sel_words(const GenArgs& a) {

@@ -259,6 +259,8 @@ class Island {
   bool graph_broken_ = false, capturing_ = false;
   uint32_t capture_base_ = 0;
   Buffer gen_dev_;
+  Buffer tp_pool_;        // binary_gen_tp pair-pool counters (tp.hpp), GPU BINARY only
+  uint32_t tp_seq_ = 0;   // their per-launch stamp
   hipStream_t cap_stream_ = nullptr;
   hipGraphExec_t gexec_ = nullptr;
   int g_cur_ = -1;

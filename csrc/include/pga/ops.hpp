@@ -53,6 +53,11 @@ TpGeom tp_geometry(uint64_t S, uint32_t islands, const void* kernel, uint32_t ng
 // the same from the resident 4-wave blocks per CU (occ4; module kernels)
 TpGeom tp_geometry_occ(uint64_t S, uint32_t islands, uint32_t occ4, uint32_t ng, uint32_t pseg = 7);
 uint32_t tp_dyn_lds_bytes(uint32_t nw, uint32_t pseg = 7);
+// units per block in binary_gen_tp's pair pool for this geometry (tp.hpp;
+// PGA_TP_POOL=d: 1/d of a 16-wave block's units; default 0: off)
+uint32_t tp_pool_units(const TpGeom& t, uint64_t S);
+// bytes of pair-pool counters a launch of up to `grid` blocks needs
+inline size_t tp_pool_bytes(uint32_t grid) { return (size_t)(grid + 1) / 2 * 128; }
 int device_cu_count();
 // raise a kernel's dynamic-LDS limit to what its static LDS leaves of the
 // CU's 160 KiB; returns that many bytes
@@ -64,10 +69,17 @@ bool force_generic_kernels();
 // ---- encodings: one launch per call, returns the grid used (= number of
 // valid entries written to best_parts, when the mode evaluates) ----
 uint32_t binary_launch(int mode, const GenArgs& a, unsigned long long* best_parts, hipStream_t s);
+// binary_launch for one group size GS (binary_gs.hip, one translation unit per GS)
+template <int GS>
+uint32_t binary_launch_group(int mode, const GenArgs& a, unsigned long long* best_parts, hipStream_t s);
 // whether a MODE_GEN launch of these arguments takes the hot two-phase kernel
 // (binary_gen_tp) and which variant: group size, full groups, dense mutation.
 // For f32-score objectives (the fused JIT generation kernel, jit.hpp).
 bool binary_tp_plan(const GenArgs& a, uint32_t& gs, bool& full, bool& dense);
+// the same for REAL (real_gen_tp, no rotation): its group size
+bool real_tp_plan(const GenArgs& a, uint32_t& gs);
+// smallest REAL population that takes real_gen_tp (PGA_TP_MIN_S overrides)
+uint64_t real_tp_min_population();
 // batched islands (binary_batch.hip): one MODE_GEN launch of up to
 // binary_max_batch() same-shape islands (args[i], best partials parts[i]);
 // returns each island's grid (its best-partials count), 0 when the islands do

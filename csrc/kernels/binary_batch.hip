@@ -23,7 +23,10 @@ uint32_t batch_go(GenBatch& b, uint32_t n, uint64_t S, bool full, bool dense, hi
                                 : (const void*)binary_gen_tp_batch<GS, OBJ, false, false>);
   // the device split between the islands (tp_geometry)
   const TpGeom t = tp_geometry(S, n, k, 64 / GS);
-  for (uint32_t i = 0; i < n; ++i) b.a[i].tp_unit = t.unit;
+  for (uint32_t i = 0; i < n; ++i) {
+    b.a[i].tp_unit = t.unit;
+    b.a[i].tp_pool_units = b.a[i].tp_pool ? tp_pool_units(t, S) : 0u;
+  }
   const dim3 grid(t.grid, n);
   if (full) {
     if (dense) hipLaunchKernelGGL((binary_gen_tp_batch<GS, OBJ, true, true>), grid, t.block, t.lds, s, b);

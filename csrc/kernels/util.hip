@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cmath>
+#include <cstdlib>
 #include <map>
 #include <mutex>
 #include <set>
@@ -84,6 +85,17 @@ TpGeom tp_geometry(uint64_t S, uint32_t islands, const void* kernel, uint32_t ng
 }
 
 uint32_t tp_dyn_lds_bytes(uint32_t nw, uint32_t pseg) { return dev::tp_dyn_lds(nw, pseg); }
+
+uint32_t tp_pool_units(const TpGeom& t, uint64_t S) {
+  // PGA_TP_POOL = d: 1/d of each block's units in the pair pool (default 0: none)
+  static const uint32_t d = [] {
+    const char* e = std::getenv("PGA_TP_POOL");
+    return e ? (uint32_t)std::strtoul(e, nullptr, 10) : 0u;  // off by default (tp.hpp)
+  }();
+  if (d == 0 || t.block != dev::kTpMaxWaves * 64 || t.grid < 2) return 0;
+  const uint64_t per = (S + t.grid - 1) / t.grid, units = (per + t.unit - 1) / t.unit;
+  return (uint32_t)(units / d);
+}
 
 TpGeom tp_geometry_occ(uint64_t S, uint32_t islands, uint32_t occ4, uint32_t ng, uint32_t pseg) {
   if (islands == 0) islands = 1;

@@ -145,3 +145,96 @@ def test_jit_fusion_unavailable_falls_back(monkeypatch):
     assert b.island.jit_fused_generations == 0
     assert "no generation-kernel bitcode" in b.island.jit_fused_error
     assert torch.equal(a.rows, b.rows) and torch.equal(a.scores, b.scores)
+
+
+QUAD_SRC = """
+__device__ float quad(const float* x, unsigned int n, const float* d) {
+  float s = 0.f;
+  for (unsigned int i = 0; i < n; ++i) { const float t = x[i] - d[i]; s += t * t; }
+  return -s;
+}
+"""
+
+
+def test_jit_real_fused_generation_object_builds_without_gpu(tmp_path, monkeypatch):
+    # REAL (the reference's float genes): jitgen_real.hip bitcode + the user's
+    monkeypatch.setenv("PGA_JIT_CACHE", str(tmp_path))
+    k = M.JitObjective("real", 30, RASTRIGIN_SRC, name="rastrigin", bounds=(-5.12, 5.12)).kernel()
+    path = k.build_generation_object(8, False, False, 30)
+    data = open(path, "rb").read()
+    assert data[:4] == b"\x7fELF"
+    assert b"_ZN3pga6jitgen11real_gen_tpILi8ELi1001ELb0EEEvNS_7GenArgsEPy" in data
+    assert b"pga_user_objective_f32" not in data  # inlined, no call left
+
+
+def test_jit_cache_must_be_private(tmp_path, monkeypatch):
+    import os
+    d = tmp_path / "shared"
+    d.mkdir()
+    os.chmod(d, 0o777)
+    monkeypatch.setenv("PGA_JIT_CACHE", str(d))
+    k = onemax_jit(256).kernel()
+    with pytest.raises(RuntimeError, match="not private"):
+        k.build_generation_object(2, True, False, 256)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("S", [1 << 18, 20000])
+def test_jit_real_fused_equals_separate_pass(S, monkeypatch):
+    """A float-gene source objective fused into real_gen_tp (one launch per
+    generation) reproduces the separate evaluation pass bit for bit: rows,
+    scores, best; both equal the fp32 torch oracle."""
+    L = 30
+    tgt = torch.linspace(-1, 1, L)
+    # the unfused twin gets its own kernel (a different source text, same
+    # function) so that no fused variant is cached for it
+    mk = lambda tag: M.JitObjective("real", L, QUAD_SRC + tag, name="quad", data=tgt, bounds=(-2.0, 2.0))
+    a = pga.GeneticAlgorithm(mk(""), S, seed=6, device="cuda:0", elitism=1)
+    a.run(8)
+    torch.cuda.synchronize()
+    assert a.island.jit_fused_generations >= 8, a.island.jit_fused_error
+    monkeypatch.setenv("PGA_JIT_DIR", "/nonexistent/pga_jit")
+    b = pga.GeneticAlgorithm(mk(f"// unfused {S}\n"), S, seed=6, device="cuda:0", elitism=1)
+    b.run(8)
+    torch.cuda.synchronize()
+    assert b.island.jit_fused_generations == 0
+    assert torch.equal(a.rows, b.rows) and torch.equal(a.scores, b.scores)
+    ref = -((a.genomes().float().cpu() - tgt) ** 2).sum(-1)
+    assert torch.allclose(ref, a.scores.cpu(), rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.gpu
+def test_jit_variant_key_distinguishes_lengths():
+    # 5000 and 5001 bits share a group size of 64 lanes: one JitKernel (same
+    # source) used at both lengths must compile two variants
+    for L in (5000, 5001):
+        a = pga.GeneticAlgorithm(M.OneMax(L), 4096, seed=3, device="cuda:0", elitism=1)
+        b = pga.GeneticAlgorithm(onemax_jit(L), 4096, seed=3, device="cuda:0", elitism=1)
+        a.run(3)
+        b.run(3)
+        torch.cuda.synchronize()
+        assert b.island.jit_fused_generations >= 3, b.island.jit_fused_error
+        assert torch.equal(a.rows, b.rows) and torch.equal(a.scores, b.scores)
+
+
+SCALED_SRC = """
+#ifndef SCALE
+#define SCALE 1.0f
+#endif
+__device__ float scaled(const unsigned int* w, unsigned int nbits, const float* data) {
+  float s = 0.f;
+  for (unsigned int i = 0; i < (nbits + 31) / 32; ++i) s += (float)__popc(w[i]);
+  return SCALE * s;
+}
+"""
+
+
+@pytest.mark.gpu
+def test_jit_options_reach_fused_kernel():
+    # -DSCALE=3.0f applies to the fused generation kernel as to the init pass
+    p = M.JitObjective("binary", 256, SCALED_SRC, name="scaled", options=["-DSCALE=3.0f"])
+    ga = pga.GeneticAlgorithm(p, 1 << 14, seed=2, device="cuda:0", elitism=1)
+    ga.run(5)
+    torch.cuda.synchronize()
+    assert ga.island.jit_fused_generations >= 5, ga.island.jit_fused_error
+    assert torch.equal(ga.scores, 3.0 * ga.genomes().float().sum(-1))

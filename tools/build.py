@@ -27,6 +27,9 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 BUILD = os.path.join(ROOT, "build")
 ARCH = os.environ.get("PGA_ARCH", "gfx950")
 
+# kernel sources built once per -D variant (tag, flags): the BINARY launchers
+# per group size, so the heaviest instantiation sets compile in parallel
+SPLIT = {"csrc/kernels/binary_gs.hip": [(f"gs{g}", f"-DPGA_BIN_GS={g}") for g in (1, 2, 4, 8, 16, 32, 64)]}
 KERNELS = ["csrc/kernels/binary.hip", "csrc/kernels/real.hip", "csrc/kernels/perm.hip",
            "csrc/kernels/util.hip", "csrc/kernels/compat.hip", "csrc/kernels/qubo.hip",
            "csrc/kernels/sort.hip", "csrc/kernels/binary_batch.hip"]
@@ -108,6 +111,17 @@ def write_ninja(opt: str, with_torch: bool) -> str:
         o = obj_path(s, "k")
         lines.append(f"build {o}: hip {s}")
         core_objs.append(o)
+    split_rdc = []
+    for s, variants in SPLIT.items():
+        for tag, flags in variants:
+            o = obj_path(s, f"{tag}.k")
+            lines.append(f"build {o}: hip {s}")
+            lines.append(f"  extra = {flags}")
+            core_objs.append(o)
+            o = obj_path(s, f"{tag}.rdc")
+            lines.append(f"build {o}: rdc {s}")
+            lines.append(f"  extra = {flags}")
+            split_rdc.append(o)
     for s in HOST:
         o = obj_path(s, "h")
         lines.append(f"build {o}: host {s}")
@@ -128,7 +142,7 @@ def write_ninja(opt: str, with_torch: bool) -> str:
     lines.append("  ldflags = -Wl,-soname,libpga.so -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib")
 
     # static rdc library for user device function pointers
-    rdc_objs = []
+    rdc_objs = list(split_rdc)
     for s in KERNELS + COMPAT:
         o = obj_path(s, "rdc")
         lines.append(f"build {o}: rdc {s}")
@@ -179,6 +193,11 @@ def write_ninja(opt: str, with_torch: bool) -> str:
                 lines.append(f"build {out}: jitbc csrc/kernels/jitgen.hip | {hdrs}")
                 lines.append(f"  extra = -DPGA_JIT_GS={gs} -DPGA_JIT_FULL={full} -DPGA_JIT_DENSE={dense}")
                 jit_bc.append(out)
+        out = f"build/jit/gen_real_{gs}.bc"
+        hdrs = " ".join(f"csrc/include/pga/{h}.hpp" for h in ("real_dev", "real_ops", "tp", "core", "device", "ops"))
+        lines.append(f"build {out}: jitbc csrc/kernels/jitgen_real.hip | {hdrs}")
+        lines.append(f"  extra = -DPGA_JIT_GS={gs}")
+        jit_bc.append(out)
 
     defaults = ["build/libpga.so", "build/libpga.a"] + ex + jit_bc
     if with_torch:

@@ -7,7 +7,10 @@ set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd "$R"; export TMPDIR=/tmp
 O=gpurun_out/${TAG:-r4}; mkdir -p $O
-timeout -k 10 300 python __graft_entry__.py smoke > $O/smoke.log 2>&1 || { cat $O/smoke.log; exit 1; }
+if [ -x build/variants/gen_base ]; then  # the headline kernel alone first (no torch import): a hang shows in 60 s
+  timeout -k 10 60 build/variants/gen_base --gens 20 --warmup 2 || exit 1
+fi
+timeout -k 10 300 python -u __graft_entry__.py smoke > $O/smoke.log 2>&1 || { cat $O/smoke.log; exit 1; }
 cat $O/smoke.log
 timeout -k 10 300 python bench.py --gpus 1 --steps 20 --warmup 5 > $O/bench20.log 2>&1 || { cat $O/bench20.log; exit 1; }
 tail -1 $O/bench20.log
