@@ -10,6 +10,7 @@ Configs (BASELINE.md "Targets" table):
   rastrigin30_rot   Rastrigin-30D rotated, pop=1M (fitness through MFMA tiles)
   tsp256_ox / _pmx  TSP-256 permutation, pop=256K, OX / PMX crossover (distance matrix)
   tsp256_euc_*      the same instance as city coordinates (TSPEuclidean)
+  tsp256_int_*      an integer EUC_2D matrix (u16 copy in LDS)
   e1_sum100_refops  reference example E1 (S=40000, L=100) with the reference's
                     operators — the head-to-head against build/bench/refsem
   e2_knap_refops    reference example E2 (S=100, L=6), launch-bound (hipGraph)
@@ -66,6 +67,11 @@ def make(name: str):
         xy = torch.rand(256, 2, generator=g)
         xo = "ox" if name.endswith("ox") else "pmx"
         return M.TSPEuclidean(xy), 1 << 18, None, dict(elitism=1, crossover=xo), 50
+    if name in ("tsp256_int_ox", "tsp256_int_pmx"):
+        # the same geometry as an integer matrix (TSPLIB EUC_2D rounding): the
+        # fused kernel evaluates tours from a u16 copy of the matrix in LDS
+        xo = "ox" if name.endswith("ox") else "pmx"
+        return M.TSP.random_integer_euclidean(256, seed=7), 1 << 18, None, dict(elitism=1, crossover=xo), 50
     if name in ("tsp256_ox", "tsp256_pmx"):
         g = torch.Generator().manual_seed(7)
         xy = torch.rand(256, 2, generator=g)
@@ -90,7 +96,8 @@ def make(name: str):
     raise KeyError(name)
 
 
-NAMES = ["onemax64_cpu", "onemax1024", "rastrigin30", "rastrigin30_rot", "tsp256_ox", "tsp256_pmx", "e1_sum100_refops",
+NAMES = ["onemax64_cpu", "onemax1024", "rastrigin30", "rastrigin30_rot", "tsp256_ox", "tsp256_pmx", "tsp256_int_ox",
+         "tsp256_int_pmx", "e1_sum100_refops",
          "tsp256_euc_ox", "tsp256_euc_pmx", "e2_knap_refops", "onemax64_gpu", "onemax1024_jit", "maxcut512_qubo",
          "qubo1024", "onemax1024_rank", "knapsack1024", "onemax1024_roulette_2pt"]
 

@@ -53,6 +53,7 @@ Island::Island(const Config& cfg, int device) : cfg_(cfg), device_(device) {
   }
   out_best_ = alloc(64);
   stats_ = alloc(4ull * (4 + 3 * 1024));
+  aux_on_ = std::getenv("PGA_TSP_NO_LDS") == nullptr;  // verification: the f32 L2 matrix path
   if (on_gpu() && cfg_.encoding == ENC_BINARY) {  // binary_gen_tp's pair-pool counters (stamp 0 = stale)
     tp_pool_ = alloc(tp_pool_bytes(kMaxGrid));
     PGA_HIP_CHECK(hipMemset(tp_pool_.ptr, 0, tp_pool_.bytes));
@@ -73,7 +74,7 @@ Island::~Island() {
   Buffer* all[] = {&rows_[0],   &rows_[1],     &scores_[0],   &scores_[1],  &best_[0],  &best_[1],   &mut_thr_,
                    &obj_data_[0], &obj_data_[1], &keys_[0], &keys_[1], &elite_idx_, &cumfit_, &cum_ws_, &roul_guide_, &topk_ws_, &stats_,
                    &out_best_,  &scratch_, &compat_rand_, &ev_parts_, &gen_dev_, &rank_order_, &rank_ws_, &qubo_qt_,
-                   &knap_tab_, &stats_parts_[0], &stats_parts_[1], &hist_, &qk_ws_, &tp_pool_};
+                   &knap_tab_, &stats_parts_[0], &stats_parts_[1], &hist_, &qk_ws_, &tp_pool_, &obj_aux_};
   drop_graph();
   if (cap_stream_) (void)hipStreamDestroy(cap_stream_);
   for (Buffer* b : all) {
@@ -221,6 +222,39 @@ void Island::prepare_objective() {
       copy_to_device(knap_tab_.ptr, tab.data(), tab.size());
     }
   }
+  if ((cfg_.objective == OBJ_TSP || cfg_.objective == OBJ_TSP_OPEN) && cfg_.encoding == ENC_PERMUTATION && on_gpu() &&
+      aux_version_ != obj_version_) {
+    // an integer matrix (entries in [0, 65535]) as u16 for the LDS-resident
+    // tour evaluation (perm.hip perm_gen_fast TBL): the strict lower triangle
+    // plus the diagonal when symmetric, else the full matrix
+    aux_version_ = obj_version_;
+    aux_kind_ = aux_bytes_ = 0;
+    const uint32_t L = cfg_.L;
+    const float* d = obj_host0_.data();
+    bool ok = obj_host0_.size() >= (size_t)L * L && L >= 2, sym = ok;
+    for (size_t i = 0; ok && i < (size_t)L * L; ++i) ok = d[i] >= 0.f && d[i] <= 65535.f && d[i] == std::floor(d[i]);
+    for (uint32_t i = 0; ok && sym && i < L; ++i)
+      for (uint32_t j = 0; sym && j < i; ++j) sym = d[(size_t)i * L + j] == d[(size_t)j * L + i];
+    if (ok) {
+      std::vector<uint16_t> t;
+      if (sym) {
+        t.reserve((size_t)L * (L + 1) / 2 + 8);
+        for (uint32_t i = 1; i < L; ++i)
+          for (uint32_t j = 0; j < i; ++j) t.push_back((uint16_t)d[(size_t)i * L + j]);
+        for (uint32_t i = 0; i < L; ++i) t.push_back((uint16_t)d[(size_t)i * L + i]);
+      } else {
+        for (size_t i = 0; i < (size_t)L * L; ++i) t.push_back((uint16_t)d[i]);
+      }
+      t.resize((t.size() + 7) / 8 * 8, 0);  // whole 16-byte stores
+      if (obj_aux_.bytes < 2 * t.size()) {
+        release(obj_aux_);
+        obj_aux_ = alloc(2 * t.size());
+      }
+      copy_to_device(obj_aux_.ptr, t.data(), 2 * t.size());
+      aux_kind_ = sym ? 1u : 2u;
+      aux_bytes_ = (uint32_t)(2 * t.size());
+    }
+  }
   if (cfg_.objective != OBJ_QUBO) return;
   if (cfg_.encoding != ENC_BINARY) throw std::invalid_argument("the QUBO objective needs the BINARY encoding");
   if (obj_len_[0] < (size_t)cfg_.L * cfg_.L) throw std::invalid_argument("QUBO: objective data must hold the L x L matrix Q");
@@ -240,6 +274,11 @@ GenArgs Island::make_args(int mode) {
   GenArgs a;
   std::memset(&a, 0, sizeof(a));
   a.qubo_qt = (const int8_t*)qubo_qt_.ptr;
+  if (aux_kind_ && aux_on_ && (cfg_.objective == OBJ_TSP || cfg_.objective == OBJ_TSP_OPEN)) {
+    a.obj_aux = obj_aux_.ptr;
+    a.obj_aux_kind = aux_kind_;
+    a.obj_aux_bytes = aux_bytes_;
+  }
   if (cfg_.objective == OBJ_KNAPSACK && knap_cols_ > 0) {
     a.knap_tab = knap_tab_.ptr;
     a.knap_dig = knap_dig_;

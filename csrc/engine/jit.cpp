@@ -154,7 +154,9 @@ std::shared_ptr<JitKernel> jit_compile(int encoding, const std::string& source, 
   rtc_program prog = nullptr;
   if (r.create(&prog, k->source.c_str(), "pga_jit_objective.hip", 0, nullptr, nullptr) != 0)
     throw std::runtime_error("hiprtcCreateProgram failed");
-  std::vector<std::string> opts = {"--offload-arch=gfx950", "-O3", "-std=c++17"};
+  // -ffp-contract=fast as in the fused build (build_gen_object): both
+  // compilations of an objective then form the same fused multiply-adds
+  std::vector<std::string> opts = {"--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=fast"};
   for (const auto& o : extra_options) opts.push_back(o);
   std::vector<const char*> copts;
   for (const auto& o : opts) copts.push_back(o.c_str());
@@ -425,6 +427,7 @@ uint32_t JitKernel::gen_launch(hipFunction_t f, const void* args, size_t args_by
   a.tp_unit = t.unit;
   const uint32_t grid = std::min(t.grid, max_grid);
   a.tp_pool_units = a.tp_pool && grid == t.grid ? tp_pool_units(t, S) : 0u;
+  a.tp_skew = grid == t.grid && a.encoding == ENC_BINARY ? tp_skew_units(t, S) : 0u;
   // kernel arguments as one packed buffer: (GenArgs a, unsigned long long* parts)
   std::vector<char> buf(args_bytes + 16);
   std::memcpy(buf.data(), &a, args_bytes);

@@ -488,7 +488,7 @@ __device__ __forceinline__ void binary_gen_tp_body(GenArgs a, unsigned long long
   // this block's children [bbegin, bend) (tp.hpp)
   const uint32_t U = tp_unit(a, NG);  // children per breed unit (tp.hpp)
   uint32_t bbegin, bend;
-  tp_block_range(S, U, bbegin, bend);
+  tp_block_range(S, U, bbegin, bend, a.tp_skew);
   const uint32_t pcap = tp_par_cap(NW);
   // the pair pool (tp.hpp): one round, tournament or random selection; the
   // block's own units end at own_end, the last P units are the pair's
@@ -496,7 +496,7 @@ __device__ __forceinline__ void binary_gen_tp_body(GenArgs a, unsigned long long
   bool pool_on = a.tp_pool != nullptr && P > 0u && bend - bbegin <= pcap && (tourn || a.selection == SEL_RANDOM);
   if (pool_on && a.n_elite > 0) {  // elites stay in block 0's own units (their sources are in its LDS)
     uint32_t b0b, b0e;
-    tp_share(S, U, 0, b0b, b0e);
+    tp_share(S, U, 0, b0b, b0e, a.tp_skew);
     pool_on = tp_pool_start(b0b, b0e, U, P) >= a.n_elite;
   }
   const uint32_t own_end = pool_on ? tp_pool_start(bbegin, bend, U, P) : bend;
@@ -774,7 +774,7 @@ __device__ __forceinline__ void binary_gen_tp_body(GenArgs a, unsigned long long
         steal = false;                                                                                      \
       } else {                                                                                              \
         uint32_t pb_, pe_;                                                                                  \
-        tp_share(S, U, pair + t_ % npair, pb_, pe_);                                                        \
+        tp_share(S, U, pair + t_ % npair, pb_, pe_, a.tp_skew);                                             \
         const uint32_t ps_ = tp_pool_start(pb_, pe_, U, P) + (t_ / npair) * U;                             \
         if (ps_ < pe_) {                                                                                    \
           US = ps_;                                                                                         \

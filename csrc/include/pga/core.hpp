@@ -359,6 +359,15 @@ struct GenArgs {
   // pool (0 / nullptr: no pool)
   unsigned long long* tp_pool;
   uint32_t tp_seq, tp_pool_units;
+  // share skew of binary_gen_tp (tp.hpp tp_share): units each odd block of a
+  // pair hands to its even neighbour (0: equal shares)
+  uint32_t tp_skew;
+  // encoding-specific derived objective table, nullptr when unused
+  // (PERMUTATION, perm.hip: the integer distance matrix as u16, kind 1 = a
+  // symmetric matrix's strict lower triangle then its diagonal, 2 = the
+  // full matrix)
+  const void* obj_aux;
+  uint32_t obj_aux_kind, obj_aux_bytes;
 };
 
 PGA_HD uint32_t sel_words(const GenArgs& a) {

@@ -260,6 +260,9 @@ class Island {
   uint32_t capture_base_ = 0;
   Buffer gen_dev_;
   Buffer tp_pool_;        // binary_gen_tp pair-pool counters (tp.hpp), GPU BINARY only
+  Buffer obj_aux_;        // derived objective table (TSP: the integer matrix as u16, GenArgs::obj_aux)
+  uint32_t aux_kind_ = 0, aux_bytes_ = 0, aux_version_ = ~0u;
+  bool aux_on_ = true;    // PGA_TSP_NO_LDS unset at construction
   uint32_t tp_seq_ = 0;   // their per-launch stamp
   hipStream_t cap_stream_ = nullptr;
   hipGraphExec_t gexec_ = nullptr;

@@ -56,6 +56,8 @@ uint32_t tp_dyn_lds_bytes(uint32_t nw, uint32_t pseg = 7);
 // units per block in binary_gen_tp's pair pool for this geometry (tp.hpp;
 // PGA_TP_POOL=d: 1/d of a 16-wave block's units; default 0: off)
 uint32_t tp_pool_units(const TpGeom& t, uint64_t S);
+// share skew for this geometry (tp.hpp tp_share; PGA_TP_SKEW units, default 2)
+uint32_t tp_skew_units(const TpGeom& t, uint64_t S);
 // bytes of pair-pool counters a launch of up to `grid` blocks needs
 inline size_t tp_pool_bytes(uint32_t grid) { return (size_t)(grid + 1) / 2 * 128; }
 int device_cu_count();

@@ -195,19 +195,26 @@ __device__ __forceinline__ uint32_t tp_unit(const GenArgs& a, uint32_t NG) {
   return u >= lo && u <= 64u && (u & (u - 1u)) == 0u ? u : 64u;
 }
 
-// the share [bb, be) of block blk
-__device__ __forceinline__ void tp_share(uint32_t S, uint32_t U, uint32_t blk, uint32_t& bb, uint32_t& be) {
+// the share [bb, be) of block blk.  skew (units, < per / U): in each block
+// pair (2p, 2p + 1) the odd block hands `skew` units to the even one.  The
+// dispatcher deals a launch's blocks to the XCDs round robin (block b ->
+// XCD b % 8), and on every box measured the odd XCDs' blocks finished ~6 us
+// behind the even ones' (phase clocks, round 4), so the launcher can skew.
+__device__ __forceinline__ void tp_share(uint32_t S, uint32_t U, uint32_t blk, uint32_t& bb, uint32_t& be,
+                                         uint32_t skew = 0) {
   uint64_t per = (S + (uint64_t)gridDim.x - 1) / gridDim.x;
   per = (per + U - 1) / U * U;
 #ifdef PGA_TP_SWAPSHARE  // experiment builds: neighbouring blocks (XCDs) trade shares
   blk = (blk ^ 1u) < gridDim.x ? (blk ^ 1u) : blk;
 #endif
-  const uint64_t b = (uint64_t)blk * per;
+  const uint64_t d = (uint64_t)skew * U < per && (blk | 1u) < gridDim.x ? (uint64_t)skew * U : 0;
+  const uint64_t b = (uint64_t)blk * per + ((blk & 1u) ? d : 0), n = (blk & 1u) ? per - d : per + d;
   bb = (uint32_t)(b < S ? b : S);
-  be = (uint32_t)(bb + per < S ? bb + per : S);
+  be = (uint32_t)(bb + n < S ? bb + n : S);
 }
-__device__ __forceinline__ void tp_block_range(uint32_t S, uint32_t U, uint32_t& bbegin, uint32_t& bend) {
-  tp_share(S, U, blockIdx.x, bbegin, bend);
+__device__ __forceinline__ void tp_block_range(uint32_t S, uint32_t U, uint32_t& bbegin, uint32_t& bend,
+                                               uint32_t skew = 0) {
+  tp_share(S, U, blockIdx.x, bbegin, bend, skew);
 }
 
 // Pair pool (cross-XCD tail sharing; OFF by default, PGA_TP_POOL=d enables

@@ -34,6 +34,7 @@ uint32_t go_tp(K kernel, const GenArgs& a0, unsigned long long* parts, hipStream
   GenArgs a = a0;
   a.tp_unit = t.unit;
   a.tp_pool_units = a.tp_pool ? tp_pool_units(t, a.S) : 0u;
+  a.tp_skew = tp_skew_units(t, a.S);
   hipLaunchKernelGGL(kernel, t.grid, t.block, t.lds, s, a, parts);
   return t.grid;
 }

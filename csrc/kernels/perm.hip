@@ -307,20 +307,30 @@ __device__ __forceinline__ uint4 set16(uint4 v, uint32_t e, uint32_t x) {
   return v;
 }
 
-template <int GS, int OBJ>
-__global__ __launch_bounds__(kBlock) void perm_gen_fast(GenArgs a, unsigned long long* best_parts) {
+// TBL (integer distance matrices, the launcher's choice): the matrix as u16
+// in LDS (GenArgs::obj_aux, staged once per block) instead of an f32 L2
+// gather per edge — 1 = a symmetric matrix's strict lower triangle plus its
+// diagonal (65 KB at L = 256, so 1024-thread blocks still fit: 16 waves share
+// one table per CU), 2 = the full matrix.  Entries are exact (u16 -> f32),
+// so the tour sums equal the f32-matrix kernel's bit for bit.
+template <int GS, int OBJ, int TBL = 0>
+__global__ __launch_bounds__(1024) void perm_gen_fast(GenArgs a, unsigned long long* best_parts) {
   resolve_gen(a);
   float* smem = (float*)pga_dyn_lds;
-  unsigned long long* lds_red = (unsigned long long*)smem;
-  uint32_t* lds_elite = (uint32_t*)(smem + 8);
+  unsigned long long* lds_red = (unsigned long long*)smem;  // 16 entries: kHdrF holds them
+  uint32_t* lds_elite = (uint32_t*)(smem + 32);
   const uint32_t L = a.L, nch = a.chunks, lp = 8 * nch;
+  const uint32_t BLK = blockDim.x, NWv = BLK >> 6;
   float* coords = smem + kHdrF;
   uint16_t* arena = (uint16_t*)(coords + (OBJ == OBJ_TSP_EUC ? 16 * nch : 0));
+  // the table after the groups' arrays (16-byte aligned: lp is a multiple of 8)
+  uint16_t* tab = arena + (size_t)(BLK / GS) * 4 * lp;
+  const uint32_t tri = L * (L - 1) / 2;  // TBL 1: the diagonal's offset
 
   const uint32_t lane = lane_id();
   const uint32_t q = lane & (GS - 1);
   const uint32_t gbase = lane & ~(uint32_t)(GS - 1);
-  constexpr uint32_t GPB = kBlock / GS;
+  const uint32_t GPB = BLK / GS;
   const uint32_t g = threadIdx.x / GS;
   uint16_t* B = arena + (size_t)g * 4 * lp + lp;
   uint16_t* Cc = B + lp;
@@ -336,11 +346,13 @@ __global__ __launch_bounds__(kBlock) void perm_gen_fast(GenArgs a, unsigned long
   const uint32_t S32 = (uint32_t)a.S;
 
   if (a.n_elite > 0 && a.elite_idx == nullptr && blockIdx.x == 0) {
-    unsigned long long b = block_reduce_parts(a.best_cur, a.n_best_cur, lds_red);
+    unsigned long long b = block_reduce_parts_n(a.best_cur, a.n_best_cur, lds_red, NWv);
     if (threadIdx.x == 0) *lds_elite = (uint32_t)best_index(b);
   }
   if (OBJ == OBJ_TSP_EUC)
-    for (uint32_t i = threadIdx.x; i < 2 * L; i += kBlock) coords[i] = a.obj_data[i];
+    for (uint32_t i = threadIdx.x; i < 2 * L; i += BLK) coords[i] = a.obj_data[i];
+  if (TBL)
+    for (uint32_t i = threadIdx.x; i < a.obj_aux_bytes / 16; i += BLK) ((uint4*)tab)[i] = ((const uint4*)a.obj_aux)[i];
   __syncthreads();
 
   unsigned long long my_best = 0;
@@ -474,7 +486,14 @@ __global__ __launch_bounds__(kBlock) void perm_gen_fast(GenArgs a, unsigned long
           if (have && p < last) {
             const uint32_t nx = p + 1 < L ? (e < 7 ? get16(Cv, e + 1) : next_first) : first;
             const uint32_t u = min(get16(Cv, e), L - 1), w = min(nx, L - 1);
-            len += a.obj_data[u * L + w];
+            if constexpr (TBL == 1) {
+              const uint32_t hi_ = u > w ? u : w, lo_ = u > w ? w : u;
+              len += (float)tab[hi_ == lo_ ? tri + u : hi_ * (hi_ - 1) / 2 + lo_];
+            } else if constexpr (TBL == 2) {
+              len += (float)tab[u * L + w];
+            } else {
+              len += a.obj_data[u * L + w];
+            }
           }
         }
       }
@@ -488,9 +507,9 @@ __global__ __launch_bounds__(kBlock) void perm_gen_fast(GenArgs a, unsigned long
     }
   }
   if (best_parts) {
-    unsigned long long b = block_max_u64(my_best, lds_red);
+    unsigned long long b = block_max_u64_n(my_best, lds_red, NWv);
     if (threadIdx.x == 0) best_parts[blockIdx.x] = b;
-    if (a.stats_parts) block_stats_store(st, a.stats_parts);
+    if (a.stats_parts) block_stats_store_n(st, a.stats_parts, NWv);
   }
 }
 
@@ -538,25 +557,39 @@ uint32_t go(const GenArgs& a, unsigned long long* parts, hipStream_t s) {
   return grid;
 }
 
-template <int GS, int OBJ>
-uint32_t go_fast(const GenArgs& a, unsigned long long* parts, hipStream_t s) {
-  const size_t lds = perm_lds_bytes(GS, a.chunks, OBJ == OBJ_TSP_EUC);
-  auto k = perm_gen_fast<GS, OBJ>;
-  static bool configured = false;
-  if (!configured) {
-    allow_dynamic_lds((const void*)k);
-    configured = true;
-  }
-  const uint32_t gpb = kBlock / GS;
+template <int GS, int OBJ, int TBL>
+uint32_t go_fast_blk(const GenArgs& a, unsigned long long* parts, hipStream_t s, uint32_t blk) {
+  const size_t lds = perm_lds_bytes(GS, a.chunks, OBJ == OBJ_TSP_EUC, blk) + (TBL ? a.obj_aux_bytes : 0);
+  auto k = perm_gen_fast<GS, OBJ, TBL>;
+  static size_t avail = 0;
+  if (!avail) avail = allow_dynamic_lds((const void*)k);
+  const uint32_t gpb = blk / GS;
   const uint64_t need = (a.S + gpb - 1) / gpb;
   int per_cu = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)k, kBlock, lds) != hipSuccess || per_cu <= 0)
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)k, (int)blk, lds) != hipSuccess || per_cu <= 0)
     per_cu = 1;
   uint64_t cap = (uint64_t)device_cu_count() * per_cu;
   if (cap > kMaxGrid) cap = kMaxGrid;
   const uint32_t grid = (uint32_t)(need < cap ? need : cap);
-  hipLaunchKernelGGL(k, grid, kBlock, lds, s, a, parts);
+  hipLaunchKernelGGL(k, grid, blk, lds, s, a, parts);
   return grid;
+}
+
+template <int GS, int OBJ>
+uint32_t go_fast(const GenArgs& a, unsigned long long* parts, hipStream_t s) {
+  if constexpr (OBJ == OBJ_TSP || OBJ == OBJ_TSP_OPEN) {
+    // an integer matrix as u16 in LDS: the largest block (up to 16 waves,
+    // one table per CU) whose group arrays fit beside it
+    if (a.obj_aux && (a.obj_aux_kind == 1 || a.obj_aux_kind == 2) && a.obj_aux_bytes % 16 == 0) {
+      const size_t avail = 160 * 1024 - 1024;  // less the static LDS (block reductions)
+      for (uint32_t blk : {1024u, 512u, 256u}) {
+        if (perm_lds_bytes(GS, a.chunks, false, blk) + a.obj_aux_bytes > avail) continue;
+        if (a.obj_aux_kind == 1) return go_fast_blk<GS, OBJ, 1>(a, parts, s, blk);
+        return go_fast_blk<GS, OBJ, 2>(a, parts, s, blk);
+      }
+    }
+  }
+  return go_fast_blk<GS, OBJ, 0>(a, parts, s, kBlock);
 }
 
 template <int GS, int OBJ>

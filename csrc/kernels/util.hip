@@ -86,6 +86,21 @@ TpGeom tp_geometry(uint64_t S, uint32_t islands, const void* kernel, uint32_t ng
 
 uint32_t tp_dyn_lds_bytes(uint32_t nw, uint32_t pseg) { return dev::tp_dyn_lds(nw, pseg); }
 
+uint32_t tp_skew_units(const TpGeom& t, uint64_t S) {
+  // PGA_TP_SKEW = units each odd block of a pair hands to its even
+  // neighbour (one 16-wave block per CU only: there block b runs on XCD b % 8;
+  // at most a quarter of a block's units)
+  static const uint32_t d = [] {
+    // default 2 of the 64 units of the headline's blocks: interleaved A/B
+    // (round 4) 0 / 2 / 4 / 6 -> 90.7 / 90.2 / 92.7 / 95.4 us per generation
+    const char* e = std::getenv("PGA_TP_SKEW");
+    return e ? (uint32_t)std::strtoul(e, nullptr, 10) : 2u;
+  }();
+  if (d == 0 || t.block != dev::kTpMaxWaves * 64 || t.grid < 2) return 0;
+  const uint64_t per = (S + t.grid - 1) / t.grid, units = (per + t.unit - 1) / t.unit;
+  return d * 4 < units ? d : 0u;
+}
+
 uint32_t tp_pool_units(const TpGeom& t, uint64_t S) {
   // PGA_TP_POOL = d: 1/d of each block's units in the pair pool (default 0: none)
   static const uint32_t d = [] {

@@ -48,6 +48,27 @@ class TSP(Problem):
         return -self.tour_length(genomes)
 
     @staticmethod
+    def random_integer_euclidean(n: int, seed: int = 0, scale: float = 1000.0, open_path: bool = False) -> "TSP":
+        """Integer Euclidean instance (TSPLIB EUC_2D: nint of the distance of
+        cities placed uniformly in [0, scale)^2): symmetric, integer-valued,
+        so the GPU evaluates tours from a u16 copy of the matrix in LDS."""
+        g = torch.Generator().manual_seed(seed)
+        xy = torch.rand(n, 2, generator=g, dtype=torch.float64) * scale
+        return TSP(torch.round(torch.cdist(xy, xy)).float(), open_path=open_path)
+
+    @staticmethod
+    def reference_e3(n: int = 100, seed: int = 0) -> "TSP":
+        """The reference's E3 instance family (test3/gen.c:26-39): d[i][i+1] =
+        10, every other entry uniform in [10, 1009] (asymmetric, integer), so
+        the path 0 -> 1 -> ... -> n-1 of length 10 (n - 1) is planted.  The
+        reference scores the open path (test3/test.cu:30-34)."""
+        g = torch.Generator().manual_seed(seed)
+        d = torch.randint(10, 1010, (n, n), generator=g).float()
+        i = torch.arange(n - 1)
+        d[i, i + 1] = 10.0
+        return TSP(d, open_path=True)
+
+    @staticmethod
     def random_euclidean(n: int, seed: int = 0, open_path: bool = False) -> "TSP":
         g = torch.Generator().manual_seed(seed)
         xy = torch.rand(n, 2, generator=g) * 1000.0

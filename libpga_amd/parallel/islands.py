@@ -309,13 +309,25 @@ class IslandModel:
         all-reduce(max) and all stop together once it reaches ``target``.
         Returns the generations executed."""
         every = check_every or self.migrate_every or 1
-        done = 0
-        for _ in range(int(generations)):
+        migrates = self.migrate_every > 0 and self.world > 1 and self.k > 0
+        done, n = 0, int(generations)
+        while done < n:
             g = self.ga.generation
-            if self.migrate_every > 0 and g > 0 and g % self.migrate_every == 0 and self._pending is None:
+            if migrates and g > 0 and g % self.migrate_every == 0 and self._pending is None and not self.degraded:
                 self.start_migration()
                 if not self.overlap:
                     self.finish_migration()
+            if self._pending is None and self.ga.torch_objective is None and target is None:
+                # no exchange in flight and nothing to do between generations:
+                # every generation up to the next migration point in ONE
+                # engine call (C++ enqueues them back to back, no per-step
+                # Python on the host path)
+                step = n - done
+                if migrates:
+                    step = min(step, self.migrate_every - g % self.migrate_every)
+                self.ga.island.run(step)
+                done += step
+                continue
             self.ga.island.run(1)
             if self.ga.torch_objective is not None:
                 self.ga._custom_eval()

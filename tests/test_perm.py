@@ -97,6 +97,39 @@ def test_gpu_bitexact_general_matrix(xo, n, shape):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("xo", ["ox", "pmx"])
+@pytest.mark.parametrize("inst", ["int_euc256", "e3_100", "int_euc100_open"])
+def test_gpu_lds_matrix_bitexact(xo, inst, monkeypatch):
+    """Integer matrices evaluate from a u16 copy in LDS (symmetric: strict
+    triangle + diagonal in 16-wave blocks; asymmetric: the full matrix):
+    rows and scores equal the CPU backend and the f32 L2 path bit for bit."""
+    p = {"int_euc256": lambda: M.TSP.random_integer_euclidean(256, seed=2),
+         "e3_100": lambda: M.TSP.reference_e3(100, seed=1),
+         "int_euc100_open": lambda: M.TSP.random_integer_euclidean(100, seed=5, open_path=True)}[inst]()
+    kw = dict(seed=8, crossover=xo, mutation="inversion", mutation_rate=0.4, elitism=1)
+    g = pga.GeneticAlgorithm(p, 5000, device="cuda:0", **kw)
+    c = pga.GeneticAlgorithm(p, 5000, device="cpu", **kw)
+    monkeypatch.setenv("PGA_TSP_NO_LDS", "1")
+    f = pga.GeneticAlgorithm(p, 5000, device="cuda:0", **kw)
+    for _ in range(3):
+        g.run(1)
+        c.run(1)
+        f.run(1)
+    torch.cuda.synchronize()
+    assert torch.equal(g.rows.cpu(), c.rows) and torch.equal(g.scores.cpu(), c.scores)
+    assert torch.equal(g.rows, f.rows) and torch.equal(g.scores, f.scores)
+    assert is_perm(g.genomes().cpu())
+
+
+def test_reference_e3_instance():
+    p = M.TSP.reference_e3(100, seed=3)
+    d = p.dist
+    assert p.open_path and d.shape == (100, 100)
+    assert bool((d == d.round()).all()) and float(d.min()) >= 10 and float(d.max()) <= 1009
+    assert float(p.tour_length(torch.arange(100).unsqueeze(0))[0]) == 990.0
+
+
+@pytest.mark.gpu
 def test_gpu_tsp256_pop256k():
     """BASELINE config 5 shape on one GPU: TSP-256, pop = 256K, OX."""
     p = M.TSPEuclidean.random(256, seed=9)
