@@ -2,6 +2,7 @@
 """Many small islands on one device: batched launch vs one stream per island.
 
     python bench/bench_islands.py [--islands 8] [--pop 4096] [--length 1024] [--gens 500]
+                                  [--problem onemax|rastrigin30]
 
 LocalIslands runs its islands either as ONE launch per generation (island =
 grid y, Island::run_batched) or each island's launch on its own HIP stream
@@ -29,9 +30,13 @@ def main() -> int:
     ap.add_argument("--pop", type=int, default=4096)
     ap.add_argument("--length", type=int, default=1024)
     ap.add_argument("--gens", type=int, default=500)
+    ap.add_argument("--problem", default="onemax", choices=["onemax", "rastrigin30"])
     a = ap.parse_args()
+    if a.problem == "rastrigin30":
+        a.length = 30
     for batched in (True, False):
-        li = LocalIslands(pga.models.OneMax(a.length), a.islands, a.pop, seed=1, device="cuda:0", migrate_every=0,
+        prob = pga.models.OneMax(a.length) if a.problem == "onemax" else pga.models.Rastrigin(30)
+        li = LocalIslands(prob, a.islands, a.pop, seed=1, device="cuda:0", migrate_every=0,
                           elitism=1, batched=batched)
         li.run(20)
         torch.cuda.synchronize()
@@ -39,7 +44,8 @@ def main() -> int:
         li.run(a.gens)
         torch.cuda.synchronize()
         dt = time.perf_counter() - t0
-        print(json.dumps({"mode": "batched" if batched else "streams", "islands": a.islands, "pop": a.pop,
+        print(json.dumps({"problem": a.problem, "mode": "batched" if batched else "streams", "islands": a.islands,
+                          "pop": a.pop,
                           "length": a.length, "gens_per_sec": a.gens / dt, "us_per_gen": dt / a.gens * 1e6,
                           "evals_per_sec": a.gens * a.islands * a.pop / dt,
                           "batched_generations": li.batched_generations}), flush=True)

@@ -413,7 +413,7 @@ bool Island::real_qk() const {
   // quantized tournament keys feed only the two-phase kernel (real_gen_tp),
   // which small populations do not take: there they would cost a launch
   return on_gpu() && cfg_.encoding == ENC_REAL && cfg_.objective != OBJ_NONE && !jit_ &&
-         cfg_.S >= real_tp_min_population();
+         cfg_.S * batch_n_ >= real_tp_min_population();
 }
 
 void Island::prepare_generation() {
@@ -507,28 +507,48 @@ void Island::run_plain(uint32_t n) {
 
 bool Island::run_batched(const std::vector<Island*>& isls, uint32_t n, hipStream_t s) {
   const size_t N = isls.size();
-  if (N < 2 || N > binary_max_batch()) return false;
+  if (N < 2 || !isls[0]) return false;
   const Island* i0 = isls[0];
+  const bool bin = i0->cfg_.encoding == ENC_BINARY, real = i0->cfg_.encoding == ENC_REAL;
+  if ((!bin && !real) || N > (bin ? binary_max_batch() : real_max_batch())) return false;
   for (const Island* i : isls) {
-    if (!i || !i->on_gpu() || i->device_ != i0->device_ || i->cfg_.encoding != ENC_BINARY || i->jit_ ||
+    if (!i || !i->on_gpu() || i->device_ != i0->device_ || i->cfg_.encoding != i0->cfg_.encoding || i->jit_ ||
         i->user_fn_ || i->user_xo_fn_ || i->user_mut_fn_ || i->hist_on_ || i->cfg_.S != i0->cfg_.S || i->cfg_.L != i0->cfg_.L)
       return false;
     for (const Island* j : isls)
       if (j != i && j->rows_[0].ptr == i->rows_[0].ptr) return false;  // the same island twice
   }
-  {  // binary_launch_batch's conditions from the configuration alone, before
+  {  // the batched kernels' conditions from the configuration alone, before
      // any launch (an island that cannot qualify pays no extra prepare pass)
     const Config& c = i0->cfg_;
-    const bool obj_ok = c.objective == OBJ_ONEMAX || c.objective == OBJ_LEADING_ONES || c.objective == OBJ_TRAP;
     const bool sel_ok = (c.selection == SEL_TOURNAMENT && c.tour_k == 2) || c.selection == SEL_RANDOM ||
                         c.selection == SEL_RANK || c.selection == SEL_ROULETTE;
     const bool o32 = (c.S + kRowPad) * (uint64_t)i0->row_words_ * 4u <= 0xFFFFFFFFull;
-    if (!obj_ok || !sel_ok || !o32 || i0->chunks_ > 64 || c.n_elite > 64 || force_generic_kernels()) return false;
-    for (const Island* i : isls)
-      if (!integer_objective(i->cfg_.objective, i->cfg_.L) || !i->keys_[0].ptr || i->cfg_.objective != c.objective)
-        return false;
+    if (!sel_ok || !o32 || i0->chunks_ > 64 || c.n_elite > 64 || force_generic_kernels()) return false;
+    if (bin) {
+      if (c.objective != OBJ_ONEMAX && c.objective != OBJ_LEADING_ONES && c.objective != OBJ_TRAP) return false;
+      for (const Island* i : isls)
+        if (!integer_objective(i->cfg_.objective, i->cfg_.L) || !i->keys_[0].ptr || i->cfg_.objective != c.objective)
+          return false;
+    } else {
+      const bool obj_ok = c.objective == OBJ_SPHERE || c.objective == OBJ_RASTRIGIN || c.objective == OBJ_ROSENBROCK ||
+                          c.objective == OBJ_ACKLEY || c.objective == OBJ_GRIEWANK || c.objective == OBJ_SCHWEFEL ||
+                          c.objective == OBJ_LINEAR || c.objective == OBJ_KNAPSACK_REAL;
+      if (!obj_ok || (c.obj_i & 2) || c.S * N < real_tp_min_population()) return false;
+      for (const Island* i : isls)
+        if (i->cfg_.objective != c.objective || i->cfg_.obj_i != c.obj_i) return false;
+    }
   }
   TraceRange tr("pga.run_batched");
+  // REAL: the batch takes the two-phase kernel, which tournaments on the
+  // quantized keys, so every island keeps them for the batch's population
+  for (Island* I : isls) I->batch_n_ = (uint32_t)N;
+  struct Reset {
+    const std::vector<Island*>& v;
+    ~Reset() {
+      for (Island* I : v) I->batch_n_ = 1;
+    }
+  } reset{isls};
   std::vector<GenArgs> args(N);
   std::vector<unsigned long long*> parts(N);
   for (uint32_t g = 0; g < n; ++g) {
@@ -539,7 +559,8 @@ bool Island::run_batched(const std::vector<Island*>& isls, uint32_t n, hipStream
       args[k] = I.make_args(MODE_GEN);
       parts[k] = (unsigned long long*)I.best_[I.cur_ ^ 1].ptr;
     }
-    const uint32_t grid = binary_launch_batch(args.data(), parts.data(), (uint32_t)N, s);
+    const uint32_t grid = bin ? binary_launch_batch(args.data(), parts.data(), (uint32_t)N, s)
+                              : real_launch_batch(args.data(), parts.data(), (uint32_t)N, s);
     if (grid == 0) {
       if (g == 0) return false;  // not eligible (decided on the first generation's arguments)
       throw std::logic_error("batched islands stopped qualifying mid-run");
@@ -549,7 +570,7 @@ bool Island::run_batched(const std::vector<Island*>& isls, uint32_t n, hipStream
       const int nx = I.cur_ ^ 1;
       I.n_best_[nx] = grid;
       I.stats_ok_[nx] = args[k].stats_parts != nullptr;
-      I.qk_valid_[nx] = false;
+      I.qk_valid_[nx] = real && args[k].qk != nullptr;  // the REAL kernel writes the keys it is given
       I.swap();
     }
   }

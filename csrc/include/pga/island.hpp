@@ -263,6 +263,7 @@ class Island {
   Buffer obj_aux_;        // derived objective table (TSP: the integer matrix as u16, GenArgs::obj_aux)
   uint32_t aux_kind_ = 0, aux_bytes_ = 0, aux_version_ = ~0u;
   bool aux_on_ = true;    // PGA_TSP_NO_LDS unset at construction
+  uint32_t batch_n_ = 1;  // islands of the batch this one runs in (run_batched), else 1
   uint32_t tp_seq_ = 0;   // their per-launch stamp
   hipStream_t cap_stream_ = nullptr;
   hipGraphExec_t gexec_ = nullptr;

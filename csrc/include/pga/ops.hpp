@@ -82,6 +82,12 @@ bool binary_tp_plan(const GenArgs& a, uint32_t& gs, bool& full, bool& dense);
 bool real_tp_plan(const GenArgs& a, uint32_t& gs);
 // smallest REAL population that takes real_gen_tp (PGA_TP_MIN_S overrides)
 uint64_t real_tp_min_population();
+// REAL batched islands (real_batch.hip): whether an island qualifies as one
+// of n, and one MODE_GEN launch of up to real_max_batch() same-shape islands
+// (returns each island's grid; 0 = not launched, run them one by one)
+bool real_tp_batchable(const GenArgs& a, uint32_t n);
+uint32_t real_max_batch();
+uint32_t real_launch_batch(const GenArgs* args, unsigned long long* const* parts, uint32_t n, hipStream_t s);
 // batched islands (binary_batch.hip): one MODE_GEN launch of up to
 // binary_max_batch() same-shape islands (args[i], best partials parts[i]);
 // returns each island's grid (its best-partials count), 0 when the islands do

@@ -82,14 +82,15 @@ __device__ __forceinline__ void real_sparse_group(const GenArgs& a, uint64_t chi
 // a contiguous share of the population, in rounds (tp.hpp tp_block_range):
 //   TOURNAMENTS  tp_select_segment (tp.hpp): one lane per child, every f32
 //                score load of a 256-child segment in flight together
-//   BREED        after one block barrier, UNITS of U <= 64 children pulled
-//                from the block's LDS counter; per unit, RESOLVE (one lane
+//   BREED        UNITS of U <= 64 children pulled from the block's LDS
+//                counter once no segment is left (a unit waits for its
+//                segment's ready flag); per unit, RESOLVE (one lane
 //                per child): the misc block
 //                (crossover test, cut points / arithmetic u, mutation count
 //                K), the first min(K, 3) distinct mutation positions and
 //                their values (gaussian z by gauss_z) -> a 32-byte child
 //                RECORD in the wave's LDS ring (2 units); per step: parent
-//                rows loaded one step ahead, crossover (BLX: one Philox block
+//                rows loaded PD steps ahead, crossover (BLX: one Philox block
 //                per lane), the record's mutations (K > 3: the group
 //                continues the sequence), objective, group butterfly, stores.
 // So a child costs 2 Philox blocks of child-level words computed once (not
@@ -149,7 +150,7 @@ __device__ __forceinline__ void rot_tile4(float* xw, const float* ms, float z[4]
 }
 
 template <int GS, int OBJ, bool ROT>
-__global__ __launch_bounds__(kTpMaxWaves * 64) void real_gen_tp(GenArgs a, unsigned long long* best_parts) {
+__device__ __forceinline__ void real_gen_tp_body(GenArgs a, unsigned long long* best_parts) {
   static_assert(!ROT || GS == 4 || GS == 8, "wave-local rotation: 16 or 32 padded dims");
   resolve_gen(a);
   a.objective = OBJ;  // compile-time objective: the term switches fold away
@@ -169,7 +170,9 @@ __global__ __launch_bounds__(kTpMaxWaves * 64) void real_gen_tp(GenArgs a, unsig
   __shared__ uint32_t lds_thr[kMutCap];
   __shared__ uint32_t lds_el[kTpMaxElite];  // elite sources
   __shared__ unsigned long long lds_red[kTpMaxWaves];
-  __shared__ uint32_t lds_next;  // the round's next unbred unit
+  __shared__ uint32_t lds_next;   // the round's next unbred unit
+  __shared__ uint32_t lds_tnext;  // the round's next tournament segment
+  __shared__ uint32_t lds_ready[kTpMaxSegs];  // per segment: its parents are in LDS
   __shared__ __attribute__((aligned(16))) float lds_rot[ROT ? (kTpMaxWaves + 2) * 16 * kRotTW : 1];  // wave tiles + M
 
   const uint32_t lane = lane_id(), wid = threadIdx.x >> 6;
@@ -208,7 +211,7 @@ __global__ __launch_bounds__(kTpMaxWaves * 64) void real_gen_tp(GenArgs a, unsig
 
   const uint32_t U = tp_unit(a, NG);  // children per breed unit (tp.hpp)
   uint32_t bbegin, bend;              // this block's children
-  tp_block_range(S, U, bbegin, bend);
+  tp_block_range(S, U, bbegin, bend, a.tp_skew);
   const uint32_t pcap = tp_par_cap(NW, PSEG);
 
   float* xw = lds_rot + (ROT ? wid * 16 * kRotTW : 0);          // this wave's X/Z tile
@@ -229,7 +232,8 @@ __global__ __launch_bounds__(kTpMaxWaves * 64) void real_gen_tp(GenArgs a, unsig
   }
   if (per_gene)
     for (uint32_t i = threadIdx.x; i < kMutCap; i += blockDim.x) lds_thr[i] = a.mut_thr[i];
-  if (threadIdx.x == 0) lds_next = 0;
+  if (threadIdx.x == 0) lds_next = lds_tnext = 0;
+  if (threadIdx.x < kTpMaxSegs) lds_ready[threadIdx.x] = 0;
 
   unsigned long long my_best = 0;
   ScoreStats st;
@@ -243,18 +247,31 @@ __global__ __launch_bounds__(kTpMaxWaves * 64) void real_gen_tp(GenArgs a, unsig
 
     // TOURNAMENTS of the round (contestants wait in the wave's record ring),
     // on the quantized u16 keys when the objective scores the children here
-    for (uint32_t sg = wid; sg < nseg; sg += NW) {
+    // pulled from a counter, each segment published by a ready flag; a unit's
+    // RESOLVE waits for its segment's flag (no block barrier, binary_dev.hpp)
+    for (;;) {
+      uint32_t ts = 0;
+      if (lane == 0) ts = __hip_atomic_fetch_add(&lds_tnext, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      const uint32_t sg = __builtin_amdgcn_readfirstlane(ts);
+      if (sg >= nseg) break;
       const uint32_t begin = rbeg + sg * kSegBatches * 64u;
       const uint32_t end = begin + kSegBatches * 64u < rend ? begin + kSegBatches * 64u : rend;
       tp_select_segment<BUILTIN ? TP_QKEY16 : TP_F32>(a, begin, end, lane, &rec[0][0][0],
                                                     lds_par + sg * kSegBatches * 64u);
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");  // the parents before the flag
+      if (lane == 0) __hip_atomic_store(&lds_ready[sg], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
-    __syncthreads();  // every parent of the round in LDS
 
     // RESOLVE: parents, crossover plan, mutation positions and draws of the
     // round's unit BI -> the records of ring slot SL
 #define PGA_RTP_RESOLVE(BI, SL)                                                                              \
   {                                                                                                          \
+    {  /* the unit's tournament segment is done (wave-uniform spin, rare) */                                 \
+      const uint32_t sg_ = (BI) * U / (kSegBatches * 64u);                                                   \
+      while (__hip_atomic_load(&lds_ready[sg_], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == 0u)       \
+        __builtin_amdgcn_s_sleep(1);                                                                         \
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");                                                 \
+    }                                                                                                        \
     const uint32_t bs_ = rbeg + (BI) * U;                                                                    \
     const uint32_t be_ = bs_ + U < rend ? bs_ + U : rend;                                                    \
     const uint32_t tc = bs_ + lane;                                                                          \
@@ -467,8 +484,9 @@ __global__ __launch_bounds__(kTpMaxWaves * 64) void real_gen_tp(GenArgs a, unsig
 #undef PGA_RTP_JIT_EVAL
     }
 #undef PGA_RTP_RESOLVE
-    __syncthreads();  // every wave out of the round's counter before it is reset
-    if (threadIdx.x == 0) lds_next = 0;
+    __syncthreads();  // every wave out of the round's counters before they are reset
+    if (threadIdx.x == 0) lds_next = lds_tnext = 0;
+    if (threadIdx.x < kTpMaxSegs) lds_ready[threadIdx.x] = 0;
   }
 #undef RROW
 #undef RELEM
@@ -477,6 +495,25 @@ __global__ __launch_bounds__(kTpMaxWaves * 64) void real_gen_tp(GenArgs a, unsig
     if (threadIdx.x == 0) best_parts[blockIdx.x] = bb;
     if (a.stats_parts) block_stats_store_n(st, a.stats_parts, NW);
   }
+}
+
+template <int GS, int OBJ, bool ROT>
+__global__ __launch_bounds__(kTpMaxWaves * 64) void real_gen_tp(GenArgs a, unsigned long long* best_parts) {
+  real_gen_tp_body<GS, OBJ, ROT>(a, best_parts);
+}
+
+// Batched islands: up to kRealMaxBatch same-shape islands of one device in
+// ONE launch, island = blockIdx.y (binary_gen_tp_batch's scheme, real.hip
+// real_launch_batch).  The reference's islands are at most MAX_POPULATIONS =
+// 10 per solver (include/pga.h:44), run one after another (src/pga.cu:272-276).
+constexpr uint32_t kRealMaxBatch = 10;
+struct RealBatch {
+  GenArgs a[kRealMaxBatch];
+  unsigned long long* parts[kRealMaxBatch];
+};
+template <int GS, int OBJ>
+__global__ __launch_bounds__(kTpMaxWaves * 64) void real_gen_tp_batch(RealBatch b) {
+  real_gen_tp_body<GS, OBJ, false>(b.a[blockIdx.y], b.parts[blockIdx.y]);
 }
 
 }  // namespace (jitgen / anonymous)

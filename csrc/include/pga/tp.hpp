@@ -159,8 +159,8 @@ __device__ __forceinline__ void tp_select_segment(const GenArgs& a, uint32_t beg
 // so that every wave gets a unit), processed in ROUNDS of at most
 // tp_par_cap(nw) children: the waves pull the round's 256-child tournament
 // segments from one LDS counter, then its units from another until none is
-// left; a unit waits for its segment's ready flag (binary_gen_tp: no block
-// barrier between the phases; real_gen_tp: one barrier).  The headline launch is one
+// left; a unit waits for its segment's ready flag (no block barrier between
+// the phases).  The headline launch is one
 // 16-wave block per CU (its LDS admits no second), so the counter balances
 // every wave slot of the CU: the oldest-first issue order only decides WHICH
 // wave breeds a unit, and the last ~20 us of thinning grid that equal static

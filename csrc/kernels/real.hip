@@ -463,6 +463,7 @@ uint32_t go_tp(K kernel, const GenArgs& a0, unsigned long long* parts, hipStream
   const TpGeom t = tp_geometry(a0.S, 1, (const void*)kernel, 64 / group_size(a0.chunks), rot ? 6 : 7);
   GenArgs a = a0;
   a.tp_unit = t.unit;
+  a.tp_skew = tp_skew_units(t, a.S);
   hipLaunchKernelGGL(kernel, t.grid, t.block, t.lds, s, a, parts);
   return t.grid;
 }
@@ -499,6 +500,18 @@ bool real_tp_eligible(const GenArgs& a, uint32_t GS, bool rot) {
 }
 
 }  // namespace
+
+bool real_tp_batchable(const GenArgs& a, uint32_t n) {
+  // real_tp_eligible for one of n batched islands: the batch fills the
+  // device, so the population threshold applies to all n together; no
+  // rotation (rotated objectives run their islands on streams)
+  if (a.chunks > 64u || n == 0) return false;
+  if ((a.obj_i & 2) && a.obj_data && real_obj_rotatable(a.objective)) return false;
+  GenArgs b = a;
+  b.S = a.S * n;  // only the threshold reads it below
+  if (!real_tp_eligible(b, group_size(a.chunks), false)) return false;
+  return (a.S + kRowPad) * (uint64_t)a.row_words * 4u <= 0xFFFFFFFFull;
+}
 
 bool real_tp_plan(const GenArgs& a, uint32_t& gs) {
   gs = group_size(a.chunks);

@@ -76,9 +76,35 @@ def test_local_islands_batched_launch_matches_streams_gpu(L, kw):
 
 
 @pytest.mark.gpu
-def test_local_islands_batched_falls_back_gpu():
-    # a float objective does not batch: the islands run on their streams
-    li = LocalIslands(pga.models.Rastrigin(8), 3, 2048, seed=1, device="cuda:0", migrate_every=0)
+@pytest.mark.parametrize("prob,kw", [("sphere30", {}), ("rosen30", dict(selection="rank")), ("sphere100", {})])
+def test_local_islands_real_batched_matches_streams_gpu(prob, kw):
+    # REAL islands in ONE launch per generation (real_gen_tp_batch, island =
+    # grid y) evolve exactly as on their own streams (the generic kernel at
+    # this island size): polynomial objectives are exact on both
+    p = {"sphere30": lambda: pga.models.Sphere(30), "rosen30": lambda: pga.models.Rosenbrock(30),
+         "sphere100": lambda: pga.models.Sphere(100)}[prob]
+    common = dict(seed=5, device="cuda:0", migrate_every=5, migrate_pct=0.02, elitism=1, **kw)
+    a = LocalIslands(p(), 8, 4096, **common)
+    b = LocalIslands(p(), 8, 4096, batched=False, **common)
+    a.run(12)
+    b.run(12)
+    torch.cuda.synchronize()
+    assert a.batched_generations == 12 and b.batched_generations == 0
+    for x, y in zip(a.islands, b.islands):
+        assert torch.equal(x.rows, y.rows) and torch.equal(x.scores, y.scores)
+        assert x.best_score() == y.best_score()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("prob", ["small", "rotated"])
+def test_local_islands_batched_falls_back_gpu(prob):
+    # a REAL batch below the two-phase kernel's population, or a rotated
+    # objective, runs its islands on their streams
+    if prob == "small":
+        li = LocalIslands(pga.models.Rastrigin(8), 3, 2048, seed=1, device="cuda:0", migrate_every=0)
+    else:
+        li = LocalIslands(pga.models.Rastrigin(16, rotate=True, seed=1), 4, 8192, seed=1, device="cuda:0",
+                          migrate_every=0)
     li.run(3)
     torch.cuda.synchronize()
     assert li.batched_generations == 0

@@ -32,7 +32,7 @@ ARCH = os.environ.get("PGA_ARCH", "gfx950")
 SPLIT = {"csrc/kernels/binary_gs.hip": [(f"gs{g}", f"-DPGA_BIN_GS={g}") for g in (1, 2, 4, 8, 16, 32, 64)]}
 KERNELS = ["csrc/kernels/binary.hip", "csrc/kernels/real.hip", "csrc/kernels/perm.hip",
            "csrc/kernels/util.hip", "csrc/kernels/compat.hip", "csrc/kernels/qubo.hip",
-           "csrc/kernels/sort.hip", "csrc/kernels/binary_batch.hip"]
+           "csrc/kernels/sort.hip", "csrc/kernels/binary_batch.hip", "csrc/kernels/real_batch.hip"]
 HOST = ["csrc/engine/island.cpp", "csrc/engine/trace.cpp", "csrc/engine/jit.cpp", "csrc/cpu/cpu_ops.cpp", "csrc/cpu/cpu_real.cpp", "csrc/cpu/cpu_perm.cpp", "csrc/cpu/parallel.cpp"]
 CAPI = ["csrc/capi/pga_capi.cpp", "csrc/capi/comm.cpp", "csrc/capi/comm_rccl.cpp"]
 COMPAT = []

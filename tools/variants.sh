@@ -19,7 +19,7 @@ mkdir -p build/variants
 flags="-O3 -std=c++17 -Icsrc/include -Iinclude -x hip --offload-arch=gfx950 -munsafe-fp-atomics -ffp-contract=fast"
 /opt/rocm/bin/hipcc $flags -c bench/gen_bench.cpp -o build/variants/gen_bench.o
 others=""
-for k in binary binary_batch perm qubo real util compat sort; do
+for k in binary binary_batch real_batch perm qubo real util compat sort; do
   [ "$k" = "$base" ] || others="$others $O/csrc_kernels_$k.k.o"
 done
 extra=""
