@@ -544,9 +544,7 @@ __device__ __forceinline__ void binary_gen_tp_body(GenArgs a, unsigned long long
     // ring (free until it breeds).  A wave breeds as soon as no segment is
     // left; a unit's RESOLVE waits for its segment's flag (no block barrier)
     for (;;) {
-      uint32_t ts = 0;
-      if (lane == 0) ts = __hip_atomic_fetch_add(&lds_tnext, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      const uint32_t sg = __builtin_amdgcn_readfirstlane(ts);
+      const uint32_t sg = tp_ticket(&lds_tnext, lane);
       if (sg >= nseg) break;
       const uint32_t begin = rbeg + sg * kSegBatches * 64u;
       const uint32_t end = begin + kSegBatches * 64u < rend ? begin + kSegBatches * 64u : rend;
@@ -652,7 +650,7 @@ __device__ __forceinline__ void binary_gen_tp_body(GenArgs a, unsigned long long
       // publish: the segment's parents (this wave's LDS stores, in order)
       // before its flag
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-      if (lane == 0) __hip_atomic_store(&lds_ready[sg], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      tp_flag_set(&lds_ready[sg]);
     }
 #ifdef PGA_TP_TIMING
     const unsigned long long clkB = clock64();
@@ -758,9 +756,7 @@ __device__ __forceinline__ void binary_gen_tp_body(GenArgs a, unsigned long long
   {                                                                                                         \
     US = kNoUnit;                                                                                           \
     if (!steal) {                                                                                           \
-      uint32_t tk_ = 0;                                                                                     \
-      if (lane == 0) tk_ = __hip_atomic_fetch_add(&lds_next, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); \
-      tk_ = __builtin_amdgcn_readfirstlane(tk_);                                                            \
+      const uint32_t tk_ = tp_ticket(&lds_next, lane);                                                      \
       if (tk_ < nb) {                                                                                       \
         US = rbeg + tk_ * U;                                                                                \
         UE = US + U < rend ? US + U : rend;                                                                 \

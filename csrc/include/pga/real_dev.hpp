@@ -250,16 +250,14 @@ __device__ __forceinline__ void real_gen_tp_body(GenArgs a, unsigned long long* 
     // pulled from a counter, each segment published by a ready flag; a unit's
     // RESOLVE waits for its segment's flag (no block barrier, binary_dev.hpp)
     for (;;) {
-      uint32_t ts = 0;
-      if (lane == 0) ts = __hip_atomic_fetch_add(&lds_tnext, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      const uint32_t sg = __builtin_amdgcn_readfirstlane(ts);
+      const uint32_t sg = tp_ticket(&lds_tnext, lane);
       if (sg >= nseg) break;
       const uint32_t begin = rbeg + sg * kSegBatches * 64u;
       const uint32_t end = begin + kSegBatches * 64u < rend ? begin + kSegBatches * 64u : rend;
       tp_select_segment<BUILTIN ? TP_QKEY16 : TP_F32>(a, begin, end, lane, &rec[0][0][0],
                                                     lds_par + sg * kSegBatches * 64u);
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");  // the parents before the flag
-      if (lane == 0) __hip_atomic_store(&lds_ready[sg], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      tp_flag_set(&lds_ready[sg]);
     }
 
     // RESOLVE: parents, crossover plan, mutation positions and draws of the
@@ -328,12 +326,9 @@ __device__ __forceinline__ void real_gen_tp_body(GenArgs a, unsigned long long* 
     // a unit into the other ring slot when it enters it; every vector memory
     // operation is unconditional (an exhausted load cursor re-reads the breed
     // cursor's rows; the children past S, at the end only, write the padding)
-    uint32_t tk = 0;
-    if (lane == 0) tk = __hip_atomic_fetch_add(&lds_next, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    const uint32_t b0 = __builtin_amdgcn_readfirstlane(tk);  // the wave's first unit
+    const uint32_t b0 = tp_ticket(&lds_next, lane);  // the wave's first unit
     if (b0 < nb) {
-      if (lane == 0) tk = __hip_atomic_fetch_add(&lds_next, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      uint32_t bn = __builtin_amdgcn_readfirstlane(tk);  // the next ticket (>= nb: none)
+      uint32_t bn = tp_ticket(&lds_next, lane);  // the next ticket (>= nb: none)
       PGA_RTP_RESOLVE(b0, 0u)
       uint32_t slot = 0, i = 0, bs = rbeg + b0 * U;  // breed cursor
       uint32_t nst = ((bs + U < rend ? bs + U : rend) - bs + NG - 1) / NG;
@@ -349,9 +344,7 @@ __device__ __forceinline__ void real_gen_tp_body(GenArgs a, unsigned long long* 
       lbs = rbeg + bn * U;                                                                                  \
       lnst = ((lbs + U < rend ? lbs + U : rend) - lbs + NG - 1) / NG;                                       \
       lpend = false;                                                                                        \
-      if (lane == 0)                                                                                        \
-        tk = __hip_atomic_fetch_add(&lds_next, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);         \
-      bn = __builtin_amdgcn_readfirstlane(tk);                                                              \
+      bn = tp_ticket(&lds_next, lane);                                                                      \
     }                                                                                                       \
     const uint4 r = rec[lmore ? lslot : slot][(lmore ? li : i) * NG + g][0];                                \
     YA = RROW(cur, r.x, qq);                                                                                \

@@ -195,6 +195,24 @@ __device__ __forceinline__ uint32_t tp_unit(const GenArgs& a, uint32_t NG) {
   return u >= lo && u <= 64u && (u & (u - 1u)) == 0u ? u : 64u;
 }
 
+// One ticket per wave from an LDS counter, with no lane divergence: every
+// lane of the (full, converged) wave adds one — the atomic optimizer folds
+// the uniform add into ONE ds_add of 64 and hands the first lane the old
+// value — so the counter counts in steps of 64 and the ticket is the old
+// value / 64.  An `if (lane == 0)` around the atomic inside the kernels'
+// ticket loops left hipcc's structurizer a divergent region in a uniform
+// loop, and real_gen_tp hung (round 4); a per-lane 0/1 add made the
+// optimizer scan the wave with a 64-step scalar loop.
+__device__ __forceinline__ uint32_t tp_ticket(uint32_t* ctr, uint32_t lane) {
+  (void)lane;
+  const uint32_t t = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  return __builtin_amdgcn_readfirstlane(t) >> 6;
+}
+// publish a ready flag: every lane stores the same value (no divergence)
+__device__ __forceinline__ void tp_flag_set(uint32_t* flag) {
+  __hip_atomic_store(flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
 // the share [bb, be) of block blk.  skew (units, < per / U): in each block
 // pair (2p, 2p + 1) the odd block hands `skew` units to the even one.  The
 // dispatcher deals a launch's blocks to the XCDs round robin (block b ->
