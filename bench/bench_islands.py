@@ -2,7 +2,7 @@
 """Many small islands on one device: batched launch vs one stream per island.
 
     python bench/bench_islands.py [--islands 8] [--pop 4096] [--length 1024] [--gens 500]
-                                  [--problem onemax|rastrigin30]
+                                  [--problem onemax|rastrigin30|tsp128]
 
 LocalIslands runs its islands either as ONE launch per generation (island =
 grid y, Island::run_batched) or each island's launch on its own HIP stream
@@ -30,12 +30,13 @@ def main() -> int:
     ap.add_argument("--pop", type=int, default=4096)
     ap.add_argument("--length", type=int, default=1024)
     ap.add_argument("--gens", type=int, default=500)
-    ap.add_argument("--problem", default="onemax", choices=["onemax", "rastrigin30"])
+    ap.add_argument("--problem", default="onemax", choices=["onemax", "rastrigin30", "tsp128"])
     a = ap.parse_args()
-    if a.problem == "rastrigin30":
-        a.length = 30
+    if a.problem != "onemax":
+        a.length = 30 if a.problem == "rastrigin30" else 128
     for batched in (True, False):
-        prob = pga.models.OneMax(a.length) if a.problem == "onemax" else pga.models.Rastrigin(30)
+        prob = {"onemax": lambda: pga.models.OneMax(a.length), "rastrigin30": lambda: pga.models.Rastrigin(30),
+                "tsp128": lambda: pga.models.TSP.random_euclidean(128, seed=1)}[a.problem]()
         li = LocalIslands(prob, a.islands, a.pop, seed=1, device="cuda:0", migrate_every=0,
                           elitism=1, batched=batched)
         li.run(20)

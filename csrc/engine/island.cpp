@@ -510,7 +510,9 @@ bool Island::run_batched(const std::vector<Island*>& isls, uint32_t n, hipStream
   if (N < 2 || !isls[0]) return false;
   const Island* i0 = isls[0];
   const bool bin = i0->cfg_.encoding == ENC_BINARY, real = i0->cfg_.encoding == ENC_REAL;
-  if ((!bin && !real) || N > (bin ? binary_max_batch() : real_max_batch())) return false;
+  const bool perm = i0->cfg_.encoding == ENC_PERMUTATION;
+  if ((!bin && !real && !perm) || N > (bin ? binary_max_batch() : real ? real_max_batch() : perm_max_batch()))
+    return false;
   for (const Island* i : isls) {
     if (!i || !i->on_gpu() || i->device_ != i0->device_ || i->cfg_.encoding != i0->cfg_.encoding || i->jit_ ||
         i->user_fn_ || i->user_xo_fn_ || i->user_mut_fn_ || i->hist_on_ || i->cfg_.S != i0->cfg_.S || i->cfg_.L != i0->cfg_.L)
@@ -524,8 +526,14 @@ bool Island::run_batched(const std::vector<Island*>& isls, uint32_t n, hipStream
     const bool sel_ok = (c.selection == SEL_TOURNAMENT && c.tour_k == 2) || c.selection == SEL_RANDOM ||
                         c.selection == SEL_RANK || c.selection == SEL_ROULETTE;
     const bool o32 = (c.S + kRowPad) * (uint64_t)i0->row_words_ * 4u <= 0xFFFFFFFFull;
-    if (!sel_ok || !o32 || i0->chunks_ > 64 || c.n_elite > 64 || force_generic_kernels()) return false;
-    if (bin) {
+    if (perm) {  // perm_gen_fast: every selection; the TSP objectives, one chunk per lane
+      if (c.objective != OBJ_TSP && c.objective != OBJ_TSP_OPEN && c.objective != OBJ_TSP_EUC) return false;
+      if (i0->chunks_ > 64 || force_generic_kernels()) return false;
+      for (const Island* i : isls)
+        if (i->cfg_.objective != c.objective) return false;
+    } else if (!sel_ok || !o32 || i0->chunks_ > 64 || c.n_elite > 64 || force_generic_kernels()) {
+      return false;
+    } else if (bin) {
       if (c.objective != OBJ_ONEMAX && c.objective != OBJ_LEADING_ONES && c.objective != OBJ_TRAP) return false;
       for (const Island* i : isls)
         if (!integer_objective(i->cfg_.objective, i->cfg_.L) || !i->keys_[0].ptr || i->cfg_.objective != c.objective)
@@ -559,8 +567,9 @@ bool Island::run_batched(const std::vector<Island*>& isls, uint32_t n, hipStream
       args[k] = I.make_args(MODE_GEN);
       parts[k] = (unsigned long long*)I.best_[I.cur_ ^ 1].ptr;
     }
-    const uint32_t grid = bin ? binary_launch_batch(args.data(), parts.data(), (uint32_t)N, s)
-                              : real_launch_batch(args.data(), parts.data(), (uint32_t)N, s);
+    const uint32_t grid = bin    ? binary_launch_batch(args.data(), parts.data(), (uint32_t)N, s)
+                          : real ? real_launch_batch(args.data(), parts.data(), (uint32_t)N, s)
+                                 : perm_launch_batch(args.data(), parts.data(), (uint32_t)N, s);
     if (grid == 0) {
       if (g == 0) return false;  // not eligible (decided on the first generation's arguments)
       throw std::logic_error("batched islands stopped qualifying mid-run");

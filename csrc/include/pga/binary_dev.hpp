@@ -652,6 +652,10 @@ __device__ __forceinline__ void binary_gen_tp_body(GenArgs a, unsigned long long
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
       tp_flag_set(&lds_ready[sg]);
     }
+    // several blocks per CU (the 4-wave grid): a barrier parks the waiting
+    // waves (a flag spin would take issue slots from the other blocks' waves:
+    // REAL at S = 100K, 36 -> 55 us/gen); one block per CU: the flags alone
+    if (NW < kTpMaxWaves) __syncthreads();
 #ifdef PGA_TP_TIMING
     const unsigned long long clkB = clock64();
     clk_t += clkB - clkA;

@@ -88,6 +88,10 @@ uint64_t real_tp_min_population();
 bool real_tp_batchable(const GenArgs& a, uint32_t n);
 uint32_t real_max_batch();
 uint32_t real_launch_batch(const GenArgs* args, unsigned long long* const* parts, uint32_t n, hipStream_t s);
+// PERMUTATION batched islands (perm.hip perm_gen_fast_batch): TSP objectives,
+// genomes of at most 512 cities
+uint32_t perm_max_batch();
+uint32_t perm_launch_batch(const GenArgs* args, unsigned long long* const* parts, uint32_t n, hipStream_t s);
 // batched islands (binary_batch.hip): one MODE_GEN launch of up to
 // binary_max_batch() same-shape islands (args[i], best partials parts[i]);
 // returns each island's grid (its best-partials count), 0 when the islands do

@@ -259,6 +259,10 @@ __device__ __forceinline__ void real_gen_tp_body(GenArgs a, unsigned long long* 
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");  // the parents before the flag
       tp_flag_set(&lds_ready[sg]);
     }
+    // several blocks per CU (the 4-wave grid): a barrier parks the waiting
+    // waves (a flag spin would take issue slots from the other blocks' waves:
+    // REAL at S = 100K, 36 -> 55 us/gen); one block per CU: the flags alone
+    if (NW < kTpMaxWaves) __syncthreads();
 
     // RESOLVE: parents, crossover plan, mutation positions and draws of the
     // round's unit BI -> the records of ring slot SL

@@ -314,7 +314,7 @@ __device__ __forceinline__ uint4 set16(uint4 v, uint32_t e, uint32_t x) {
 // one table per CU), 2 = the full matrix.  Entries are exact (u16 -> f32),
 // so the tour sums equal the f32-matrix kernel's bit for bit.
 template <int GS, int OBJ, int TBL = 0>
-__global__ __launch_bounds__(1024) void perm_gen_fast(GenArgs a, unsigned long long* best_parts) {
+__device__ __forceinline__ void perm_gen_fast_body(GenArgs a, unsigned long long* best_parts) {
   resolve_gen(a);
   float* smem = (float*)pga_dyn_lds;
   unsigned long long* lds_red = (unsigned long long*)smem;  // 16 entries: kHdrF holds them
@@ -513,6 +513,26 @@ __global__ __launch_bounds__(1024) void perm_gen_fast(GenArgs a, unsigned long l
   }
 }
 
+template <int GS, int OBJ, int TBL = 0>
+__global__ __launch_bounds__(1024) void perm_gen_fast(GenArgs a, unsigned long long* best_parts) {
+  perm_gen_fast_body<GS, OBJ, TBL>(a, best_parts);
+}
+
+// Batched islands: up to kPermMaxBatch same-shape islands in ONE launch,
+// island = blockIdx.y (the binary / real batched kernels' scheme; the tour
+// evaluation from each island's f32 matrix or coordinates).  Reference: at
+// most MAX_POPULATIONS = 10 islands per solver (include/pga.h:44), run one
+// after another (src/pga.cu:272-276).
+constexpr uint32_t kPermMaxBatch = 10;
+struct PermBatch {
+  GenArgs a[kPermMaxBatch];
+  unsigned long long* parts[kPermMaxBatch];
+};
+template <int GS, int OBJ>
+__global__ __launch_bounds__(1024) void perm_gen_fast_batch(PermBatch b) {
+  perm_gen_fast_body<GS, OBJ, 0>(b.a[blockIdx.y], b.parts[blockIdx.y]);
+}
+
 // Genomes beyond kPermMaxL genes: one 64-lane block per individual, so the
 // four per-child LDS arrays (8 L bytes, +8 L of EUC coordinates) fit in
 // 160 KiB up to ~20 000 cities (u16 ids cap L at 65 535 anyway)
@@ -580,7 +600,10 @@ uint32_t go_fast(const GenArgs& a, unsigned long long* parts, hipStream_t s) {
   if constexpr (OBJ == OBJ_TSP || OBJ == OBJ_TSP_OPEN) {
     // an integer matrix as u16 in LDS: the largest block (up to 16 waves,
     // one table per CU) whose group arrays fit beside it
-    if (a.obj_aux && (a.obj_aux_kind == 1 || a.obj_aux_kind == 2) && a.obj_aux_bytes % 16 == 0) {
+    // (OX / no crossover: TSP-256 OX 3,265 -> 4,013 gens/s; PMX's chain
+    // walks want the 256-thread occupancy more: 2,793 vs 2,650, L2 path kept)
+    if (a.obj_aux && (a.obj_aux_kind == 1 || a.obj_aux_kind == 2) && a.obj_aux_bytes % 16 == 0 &&
+        a.crossover != XO_PMX) {
       const size_t avail = 160 * 1024 - 1024;  // less the static LDS (block reductions)
       for (uint32_t blk : {1024u, 512u, 256u}) {
         if (perm_lds_bytes(GS, a.chunks, false, blk) + a.obj_aux_bytes > avail) continue;
@@ -615,7 +638,63 @@ uint32_t launch_obj(int mode, const GenArgs& a, unsigned long long* parts, hipSt
   }
 }
 
+template <int GS, int OBJ>
+uint32_t batch_go(PermBatch& b, uint32_t n, hipStream_t s) {
+  const GenArgs& a0 = b.a[0];
+  const size_t lds = perm_lds_bytes(GS, a0.chunks, OBJ == OBJ_TSP_EUC);
+  const void* k = (const void*)perm_gen_fast_batch<GS, OBJ>;
+  static bool configured = false;
+  if (!configured) {
+    allow_dynamic_lds(k);
+    configured = true;
+  }
+  const uint32_t gpb = kBlock / GS;
+  const uint64_t need = (a0.S + gpb - 1) / gpb;
+  uint64_t cap = (uint64_t)device_cu_count() * occupancy_blocks(k, kBlock, lds) / n;  // the device split
+  if (cap < 1) cap = 1;
+  if (cap > kMaxGrid) cap = kMaxGrid;
+  const uint32_t gx = (uint32_t)(need < cap ? need : cap);
+  hipLaunchKernelGGL((perm_gen_fast_batch<GS, OBJ>), dim3(gx, n), kBlock, lds, s, b);
+  PGA_HIP_CHECK(hipGetLastError());
+  return gx;
+}
+
+template <int GS>
+uint32_t batch_obj(PermBatch& b, uint32_t n, hipStream_t s) {
+  switch (b.a[0].objective) {
+    case OBJ_TSP: return batch_go<GS, OBJ_TSP>(b, n, s);
+    case OBJ_TSP_OPEN: return batch_go<GS, OBJ_TSP_OPEN>(b, n, s);
+    case OBJ_TSP_EUC: return batch_go<GS, OBJ_TSP_EUC>(b, n, s);
+    default: return 0;
+  }
+}
+
 }  // namespace
+
+uint32_t perm_max_batch() { return kPermMaxBatch; }
+
+uint32_t perm_launch_batch(const GenArgs* args, unsigned long long* const* parts, uint32_t n, hipStream_t s) {
+  if (n == 0 || n > kPermMaxBatch || force_generic_kernels()) return 0;
+  const GenArgs& a0 = args[0];
+  if (a0.objective != OBJ_TSP && a0.objective != OBJ_TSP_OPEN && a0.objective != OBJ_TSP_EUC) return 0;
+  if (a0.chunks > 64u || a0.L > 65535) return 0;  // the fast kernel: one chunk per lane
+  PermBatch b;
+  for (uint32_t i = 0; i < n; ++i) {
+    const GenArgs& a = args[i];
+    if (a.S != a0.S || a.L != a0.L || a.chunks != a0.chunks || a.objective != a0.objective) return 0;
+    b.a[i] = a;
+    b.parts[i] = parts[i];
+  }
+  switch (group_size(a0.chunks)) {
+    case 1: return batch_obj<1>(b, n, s);
+    case 2: return batch_obj<2>(b, n, s);
+    case 4: return batch_obj<4>(b, n, s);
+    case 8: return batch_obj<8>(b, n, s);
+    case 16: return batch_obj<16>(b, n, s);
+    case 32: return batch_obj<32>(b, n, s);
+    default: return batch_obj<64>(b, n, s);
+  }
+}
 
 uint32_t perm_launch(int mode, const GenArgs& a, unsigned long long* best_parts, hipStream_t s) {
   if (a.L > 65535) throw std::invalid_argument("PERMUTATION encoding supports at most 65535 genes (u16 city ids)");

@@ -213,9 +213,11 @@ def test_jit_real_fused_equals_separate_pass(S, monkeypatch):
 def test_jit_variant_key_distinguishes_lengths():
     # 5000 and 5001 bits share a group size of 64 lanes: one JitKernel (same
     # source) used at both lengths must compile two variants
+    src = ONEMAX_SRC + "// variant-key test\n"  # its own kernel: another test's failed fusion is cached per kernel
     for L in (5000, 5001):
         a = pga.GeneticAlgorithm(M.OneMax(L), 4096, seed=3, device="cuda:0", elitism=1)
-        b = pga.GeneticAlgorithm(onemax_jit(L), 4096, seed=3, device="cuda:0", elitism=1)
+        b = pga.GeneticAlgorithm(M.JitObjective("binary", L, src, name="ones"), 4096, seed=3, device="cuda:0",
+                                 elitism=1)
         a.run(3)
         b.run(3)
         torch.cuda.synchronize()

@@ -96,6 +96,24 @@ def test_local_islands_real_batched_matches_streams_gpu(prob, kw):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("prob,xo", [("matrix", "ox"), ("euc", "pmx"), ("open", "ox")])
+def test_local_islands_perm_batched_matches_streams_gpu(prob, xo):
+    # TSP islands in ONE launch per generation (perm_gen_fast_batch)
+    p = {"matrix": lambda: pga.models.TSP.random_euclidean(100, seed=3),
+         "euc": lambda: pga.models.TSPEuclidean.random(64, seed=4),
+         "open": lambda: pga.models.TSP.reference_e3(100, seed=2)}[prob]
+    common = dict(seed=7, device="cuda:0", migrate_every=4, migrate_pct=0.02, elitism=1, crossover=xo)
+    a = LocalIslands(p(), 6, 2048, **common)
+    b = LocalIslands(p(), 6, 2048, batched=False, **common)
+    a.run(9)
+    b.run(9)
+    torch.cuda.synchronize()
+    assert a.batched_generations == 9 and b.batched_generations == 0
+    for x, y in zip(a.islands, b.islands):
+        assert torch.equal(x.rows, y.rows) and torch.equal(x.scores, y.scores)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("prob", ["small", "rotated"])
 def test_local_islands_batched_falls_back_gpu(prob):
     # a REAL batch below the two-phase kernel's population, or a rotated
