@@ -467,6 +467,7 @@ void Island::prepare_generation() {
 
 void Island::run(uint32_t n) {
   TraceRange tr("pga.run");
+  if (run_tiny(n)) return;
   if (on_gpu() && graph_g_ > 0 && !graph_broken_ && !hist_on_ && n >= graph_g_ + 2) {
     const bool fresh = gexec_ && g_cur_ == cur_ && g_epoch_ == epoch_ && g_version_ == version_ &&
                        g_nbest_ == n_best_[cur_] && g_len_ == graph_g_;
@@ -480,6 +481,28 @@ void Island::run(uint32_t n) {
     if (run_graph(reps, fresh)) n -= reps * graph_g_;
   }
   run_plain(n);
+}
+
+bool Island::run_tiny(uint32_t n) {
+  // REAL populations that fit one block: all n generations in one launch
+  // (real_launch_multi); nothing to prepare between generations, so the
+  // launch is exactly n run_plain generations
+  if (!on_gpu() || n < 2 || cfg_.encoding != ENC_REAL || jit_ || hist_on_ || capturing_ || real_qk()) return false;
+  if (cfg_.n_elite > 1 || (cfg_.selection != SEL_TOURNAMENT && cfg_.selection != SEL_RANDOM)) return false;
+  GenArgs a = make_args(MODE_GEN);
+  const int nx = cur_ ^ 1;
+  unsigned long long* const parts[2] = {(unsigned long long*)best_[nx].ptr, (unsigned long long*)best_[cur_].ptr};
+  float* const st[2] = {a.stats_parts, a.stats_parts ? (float*)stats_parts_[cur_].ptr : nullptr};
+  if (!real_launch_multi(a, parts, st, n, stream)) return false;
+  TraceRange tg("pga.generations_tiny", 2);
+  // the kernel keeps the population in LDS between generations: only the
+  // last generation's buffers (the new current parity) are written
+  for (uint32_t i = 0; i < n; ++i) swap();
+  n_best_[cur_] = n_best_[cur_ ^ 1] = 1;
+  stats_ok_[cur_] = a.stats_parts != nullptr;
+  stats_ok_[cur_ ^ 1] = false;
+  qk_valid_[0] = qk_valid_[1] = false;
+  return true;
 }
 
 void Island::run_plain(uint32_t n) {

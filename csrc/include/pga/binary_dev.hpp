@@ -16,10 +16,10 @@
 // The user objective of a fused JIT generation kernel (jitgen.hip): defined in
 // the user's bitcode, LTO-linked with the kernel's bitcode and inlined
 // (jit.cpp).  Never referenced by the built-in kernels.
-// The row pointer is a global (address space 1) pointer: the child's row as
-// the kernel just stored it.
-typedef __attribute__((address_space(1))) const unsigned int* pga_global_words;
-extern "C" __device__ float pga_user_objective(pga_global_words words, unsigned int nbits, const float* data);
+// The row pointer is an LDS (address space 3) pointer: the child's row as the
+// step just staged it next to its global store (see kJitStageSteps).
+typedef __attribute__((address_space(3))) const unsigned int* pga_lds_words;
+extern "C" __device__ float pga_user_objective(pga_lds_words words, unsigned int nbits, const float* data);
 
 namespace pga {
 // jitgen.hip instantiates the generation kernel with external linkage (a named
@@ -454,9 +454,13 @@ __device__ __forceinline__ void binary_gen_tp_body(GenArgs a, unsigned long long
   constexpr bool KMF = OBJ == kObjKnapMfma;
   __shared__ uint4 lds_kscr[KMF ? kTpMaxWaves : 1][kKnapScratch];      // knapsack: per-wave chunk / C scratch
   __shared__ uint4 lds_ktab[KMF ? kKnapSlices * 4 * kKnapMaxCols : 1];  // knapsack: digit table
-  // JIT (a linked user objective): the steps only store the children; after
-  // each batch's last step every lane evaluates one child of the batch from
-  // the rows just stored (8 KB per wave, still in the L2)
+  // JIT (a linked user objective): each step also stages its children's rows
+  // in the wave's LDS slice (64 lanes x 16 B), and every kJitStageSteps steps
+  // one lane per staged child runs the objective on its LDS row.  Reading the
+  // rows back from global memory instead (round 3/4: once per unit) has to
+  // wait for every load issued before it -- the parent rows in flight PD steps
+  // ahead -- since vector memory counters retire in order: a drained pipeline
+  // per unit (110.8 vs 89.8 us/gen); LDS reads wait on their own counter.
   constexpr bool JIT = OBJ == kObjJit;
 
   const uint32_t lane = lane_id(), wid = threadIdx.x >> 6;
@@ -490,6 +494,9 @@ __device__ __forceinline__ void binary_gen_tp_body(GenArgs a, unsigned long long
   uint32_t bbegin, bend;
   tp_block_range(S, U, bbegin, bend, a.tp_skew);
   const uint32_t pcap = tp_par_cap(NW);
+  // JIT staging after the parents: kJitStageSteps KB per wave (jit.cpp adds it to the launch's LDS)
+  uint4* lds_stage = (uint4*)(pga_dyn_lds + NW * 4096u + pcap * 8u) + wid * (kJitStageSteps * 64u);
+  (void)lds_stage;
   // the pair pool (tp.hpp): one round, tournament or random selection; the
   // block's own units end at own_end, the last P units are the pair's
   const uint32_t P = a.tp_pool_units;
@@ -868,6 +875,10 @@ __device__ __forceinline__ void binary_gen_tp_body(GenArgs a, unsigned long long
       sc = acc.template finish<GS>(a);                                                                      \
     }                                                                                                       \
     if (have) ROW(nxt, c, q) = v;                                                                           \
+    if constexpr (JIT) {                                                                                    \
+      lds_stage[(i % kJitStageSteps) * 64u + lane] = v;                                                     \
+      if (i % kJitStageSteps == kJitStageSteps - 1u || i + 1u == nst) PGA_TP_JIT_EVAL                       \
+    }                                                                                                       \
     if (EVALS && !JIT) { /* every lane of the group stores the same score */                                \
       ELEM(float, a.score_next, c) = sc;                                                                    \
       if (KEY) ELEM(uint16_t, a.key_next, c) = (uint16_t)sc;                                                \
@@ -876,7 +887,6 @@ __device__ __forceinline__ void binary_gen_tp_body(GenArgs a, unsigned long long
       st.add_if(q == 0u && c < S, sc);                                                                      \
     }                                                                                                       \
     if (++i == nst) {                                                                                       \
-      if constexpr (JIT) PGA_TP_JIT_EVAL                                                                    \
       PGA_TP_COUNT                                                                                          \
       if (lbs == bs) { /* the load cursor never left this unit: it was the wave's last */                   \
         done = true;                                                                                        \
@@ -889,19 +899,24 @@ __device__ __forceinline__ void binary_gen_tp_body(GenArgs a, unsigned long long
     }                                                                                                       \
   }
 
-      // JIT: this wave's stores of the unit's rows complete before its lanes
-      // read them back (no other CU wrote them, so no stale L1 line can exist)
+      // JIT: the staged steps s0..i of the unit, child j = lane (step s0 + j / NG,
+      // group j % NG); the wavefront fences keep the compiler from moving LDS
+      // accesses across (one wave's LDS operations execute in order)
 #define PGA_TP_JIT_EVAL                                                                                     \
   {                                                                                                         \
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");                                                  \
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");                                                  \
-    const uint32_t cj = bs + lane;                                                                          \
-    if (cj < be) {                                                                                          \
-      const float sj = pga_user_objective((pga_global_words)((const char*)nxt + cj * rb), L, a.obj_data);   \
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");                                                  \
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");                                                  \
+    const uint32_t s0 = i - i % kJitStageSteps, ns = i - s0 + 1u;                                           \
+    const uint32_t cj = bs + s0 * NG + lane;                                                                \
+    if (lane < ns * NG && cj < be) {                                                                        \
+      const uint32_t js = lane / NG, jg = lane % NG;                                                        \
+      const float sj = pga_user_objective((pga_lds_words)(lds_stage + js * 64u + jg * GS), L, a.obj_data);  \
       ELEM(float, a.score_next, cj) = sj;                                                                   \
       my_best = pack_best(sj, cj) > my_best ? pack_best(sj, cj) : my_best;                                  \
       st.add(sj);                                                                                           \
     }                                                                                                       \
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");                                                  \
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");                                                  \
   }
 #ifdef PGA_TP_TIMING
 #define PGA_TP_COUNT n_bred += be - bs;

@@ -251,6 +251,7 @@ class Island {
 
   // graph replay state
   void run_plain(uint32_t n);
+  bool run_tiny(uint32_t n);
   bool run_graph(uint32_t reps, bool fresh);
   bool capture_graph();
   void drop_graph();

@@ -53,6 +53,8 @@ TpGeom tp_geometry(uint64_t S, uint32_t islands, const void* kernel, uint32_t ng
 // the same from the resident 4-wave blocks per CU (occ4; module kernels)
 TpGeom tp_geometry_occ(uint64_t S, uint32_t islands, uint32_t occ4, uint32_t ng, uint32_t pseg = 7);
 uint32_t tp_dyn_lds_bytes(uint32_t nw, uint32_t pseg = 7);
+// LDS a fused BINARY JIT launch adds for its staged children (tp.hpp kJitStageSteps)
+uint32_t tp_jit_stage_bytes(uint32_t nw);
 // units per block in binary_gen_tp's pair pool for this geometry (tp.hpp;
 // PGA_TP_POOL=d: 1/d of a 16-wave block's units; default 0: off)
 uint32_t tp_pool_units(const TpGeom& t, uint64_t S);
@@ -105,6 +107,13 @@ uint32_t binary_launch_batch(const GenArgs* args, unsigned long long* const* par
 bool build_knap_table(const float* values, const float* weights, uint32_t L, uint32_t chunks,
                       std::vector<uint8_t>& tab, uint32_t& digits, uint32_t& cols);
 uint32_t real_launch(int mode, const GenArgs& a, unsigned long long* best_parts, hipStream_t s);
+// REAL tiny populations (every child in one block): n >= 2 MODE_GEN
+// generations in one launch (real.hip real_multi_kernel); parts / stats of
+// the even and odd generations; false (nothing launched) when `a` does not
+// qualify (per-generation host work: rank / roulette / top-k elites, user
+// operators, rotation, quantized keys; PGA_TINY_MULTI=0 turns it off)
+bool real_launch_multi(const GenArgs& a, unsigned long long* const parts[2], float* const stats[2], uint32_t n,
+                       hipStream_t s);
 uint32_t perm_launch(int mode, const GenArgs& a, unsigned long long* best_parts, hipStream_t s);
 
 // reference-ABI path: thread-per-individual kernel calling user device

@@ -220,8 +220,12 @@ PGA_HD void real_cross_chunk(const GenArgs& a, uint64_t child, uint32_t c, const
       for (int j = 0; j < 4; ++j) v[j] = fsel((ubits >> j) & 1u, A[j], B[j]);
       break;
     case XO_BLEND: {  // BLX-alpha: u in [-alpha, 1 + alpha] per gene, seeded by cut (real_cut_word)
+      // one 32-bit hash per gene pair, 16 bits of u each (the hash was a
+      // third of the Rastrigin-30D breed step's VALU)
+      const uint32_t h0 = mut_skip_word(cut, 2 * c), h1 = mut_skip_word(cut, 2 * c + 1);
+      const uint32_t hw[4] = {h0 << 16, h0 & 0xFFFF0000u, h1 << 16, h1 & 0xFFFF0000u};
       for (int j = 0; j < 4; ++j) {
-        const float u = fmaf(1.f + 2.f * a.blend_alpha, word_to_unit(mut_skip_word(cut, 4 * c + j)), -a.blend_alpha);
+        const float u = fmaf(1.f + 2.f * a.blend_alpha, word_to_unit(hw[j]), -a.blend_alpha);
         v[j] = clampf(fmaf(u, B[j] - A[j], A[j]), a.lo, a.hi);
       }
       break;

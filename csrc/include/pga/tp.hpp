@@ -181,6 +181,11 @@ __host__ __device__ constexpr uint32_t tp_dyn_lds(uint32_t nw, uint32_t pseg = 7
   return nw * 4096u + tp_par_cap(nw, pseg) * 8u;
 }
 static_assert(tp_par_cap(4) % (kSegBatches * 64) == 0, "rounds hold whole segments");
+// fused BINARY JIT kernels (binary_dev.hpp): steps of children staged in LDS
+// per objective pass, 1 KB per wave per step after the parents (16 waves:
+// 120 + 32 KB of dynamic LDS); tp_jit_stage_lds is what the launch adds
+constexpr uint32_t kJitStageSteps = 2;
+__host__ __device__ constexpr uint32_t tp_jit_stage_lds(uint32_t nw) { return nw * kJitStageSteps * 1024u; }
 constexpr uint32_t kTpMaxSegs = tp_par_cap(kTpMaxWaves) / (kSegBatches * 64);  // tournament segments per round
 
 // Breed prefetch depth: parent rows are loaded PD steps ahead (<= 3; a unit

@@ -73,7 +73,7 @@ __host__ __device__ inline size_t real_lds_floats(uint32_t GS, uint32_t chunks, 
 // register allocation on every instantiation that can reach it).
 // ---------------------------------------------------------------------------
 template <int GS, int MODE, bool ROT, bool UFN>
-__global__ __launch_bounds__(kBlock) void real_kernel(GenArgs a, unsigned long long* best_parts) {
+__device__ __forceinline__ void real_generic_body(GenArgs& a, unsigned long long* best_parts) {
   resolve_gen(a);
   float* smem = (float*)pga_dyn_lds;
   uint32_t* lds_thr = (uint32_t*)smem;
@@ -263,6 +263,95 @@ __global__ __launch_bounds__(kBlock) void real_kernel(GenArgs a, unsigned long l
     unsigned long long b = block_max_u64(my_best, lds_red);
     if (threadIdx.x == 0) best_parts[blockIdx.x] = b;
     if (a.stats_parts) block_stats_store(st, a.stats_parts);
+  }
+}
+
+template <int GS, int MODE, bool ROT, bool UFN>
+__global__ __launch_bounds__(kBlock) void real_kernel(GenArgs a, unsigned long long* best_parts) {
+  real_generic_body<GS, MODE, ROT, UFN>(a, best_parts);
+}
+
+// ---------------------------------------------------------------------------
+// Tiny populations (every child in one block, e.g. the reference's E2 at
+// S = 100): n generations in ONE launch with the population resident in LDS.
+// As one launch per generation, 100 children cost a chain of dependent global
+// round trips (best partial -> scores -> parent rows -> stores drained) plus
+// the launch: 7.1 us/gen on hipGraph replay; one launch re-reading global
+// memory each generation still 4.6 us.  Here generation 0 reads the global
+// population and writes LDS, the middle ones run LDS -> LDS (rows, scores,
+// best partial: no global access but the mutation table's first copy), the
+// last writes the global buffers of its parity, its best partial and stats.
+// Each generation is the generic kernel's generation gen + g, bit for bit.
+// Three call sites of the generic body, so each sees its pointers' address
+// space (global or LDS) after inlining.
+// ---------------------------------------------------------------------------
+struct RealMulti {
+  void* rows_out;                 // the last generation's children (its parity's buffers)
+  float* scores_out;
+  uint16_t* keys_out;
+  unsigned long long* parts_out;  // its best partial
+  float* stats_out;               // its stats partials (or null)
+  uint32_t n;                     // generations (>= 2)
+  uint32_t lds_off;               // floats: the population region after the body's LDS
+};
+
+// LDS floats of the resident population: 2 best partials, 2 x S rows, 2 x S scores
+__host__ __device__ inline uint32_t real_multi_floats(uint32_t S, uint32_t row_words) {
+  return 4u + 2u * S * row_words + 2u * S;
+}
+
+template <int GS, bool UFN>
+__global__ __launch_bounds__(kBlock) void real_multi_kernel(GenArgs a, RealMulti m) {
+  const uint32_t S = (uint32_t)a.S, rf = a.row_words;
+  float* pop = (float*)pga_dyn_lds + m.lds_off;
+  unsigned long long* bl = (unsigned long long*)pop;
+  float* rows0 = pop + 4;
+  float* rows1 = rows0 + S * rf;
+  float* sc0 = rows1 + S * rf;
+  float* sc1 = sc0 + S;
+  const uint32_t* thr = (const uint32_t*)pga_dyn_lds;  // the body's copy of the mutation table
+  {  // generation 0: global -> LDS buffer 0
+    GenArgs b = a;
+    b.next = rows0;
+    b.score_next = sc0;
+    b.key_next = nullptr;
+    b.stats_parts = nullptr;
+    real_generic_body<GS, MODE_GEN, false, UFN>(b, &bl[0]);
+    __syncthreads();
+  }
+  for (uint32_t g = 1; g + 1 < m.n; ++g) {  // LDS -> LDS
+    GenArgs b = a;
+    const bool odd = g & 1u;
+    b.cur = odd ? rows0 : rows1;
+    b.next = odd ? rows1 : rows0;
+    b.score_cur = odd ? sc0 : sc1;
+    b.score_next = odd ? sc1 : sc0;
+    b.best_cur = odd ? &bl[0] : &bl[1];
+    b.n_best_cur = 1;
+    b.mut_thr = thr;
+    b.key_cur = nullptr;
+    b.key_next = nullptr;
+    b.stats_parts = nullptr;
+    b.key.gen = a.key.gen + g;
+    real_generic_body<GS, MODE_GEN, false, UFN>(b, odd ? &bl[1] : &bl[0]);
+    __syncthreads();
+  }
+  {  // the last generation: LDS -> the global buffers of its parity
+    const uint32_t g = m.n - 1;
+    const bool odd = g & 1u;
+    GenArgs b = a;
+    b.cur = odd ? rows0 : rows1;
+    b.score_cur = odd ? sc0 : sc1;
+    b.best_cur = odd ? &bl[0] : &bl[1];
+    b.n_best_cur = 1;
+    b.mut_thr = thr;
+    b.key_cur = nullptr;
+    b.next = m.rows_out;
+    b.score_next = m.scores_out;
+    b.key_next = m.keys_out;
+    b.stats_parts = m.stats_out;
+    b.key.gen = a.key.gen + g;
+    real_generic_body<GS, MODE_GEN, false, UFN>(b, m.parts_out);
   }
 }
 
@@ -601,6 +690,53 @@ uint32_t real_launch(int mode, const GenArgs& a, unsigned long long* best_parts,
   }
   PGA_HIP_CHECK(hipGetLastError());
   return grid;
+}
+
+namespace {
+template <int GS>
+void go_multi(const GenArgs& a, const RealMulti& m, hipStream_t s) {
+  const size_t lds = ((size_t)m.lds_off + real_multi_floats((uint32_t)a.S, a.row_words)) * sizeof(float);
+  if (a.objective == OBJ_USER_FNPTR) hipLaunchKernelGGL((real_multi_kernel<GS, true>), 1, kBlock, lds, s, a, m);
+  else hipLaunchKernelGGL((real_multi_kernel<GS, false>), 1, kBlock, lds, s, a, m);
+}
+}  // namespace
+
+bool real_launch_multi(const GenArgs& a, unsigned long long* const parts[2], float* const stats[2], uint32_t n,
+                       hipStream_t s) {
+  static const bool on = [] {
+    const char* e = std::getenv("PGA_TINY_MULTI");
+    return !(e && e[0] == '0');
+  }();
+  if (!on || n < 2 || a.chunks == 0 || a.chunks > 64 || force_generic_kernels()) return false;
+  const uint32_t gs = group_size(a.chunks);
+  if (a.S == 0 || a.S > kBlock / gs) return false;  // one block holds every child
+  if (a.objective == OBJ_NONE || ((a.obj_i & 2) && real_obj_rotatable(a.objective))) return false;
+  if (a.selection != SEL_TOURNAMENT && a.selection != SEL_RANDOM) return false;
+  if (a.n_elite > 1 || a.elite_idx || a.qk || a.gen_dev) return false;
+  if (a.user_xo_fn || a.user_mut_fn) return false;  // the compat operators draw a host-filled buffer
+  if (!parts[0] || !parts[1]) return false;
+  RealMulti m;
+  // per-generation parity: generation g writes buffer set (cur + g + 1) & 1,
+  // so the last one (n - 1) writes `next` for odd n and `cur` for even n
+  const bool odd = n & 1u;
+  m.rows_out = odd ? a.next : const_cast<void*>(a.cur);
+  m.scores_out = odd ? a.score_next : const_cast<float*>(a.score_cur);
+  m.keys_out = odd ? a.key_next : const_cast<uint16_t*>(a.key_cur);
+  m.parts_out = parts[odd ? 0 : 1];
+  m.stats_out = stats[odd ? 0 : 1];
+  m.n = n;
+  m.lds_off = (uint32_t)((real_lds_floats(gs, a.chunks, false) + 3) & ~(size_t)3);
+  switch (gs) {
+    case 1: go_multi<1>(a, m, s); break;
+    case 2: go_multi<2>(a, m, s); break;
+    case 4: go_multi<4>(a, m, s); break;
+    case 8: go_multi<8>(a, m, s); break;
+    case 16: go_multi<16>(a, m, s); break;
+    case 32: go_multi<32>(a, m, s); break;
+    default: go_multi<64>(a, m, s); break;
+  }
+  PGA_HIP_CHECK(hipGetLastError());
+  return true;
 }
 
 }  // namespace pga

@@ -85,6 +85,7 @@ TpGeom tp_geometry(uint64_t S, uint32_t islands, const void* kernel, uint32_t ng
 }
 
 uint32_t tp_dyn_lds_bytes(uint32_t nw, uint32_t pseg) { return dev::tp_dyn_lds(nw, pseg); }
+uint32_t tp_jit_stage_bytes(uint32_t nw) { return dev::tp_jit_stage_lds(nw); }
 
 uint32_t tp_skew_units(const TpGeom& t, uint64_t S) {
   // PGA_TP_SKEW = units each odd block of a pair hands to its even
@@ -127,7 +128,11 @@ TpGeom tp_geometry_occ(uint64_t S, uint32_t islands, uint32_t occ4, uint32_t ng,
   if (cap > kMaxGrid) cap = kMaxGrid;
   const uint64_t per_wave = (S + 4 * cap - 1) / (4 * cap);
   uint32_t u = ng * dev::tp_prefetch_depth(64 / ng);  // a unit holds >= PD steps
-  while (u < 64 && u < per_wave) u *= 2;
+  static const uint32_t umax = [] {  // PGA_TP_UMAX: largest unit of this grid (sweeps)
+    const char* e = std::getenv("PGA_TP_UMAX");
+    return e ? (uint32_t)std::strtoul(e, nullptr, 10) : 64u;
+  }();
+  while (u < 64 && u < per_wave && 2 * u <= umax) u *= 2;
   const uint64_t need = (S + 4ull * u - 1) / (4ull * u);
   const uint64_t g = need < cap ? need : cap;
   return {(uint32_t)(g == 0 ? 1 : g), 256u, dev::tp_dyn_lds(4, pseg), u};

@@ -298,3 +298,35 @@ def test_gpu_small_population_generic_route_bitexact(monkeypatch):
     monkeypatch.delenv("PGA_TP_MIN_S", raising=False)
     _exact_pair(M.Sphere(30), 3000, 3, seed=31, elitism=1, crossover="blend", mutation="gaussian")
     _exact_pair(M.SumGenes(100), 3000, 2, seed=32, crossover="uniform", mutation="reset_one")
+
+
+# tiny populations (every child in one block): GA.run(n) is ONE launch of n
+# generations (real.hip real_multi_kernel); rows and scores equal the CPU
+# backend's after each multi-generation run
+TINY = {
+    "knap100": (lambda: M.ReferenceKnapsack(), 100),  # reference E2, GS 2
+    "sphere3": (lambda: M.Sphere(3), 256),            # GS 1, the block's 256 groups
+    "sum30": (lambda: M.SumGenes(30), 32),            # GS 8
+    "rosen30": (lambda: M.Rosenbrock(30), 17),        # neighbour gene across lanes
+    "sphere100": (lambda: M.Sphere(100), 8),          # GS 32
+    "sphere256": (lambda: M.Sphere(256), 4),          # GS 64
+}
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", list(TINY))
+@pytest.mark.parametrize("kw", [dict(elitism=1), dict(elitism=0, tournament_k=3, mutation="reset_one"),
+                                dict(elitism=1, selection="random", crossover="blend")])
+def test_gpu_tiny_multi_generation_bitexact(name, kw, monkeypatch):
+    monkeypatch.delenv("PGA_TP_MIN_S", raising=False)  # tiny populations: no quantized keys
+    mk, S = TINY[name]
+    p = mk()
+    g = pga.GeneticAlgorithm(p, S, seed=5, device="cuda:0", **kw)
+    c = pga.GeneticAlgorithm(p, S, seed=5, device="cpu", **kw)
+    for n in (2, 7, 3):
+        g.run(n)
+        c.run(n)
+        torch.cuda.synchronize()
+        assert torch.equal(g.rows.cpu(), c.rows), f"rows differ after run({n})"
+        assert torch.equal(g.scores.cpu(), c.scores), f"scores differ after run({n})"
+    assert g.best_score() == c.best_score() and g.best_index() == c.best_index()
