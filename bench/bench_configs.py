@@ -16,6 +16,7 @@ Configs (BASELINE.md "Targets" table):
   e2_knap_refops    reference example E2 (S=100, L=6), launch-bound (hipGraph)
   onemax64_gpu      OneMax 64-bit, pop=1024 on the GPU (launch-bound)
   onemax1024_jit    the headline island with a hipRTC-compiled objective
+  rastrigin30_jit   Rastrigin-30D written as HIP source, fused into the REAL kernel
   knapsack1024      0/1 knapsack, 1024 items, pop=1M (matrix-core evaluation)
 The 8-GPU island configs are bench.py under torchrun (the driver runs those).
 Each line: gens/s, evals/s, ms/gen, best fitness, effective HBM GB/s (the
@@ -55,6 +56,13 @@ def make(name: str):
         src = """__device__ float ones(const unsigned int* w, unsigned int n, const float* d) {
             float s = 0.f; for (unsigned i = 0; i < (n + 31) / 32; ++i) s += __popc(w[i]); return s; }"""
         return M.JitObjective("binary", 1024, src, name="ones"), 1 << 20, None, dict(elitism=1), 300
+    if name == "rastrigin30_jit":
+        # the rastrigin30 config with the objective as user source (fused, LDS rows)
+        src = """__device__ float rast(const float* x, unsigned int n, const float* d) {
+            float s = 10.f * n;
+            for (unsigned int i = 0; i < n; ++i) s += x[i] * x[i] - 10.f * __cosf(6.28318530718f * x[i]);
+            return -s; }"""
+        return M.JitObjective("real", 30, src, name="rast", bounds=(-5.12, 5.12)), 1 << 20, None, dict(elitism=1), 200
     if name == "e2_knap_refops":
         # reference example E2 (S=100, L=6): launch-bound, the hipGraph replay case
         return M.ReferenceKnapsack(), 100, None, {}, 5000
@@ -98,7 +106,7 @@ def make(name: str):
 
 NAMES = ["onemax64_cpu", "onemax1024", "rastrigin30", "rastrigin30_rot", "tsp256_ox", "tsp256_pmx", "tsp256_int_ox",
          "tsp256_int_pmx", "e1_sum100_refops",
-         "tsp256_euc_ox", "tsp256_euc_pmx", "e2_knap_refops", "onemax64_gpu", "onemax1024_jit", "maxcut512_qubo",
+         "tsp256_euc_ox", "tsp256_euc_pmx", "e2_knap_refops", "onemax64_gpu", "onemax1024_jit", "rastrigin30_jit", "maxcut512_qubo",
          "qubo1024", "onemax1024_rank", "knapsack1024", "onemax1024_roulette_2pt"]
 
 

@@ -336,14 +336,13 @@ std::string JitKernel::build_gen_object(uint32_t gs, bool full, bool dense, uint
   const char* rp = std::getenv("ROCM_PATH");
   const std::string rocm = rp && *rp ? rp : "/opt/rocm";
   // the user's source + the external-linkage entry the kernel bitcode calls:
-  // the row arrives as an address-space pointer (LDS for BINARY, whose kernel
-  // stages each step's children there; global for REAL) -- ds / global
-  // loads, not flat -- and the genome length as a constant, so fixed-trip loops over the row unroll with
+  // the row arrives as an LDS pointer (the kernel stages each step's children
+  // there: ds loads, not flat) and the genome length as a constant, so fixed-trip loops over the row unroll with
   // every load in flight (the length is part of the cache key)
   const std::string T = real ? "float" : "unsigned int";
   const std::string src = "#include <hip/hip_runtime.h>\n#line 1 \"user_objective\"\n" + user_source + "\n" +
                           "extern \"C\" __device__ float " + (real ? "pga_user_objective_f32" : "pga_user_objective") +
-                          "(__attribute__((address_space(" + (real ? "1" : "3") + "))) const " + T +
+                          "(__attribute__((address_space(3))) const " + T +
                           "* w, unsigned int, const float* d) { return " +
                           name + "((const " + T + "*)w, " + std::to_string(L) + "u, d); }\n";
   // the user's compile options (-D, -I, ...) apply to the fused objective as
@@ -408,7 +407,7 @@ hipFunction_t JitKernel::gen_function(int device, uint32_t gs, bool full, bool d
     return nullptr;
   }
   int occ = 0;  // resident 4-wave blocks per CU (tp_geometry_occ)
-  const uint32_t lds4 = tp_dyn_lds_bytes(4) + (encoding == ENC_BINARY ? tp_jit_stage_bytes(4) : 0u);
+  const uint32_t lds4 = tp_dyn_lds_bytes(4) + tp_jit_stage_bytes(4);
   if (hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&occ, v.fn, 256, lds4) != hipSuccess ||
       occ <= 0)
     occ = 1;
@@ -439,8 +438,8 @@ uint32_t JitKernel::gen_launch(hipFunction_t f, const void* args, size_t args_by
   size_t total = off + sizeof(parts);
   void* cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, buf.data(), HIP_LAUNCH_PARAM_BUFFER_SIZE, &total,
                  HIP_LAUNCH_PARAM_END};
-  // BINARY kernels stage each step's children in LDS for the objective
-  const uint32_t lds = t.lds + (a.encoding == ENC_BINARY ? tp_jit_stage_bytes(t.block / 64) : 0u);
+  // the kernels stage each step's children in LDS for the objective
+  const uint32_t lds = t.lds + tp_jit_stage_bytes(t.block / 64);
   PGA_HIP_CHECK(hipModuleLaunchKernel(f, grid, 1, 1, t.block, 1, 1, lds, s, nullptr, cfg));
   return grid;
 }

@@ -12,10 +12,10 @@
 
 // The user objective of a fused JIT generation kernel (jitgen_real.hip):
 // defined in the user's bitcode, LTO-linked with the kernel's bitcode and
-// inlined (jit.cpp).  The genes are the child's row as the kernel just stored
-// it (a global pointer).
-typedef __attribute__((address_space(1))) const float* pga_global_floats;
-extern "C" __device__ float pga_user_objective_f32(pga_global_floats genes, unsigned int n, const float* data);
+// inlined (jit.cpp).  The genes are the child's row as the step staged it in
+// LDS next to its global store (binary_dev.hpp: the same staging, and why).
+typedef __attribute__((address_space(3))) const float* pga_lds_floats;
+extern "C" __device__ float pga_user_objective_f32(pga_lds_floats genes, unsigned int n, const float* data);
 
 namespace pga {
 // jitgen_real.hip instantiates the kernel with external linkage (a named
@@ -159,9 +159,10 @@ __device__ __forceinline__ void real_gen_tp_body(GenArgs a, unsigned long long* 
   constexpr uint32_t PD = tp_prefetch_depth(GS);  // steps of parent rows in flight (tp.hpp)
   constexpr uint32_t PSEG = ROT ? 6 : 7;  // tp_par_cap segments: the rotation tiles take static LDS
   constexpr bool EVALS = OBJ != OBJ_NONE;
-  // JIT (a linked user objective, jitgen_real.hip): the steps only store the
-  // children; after a unit's last step every lane evaluates one child of the
-  // unit from the row just stored (L2), and tournaments read the f32 scores
+  // JIT (a linked user objective, jitgen_real.hip): the steps also stage
+  // their children in the wave's LDS slice; every kJitStageSteps steps one
+  // lane per staged child runs the objective on its LDS row (binary_dev.hpp);
+  // tournaments read the f32 scores
   constexpr bool JIT = OBJ == kObjJit;
   constexpr bool BUILTIN = EVALS && !JIT;
   // dynamic LDS: per wave 2 units x 64 records x 32 B, then the round's parents
@@ -213,6 +214,9 @@ __device__ __forceinline__ void real_gen_tp_body(GenArgs a, unsigned long long* 
   uint32_t bbegin, bend;              // this block's children
   tp_block_range(S, U, bbegin, bend, a.tp_skew);
   const uint32_t pcap = tp_par_cap(NW, PSEG);
+  // JIT staging after the parents: kJitStageSteps KB per wave (jit.cpp adds it to the launch's LDS)
+  float4* lds_stage = (float4*)(pga_dyn_lds + NW * 4096u + pcap * 8u) + wid * (kJitStageSteps * 64u);
+  (void)lds_stage;
 
   float* xw = lds_rot + (ROT ? wid * 16 * kRotTW : 0);          // this wave's X/Z tile
   float* ms = lds_rot + (ROT ? kTpMaxWaves * 16 * kRotTW : 0);  // M[n][k], block-shared
@@ -390,6 +394,10 @@ __device__ __forceinline__ void real_gen_tp_body(GenArgs a, unsigned long long* 
     }                                                                                                       \
     _Pragma("unroll") for (uint32_t j = 0; j < 4; ++j) v[j] = j < clen ? v[j] : 0.f;                        \
     if (have) RROW(nxt, c, q) = make_float4(v[0], v[1], v[2], v[3]);                                        \
+    if constexpr (JIT) {                                                                                    \
+      lds_stage[(i % kJitStageSteps) * 64u + lane] = make_float4(v[0], v[1], v[2], v[3]);                   \
+      if (i % kJitStageSteps == kJitStageSteps - 1u || i + 1u == nst) PGA_RTP_JIT_EVAL                      \
+    }                                                                                                       \
     if constexpr (BUILTIN) {                                                                                \
       float z[4], zn[4];                                                                                    \
       _Pragma("unroll") for (uint32_t j = 0; j < 4; ++j) z[j] = 4 * q + j < L ? v[j] - sh[j] : 0.f;         \
@@ -413,7 +421,6 @@ __device__ __forceinline__ void real_gen_tp_body(GenArgs a, unsigned long long* 
       st.add_if(q == 0u && c < S, sc);                                                                      \
     }                                                                                                       \
     if (++i == nst) {                                                                                       \
-      if constexpr (JIT) PGA_RTP_JIT_EVAL                                                                   \
       if (lbs == bs) { /* the load cursor never left this unit: it was the wave's last */                   \
         done = true;                                                                                        \
       } else {                                                                                              \
@@ -425,19 +432,23 @@ __device__ __forceinline__ void real_gen_tp_body(GenArgs a, unsigned long long* 
     }                                                                                                       \
   }
 
-      // JIT: this wave's stores of the unit's rows complete before its lanes
-      // read them back (no other CU wrote them, so no stale L1 line can exist)
+      // JIT: the staged steps s0..i of the unit (binary_dev.hpp PGA_TP_JIT_EVAL)
 #define PGA_RTP_JIT_EVAL                                                                                    \
   {                                                                                                         \
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");                                                  \
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");                                                  \
-    const uint32_t cj = bs + lane;                                                                          \
-    if (lane < U && cj < rend) {                                                                            \
-      const float sj = pga_user_objective_f32((pga_global_floats)((const char*)nxt + cj * rb), L, a.obj_data); \
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");                                                  \
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");                                                  \
+    const uint32_t s0 = i - i % kJitStageSteps, ns = i - s0 + 1u;                                           \
+    const uint32_t cj = bs + s0 * NG + lane;                                                                \
+    const uint32_t ue = bs + U < rend ? bs + U : rend;                                                      \
+    if (lane < ns * NG && cj < ue) {                                                                        \
+      const uint32_t js = lane / NG, jg = lane % NG;                                                        \
+      const float sj = pga_user_objective_f32((pga_lds_floats)(lds_stage + js * 64u + jg * GS), L, a.obj_data); \
       RELEM(float, a.score_next, cj) = sj;                                                                  \
       my_best = pack_best(sj, cj) > my_best ? pack_best(sj, cj) : my_best;                                  \
       st.add(sj);                                                                                           \
     }                                                                                                       \
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");                                                  \
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");                                                  \
   }
 
       float4 A0, B0, A1, B1, A2, B2, A3, B3;  // PD + 1 register sets, rotated statically
