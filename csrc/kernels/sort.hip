@@ -217,6 +217,7 @@ template <int SRC, int VAL, uint32_t MAXD>  // VAL: 0 = the key's index, 1 = src
 __global__ __launch_bounds__(kBlock) void radix_scatter_kernel(KeySrc src, const uint32_t* __restrict__ vin, uint64_t n,
                                                                uint32_t shift, uint32_t bits, uint32_t D, uint64_t tiles,
                                                                const uint32_t* __restrict__ base,
+                                                               const uint32_t* __restrict__ csums, uint32_t nchunks,
                                                                uint32_t* __restrict__ kout, uint32_t* __restrict__ vout) {
   __shared__ uint32_t cnt[kBlock / 64][MAXD];  // per wave: running digit counts, then output bases
   const uint32_t mask = (1u << bits) - 1u;
@@ -288,7 +289,13 @@ __global__ __launch_bounds__(kBlock) void radix_scatter_kernel(KeySrc src, const
     if (d < D) {
 #pragma unroll
       for (uint32_t w = 0; w < kBlock / 64; ++w) cnt[w][d] += ls;  // local start of (wave w, digit d)
-      gofs[d] = base[(uint64_t)d * tiles + blockIdx.x] - ls;       // output index = gofs[d] + local index
+      // base: exclusive scan WITHIN its scan chunk; csums: the chunk totals
+      // (scan_chunks), whose prefix this adds (nchunks <= kScanFold)
+      const uint64_t e = (uint64_t)d * tiles + blockIdx.x;
+      uint32_t pre = 0;
+      const uint32_t ce = csums ? (uint32_t)(e / kScanChunk) : 0u;
+      for (uint32_t c = 0; c < ce && c < nchunks; ++c) pre += csums[c];
+      gofs[d] = base[e] + pre - ls;  // output index = gofs[d] + local index
     }
     ls += tcs[j];
   }
@@ -312,6 +319,15 @@ __global__ __launch_bounds__(kBlock) void radix_scatter_kernel(KeySrc src, const
   }
 }
 
+// The scatter's bases with at most kScanFold scan chunks: ONE launch scans
+// each chunk in place and stores the chunk totals; the scatter adds the
+// prefix of the totals itself (<= kScanFold L2 loads per digit) instead of two
+// more launches (scan of the totals, add back: ~4.8 + 5.0 us for the rank
+// order of 1M u16 keys, profiles/rank_kernel_stats_r03.csv).  Returns the
+// chunk count (0: x is fully scanned, nothing to fold).
+constexpr uint32_t kScanFold = 64;
+uint32_t scan_chunks(uint32_t* x, uint64_t m, const RadixWs& w, hipStream_t s);
+
 // exclusive scan of m entries in place (m <= kScanChunk^3)
 void scan_exclusive(uint32_t* x, uint64_t m, const RadixWs& w, hipStream_t s) {
   const uint64_t chunks = (m + kScanChunk - 1) / kScanChunk;
@@ -331,6 +347,16 @@ void scan_exclusive(uint32_t* x, uint64_t m, const RadixWs& w, hipStream_t s) {
                        w.sums2);
   }
   hipLaunchKernelGGL(scan_add_kernel, (uint32_t)((m + kBlock - 1) / kBlock), kBlock, 0, s, x, m, w.sums);
+}
+
+uint32_t scan_chunks(uint32_t* x, uint64_t m, const RadixWs& w, hipStream_t s) {
+  const uint64_t chunks = (m + kScanChunk - 1) / kScanChunk;
+  if (chunks <= 1 || chunks > kScanFold) {
+    scan_exclusive(x, m, w, s);
+    return 0;
+  }
+  hipLaunchKernelGGL(scan_chunk_kernel, (uint32_t)chunks, kScanBlock, 0, s, x, m, w.sums);
+  return (uint32_t)chunks;
 }
 
 // one sort: per pass count -> scan -> scatter.  The passes ping-pong between
@@ -362,17 +388,17 @@ void radix_run(const KeySrc& src0, uint64_t n, uint32_t bits, uint32_t* kout, ui
     const uint32_t D = wide ? key_range : (1u << pb);
     const dim3 g((uint32_t)tiles);
 #define PGA_COUNT(K, MD) hipLaunchKernelGGL((radix_count_kernel<K, MD>), g, kBlock, 0, s, src, n, shift, pb, D, tiles, w.counts)
-#define PGA_SCATTER(K, V, MD) hipLaunchKernelGGL((radix_scatter_kernel<K, V, MD>), g, kBlock, 0, s, src, cv, n, shift, pb, D, tiles, w.counts, dk, dv)
+#define PGA_SCATTER(K, V, MD) hipLaunchKernelGGL((radix_scatter_kernel<K, V, MD>), g, kBlock, 0, s, src, cv, n, shift, pb, D, tiles, w.counts, nch ? w.sums : nullptr, nch, dk, dv)
     if (wide) {  // one pass over u16 keys (rank order of an integer objective)
       if (kind != SRC_U16 || vk != 0) throw std::logic_error("radix sort: single-pass mode is for u16 keys");
       PGA_COUNT(SRC_U16, kWideDigits);
-      scan_exclusive(w.counts, (uint64_t)D * tiles, w, s);
+      const uint32_t nch = scan_chunks(w.counts, (uint64_t)D * tiles, w, s);
       PGA_SCATTER(SRC_U16, 0, kWideDigits);
     } else {
       if (kind == SRC_U32) PGA_COUNT(SRC_U32, kMaxDigits);
       if (kind == SRC_U16) PGA_COUNT(SRC_U16, kMaxDigits);
       if (kind == SRC_F32) PGA_COUNT(SRC_F32, kMaxDigits);
-      scan_exclusive(w.counts, (uint64_t)D * tiles, w, s);
+      const uint32_t nch = scan_chunks(w.counts, (uint64_t)D * tiles, w, s);
       if (vk == 2) PGA_SCATTER(SRC_U32, 2, kMaxDigits);
       else if (kind == SRC_U32) { if (vk) PGA_SCATTER(SRC_U32, 1, kMaxDigits); else PGA_SCATTER(SRC_U32, 0, kMaxDigits); }
       else if (kind == SRC_U16) { if (vk) PGA_SCATTER(SRC_U16, 1, kMaxDigits); else PGA_SCATTER(SRC_U16, 0, kMaxDigits); }
