@@ -232,6 +232,19 @@ __global__ __launch_bounds__(kBlock) void radix_scatter_kernel(KeySrc src, const
     key[r] = load_key<SRC>(src, ec);
     val[r] = VAL == 2 ? vin[ec] : (VAL == 1 ? src.vals[ec] : (uint32_t)e);
   }
+  // exclusive prefix of the scan-chunk totals (nchunks <= kScanFold = 64):
+  // one wave's scan into LDS, read per digit below
+  __shared__ uint32_t cpre[64];
+  if (csums && wid == 0) {
+    const uint32_t c = lane < nchunks ? csums[lane] : 0u;
+    uint32_t incl = c;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t y = (uint32_t)__shfl_up((int)incl, o, 64);
+      if (lane >= (uint32_t)o) incl += y;
+    }
+    cpre[lane] = incl - c;
+  }
   const uint64_t below = (1ull << lane) - 1ull;
   uint32_t pos[kRounds];
 #pragma unroll
@@ -289,12 +302,10 @@ __global__ __launch_bounds__(kBlock) void radix_scatter_kernel(KeySrc src, const
     if (d < D) {
 #pragma unroll
       for (uint32_t w = 0; w < kBlock / 64; ++w) cnt[w][d] += ls;  // local start of (wave w, digit d)
-      // base: exclusive scan WITHIN its scan chunk; csums: the chunk totals
-      // (scan_chunks), whose prefix this adds (nchunks <= kScanFold)
+      // base: exclusive scan WITHIN its scan chunk; cpre: the prefix of the
+      // chunk totals (scan_chunks)
       const uint64_t e = (uint64_t)d * tiles + blockIdx.x;
-      uint32_t pre = 0;
-      const uint32_t ce = csums ? (uint32_t)(e / kScanChunk) : 0u;
-      for (uint32_t c = 0; c < ce && c < nchunks; ++c) pre += csums[c];
+      const uint32_t pre = csums ? cpre[e / kScanChunk] : 0u;
       gofs[d] = base[e] + pre - ls;  // output index = gofs[d] + local index
     }
     ls += tcs[j];
@@ -321,7 +332,7 @@ __global__ __launch_bounds__(kBlock) void radix_scatter_kernel(KeySrc src, const
 
 // The scatter's bases with at most kScanFold scan chunks: ONE launch scans
 // each chunk in place and stores the chunk totals; the scatter adds the
-// prefix of the totals itself (<= kScanFold L2 loads per digit) instead of two
+// prefix of the totals itself (one wave scan into LDS) instead of two
 // more launches (scan of the totals, add back: ~4.8 + 5.0 us for the rank
 // order of 1M u16 keys, profiles/rank_kernel_stats_r03.csv).  Returns the
 // chunk count (0: x is fully scanned, nothing to fold).
