@@ -34,6 +34,7 @@ int main(int argc, char** argv) {
     else if (k == "--warmup") warm = std::atoi(v.c_str());
     else if (k == "--elitism") c.n_elite = (uint32_t)std::atoi(v.c_str());
     else if (k == "--objective") c.objective = std::atoi(v.c_str());
+    else if (k == "--mutation") c.mutation = v == "reset_one" ? pga::MUT_RESET_ONE : pga::MUT_GAUSSIAN;
     else if (k == "--xo")
       c.crossover = v == "one" ? pga::XO_ONE_POINT
                     : v == "two" ? pga::XO_TWO_POINT
@@ -52,6 +53,14 @@ int main(int argc, char** argv) {
       }
       if (c.encoding == pga::ENC_PERMUTATION) { c.mutation = pga::MUT_SWAP; c.crossover = pga::XO_OX; }
     }
+  }
+  for (int i = 1; i + 1 < argc; i += 2) {  // options that override the encoding's defaults
+    std::string k = argv[i], v = argv[i + 1];
+    if (k == "--objective") c.objective = std::atoi(v.c_str());
+    else if (k == "--mutation") c.mutation = v == "reset_one" ? pga::MUT_RESET_ONE : pga::MUT_GAUSSIAN;
+    else if (k == "--xo") c.crossover = v == "uniform" ? pga::XO_UNIFORM : c.crossover;
+    else if (k == "--lo") c.lo = std::strtof(v.c_str(), nullptr);
+    else if (k == "--hi") c.hi = std::strtof(v.c_str(), nullptr);
   }
   pga::Island isl(c, 0);
   isl.initialize();

@@ -149,6 +149,13 @@ __device__ __forceinline__ void rot_tile4(float* xw, const float* ms, float z[4]
   rot_tile4_sync();
 }
 
+// experiment builds only (tools/variants.sh "p0:-DPGA_RTP_PROBE=0" ...): the
+// kernel returns after its prologue (0), after the first round's tournaments
+// (1) or skips the epilogue (2), to split the fixed per-generation cost
+#ifndef PGA_RTP_PROBE
+#define PGA_RTP_PROBE 9
+#endif
+
 template <int GS, int OBJ, bool ROT>
 __device__ __forceinline__ void real_gen_tp_body(GenArgs a, unsigned long long* best_parts) {
   static_assert(!ROT || GS == 4 || GS == 8, "wave-local rotation: 16 or 32 padded dims");
@@ -243,6 +250,7 @@ __device__ __forceinline__ void real_gen_tp_body(GenArgs a, unsigned long long* 
   ScoreStats st;
   uint4(*rec)[64][2] = lds_rec[wid];
   static_assert(sizeof(lds_rec[0]) >= kSegBatches * 64 * sizeof(uint4), "contestant staging");
+  if constexpr (PGA_RTP_PROBE == 0) return;
   for (uint32_t rbeg = bbegin; rbeg < bend; rbeg += pcap) {  // block-uniform rounds
     const uint32_t rend = rbeg + pcap < bend ? rbeg + pcap : bend;
     const uint32_t nb = (rend - rbeg + U - 1) / U;                                  // the round's units
@@ -267,6 +275,7 @@ __device__ __forceinline__ void real_gen_tp_body(GenArgs a, unsigned long long* 
     // waves (a flag spin would take issue slots from the other blocks' waves:
     // REAL at S = 100K, 36 -> 55 us/gen); one block per CU: the flags alone
     if (NW < kTpMaxWaves) __syncthreads();
+    if constexpr (PGA_RTP_PROBE == 1) return;
 
     // RESOLVE: parents, crossover plan, mutation positions and draws of the
     // round's unit BI -> the records of ring slot SL
@@ -498,7 +507,7 @@ __device__ __forceinline__ void real_gen_tp_body(GenArgs a, unsigned long long* 
   }
 #undef RROW
 #undef RELEM
-  if (EVALS && best_parts) {  // block-uniform
+  if (EVALS && best_parts && PGA_RTP_PROBE != 2) {  // block-uniform
     unsigned long long bb = block_max_u64_n(my_best, lds_red, NW);
     if (threadIdx.x == 0) best_parts[blockIdx.x] = bb;
     if (a.stats_parts) block_stats_store_n(st, a.stats_parts, NW);

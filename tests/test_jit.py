@@ -68,11 +68,15 @@ def test_jit_cpu_uses_fallback():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("L,kw", [(1024, {}), (777, {}), (1024, dict(mutation_rate=0.02)), (300, dict(selection="rank"))])
-def test_jit_onemax_bit_identical_to_builtin(L, kw):
+@pytest.mark.parametrize("L,kw,S", [(1024, {}, 1 << 16), (777, {}, 1 << 16), (1024, dict(mutation_rate=0.02), 1 << 16),
+                                    (300, dict(selection="rank"), 1 << 16),
+                                    # LDS staging: one step per objective pass (GS 1), 32-lane rows
+                                    (32, {}, 1 << 16), (4096, {}, 1 << 14),
+                                    # the headline geometry (16-wave blocks, XCD skew), a partial last unit
+                                    (1024, {}, 1 << 20), (1024, {}, 100003)])
+def test_jit_onemax_bit_identical_to_builtin(L, kw, S):
     # the objective is linked into the hot generation kernel (one launch per
     # generation): rows, scores and best equal the built-in OneMax bit for bit
-    S = 1 << 16
     a = pga.GeneticAlgorithm(M.OneMax(L), S, seed=4, device="cuda:0", elitism=1, **kw)
     b = pga.GeneticAlgorithm(onemax_jit(L), S, seed=4, device="cuda:0", elitism=1, **kw)
     assert b.island.has_jit
