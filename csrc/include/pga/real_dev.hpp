@@ -194,6 +194,7 @@ __device__ __forceinline__ void real_gen_tp_body(GenArgs a, unsigned long long* 
   const bool xo_on = a.crossover != XO_NONE;
   const bool uniform_xo = a.crossover == XO_UNIFORM;
   const bool u_word0 = uniform_xo && L <= 32u;  // the record carries every chunk's mask bits
+  const bool uwords = uniform_xo && !u_word0 && L <= 128u;  // the record can carry the child's crossover block
   const bool per_gene = real_per_gene_mutation(a);
   const bool dense = per_gene && !a.mut_sparse;
   const bool sparse = per_gene && a.mut_sparse;
@@ -330,8 +331,20 @@ __device__ __forceinline__ void real_gen_tp_body(GenArgs a, unsigned long long* 
       if (kk > 1u) d1 = f2u(real_mut_draw<true>(a, cc, 1));                                                  \
       if (kk > 2u) d2 = f2u(real_mut_draw<true>(a, cc, 2));                                                  \
     }                                                                                                        \
-    const uint32_t meta =                                                                                    \
-        (K > 255u ? 255u : K) | ((jn > 0xFFFFu ? 0xFFFFu : jn) << 8) | (xo ? 1u << 30 : 0u) | (elite ? 1u << 31 : 0u); \
+    /* UNIFORM crossover, 33..128 genes, no mutation (the usual child of the                                 \
+       reference operators): the child's crossover block rides in the unused                                \
+       second record word, one Philox per child here instead of one per lane                                 \
+       per step (meta bit 29) */                                                                             \
+    const bool xw = uwords && xo && K == 0u;                                                                 \
+    if (xw) {                                                                                                \
+      const u32x4 xb = draw<true>(a.key, ST_XO, cc, 0);                                                      \
+      posw = xb.x;                                                                                           \
+      d0 = xb.y;                                                                                             \
+      d1 = xb.z;                                                                                             \
+      d2 = xb.w;                                                                                             \
+    }                                                                                                        \
+    const uint32_t meta = (K > 255u ? 255u : K) | ((jn > 0xFFFFu ? 0xFFFFu : jn) << 8) | (xw ? 1u << 29 : 0u) | \
+                          (xo ? 1u << 30 : 0u) | (elite ? 1u << 31 : 0u);                                    \
     uint4(*r)[2] = rec[(SL)];                                                                                \
     r[lane][0] = make_uint4(pa, pb, cut, meta);                                                              \
     r[lane][1] = make_uint4(posw, d0, d1, d2);                                                               \
@@ -378,16 +391,21 @@ __device__ __forceinline__ void real_gen_tp_body(GenArgs a, unsigned long long* 
     const uint32_t c = bs + i * NG + g;                                                                     \
     const uint4 r0 = rec[slot][i * NG + g][0];                                                              \
     const uint32_t meta = r0.w;                                                                             \
+    const uint4 r1 = rec[slot][i * NG + g][1];                                                              \
     const float A_[4] = {XA.x, XA.y, XA.z, XA.w}, B_[4] = {XB.x, XB.y, XB.z, XB.w};                         \
     float v[4];                                                                                             \
     {                                                                                                       \
       uint32_t ub = 0;                                                                                      \
-      if (uniform_xo) ub = u_word0 ? (r0.z >> ((4u * q) & 31u)) & 0xFu : real_uniform_bits<true>(a.key, c, q); \
+      if (uniform_xo) {                                                                                     \
+        if (u_word0) ub = (r0.z >> ((4u * q) & 31u)) & 0xFu;                                                \
+        else if ((meta >> 29) & 1u) /* real_uniform_bits from the record's block */                         \
+          ub = (sel4(u32x4{r1.x, r1.y, r1.z, r1.w}, (q >> 3) & 3u) >> ((4u * q) & 31u)) & 0xFu;              \
+        else ub = real_uniform_bits<true>(a.key, c, q);                                                     \
+      }                                                                                                     \
       real_cross_chunk<true>(a, c, q, A_, B_, (meta >> 30) & 1u, r0.z, ub, v);                             \
     }                                                                                                       \
     const uint32_t K = meta & 0xFFu;                                                                        \
     if (K > 0u) { /* group-uniform */                                                                       \
-      const uint4 r1 = rec[slot][i * NG + g][1];                                                            \
       uint32_t mm = 0;                                                                                      \
       _Pragma("unroll") for (uint32_t k = 0; k < 3; ++k) {                                                  \
         const uint32_t p = (r1.x >> (8u * k)) & 0xFFu;                                                      \

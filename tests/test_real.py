@@ -168,6 +168,17 @@ def test_gpu_tp_bitexact_operators(xo, mut):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("L", [33, 100, 128])
+@pytest.mark.parametrize("mut", ["reset_one", "gaussian"])
+def test_gpu_tp_uniform_crossover_block_in_record(L, mut):
+    """UNIFORM crossover on 33..128 genes: a child without mutations carries
+    its crossover block in the record (one Philox per child), a mutated one
+    draws it per lane; both bit for bit vs the CPU backend (reference E1's
+    operators at L = 100)."""
+    _exact_pair(M.SumGenes(L), 3000, 3, seed=8, elitism=1, crossover="uniform", mutation=mut)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("name", list(EXACT))
 def test_gpu_tp_bitexact_geometries(name):
     p = EXACT[name]()
