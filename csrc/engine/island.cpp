@@ -428,10 +428,12 @@ void Island::prepare_generation() {
     // The quantization range only has to be the same for every key of a
     // generation: keys are monotonic in the score and equal keys fall back to
     // the exact f32 compare, so any range gives the same tournaments.  It is
-    // refreshed every kQkRefresh generations (a stale range only costs more
+    // refreshed every few generations (a stale range only costs more
     // ties), not every generation: small populations are launch-bound.
-    constexpr uint32_t kQkRefresh = 8;
-    if (qk_age_++ % kQkRefresh == 0) {
+    // Every 8 generations (32 below 2^18 children, where the ~5 us refresh
+    // launch is a larger share of a short generation: reference E1).
+    const uint32_t refresh = cfg_.S * batch_n_ < (1ull << 18) ? 32u : 8u;
+    if (qk_age_++ % refresh == 0) {
       if (stats_ok_[cur_])
         stats_from_parts_launch((const float*)stats_parts_[cur_].ptr, (const unsigned long long*)best_[cur_].ptr,
                                 n_best_[cur_], cfg_.S, (float*)qk_ws_.ptr, stream);
