@@ -43,8 +43,22 @@ def main():
         epoch()
     torch.cuda.synchronize()
     res = {}
+    def epoch_gen():  # IslandModel's order: emigrate, one generation, re-score, immigrate
+        isl.emigrate(k, rows, sc)
+        isl.run(1)
+        isl.evaluate_rows(rows, sc)
+        isl.immigrate(k, rows, sc)
+
+    def with_fused(on, fn):
+        def f():
+            isl.fused_histogram = on
+            fn()
+        return f
+
     for name, fn in (("topk_sorted", lambda: isl.topk(k, True)), ("topk", lambda: isl.topk(k, True, False)),
-                     ("epoch", epoch), ("generation", lambda: isl.run(1))):
+                     ("epoch", epoch), ("generation", lambda: isl.run(1)),
+                     ("epoch_gen_nofused", with_fused(False, epoch_gen)), ("epoch_gen_fused", with_fused(True, epoch_gen)),
+                     ("generation_fused", with_fused(True, lambda: isl.run(1)))):
         a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         n = 50
         a.record()
@@ -53,6 +67,11 @@ def main():
         b.record()
         b.synchronize()
         res[name + "_us"] = a.elapsed_time(b) / n * 1e3
+        isl.fused_histogram = False
+    # the epoch's device work beyond the generation it overlaps (what the
+    # island model adds every migrate_every generations)
+    res["epoch_device_nofused_us"] = res["epoch_gen_nofused_us"] - res["generation_us"]
+    res["epoch_device_fused_us"] = res["epoch_gen_fused_us"] - res["generation_fused_us"]
     res.update(pop=S, k=k)
     emit(res)
 
@@ -111,12 +130,18 @@ def rccl_self_overhead(S=1 << 20, every=10, gens=500):
     torch.cuda.set_device(0)
     dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
     out = {}
-    arms = (("none", 0, True, True), ("rccl_self", every, True, True), ("rccl_self_noside", every, False, True),
-            ("rccl_self_serial", every, False, False))
-    for name, ev, side, overlap in arms:
+    # (name, every, side stream, overlap, fused histogram, transport)
+    arms = (("none", 0, False, True, False, "torch"), ("rccl_self", every, False, True, True, "engine"),
+            ("rccl_self_torch", every, False, True, True, "torch"),
+            ("rccl_self_torch_side", every, True, True, True, "torch"),
+            ("rccl_self_serial", every, False, False, True, "engine"),
+            ("rccl_self_nofused", every, False, True, False, "engine"))
+    for name, ev, side, overlap, fused, transport in arms:
         ga = pga.GeneticAlgorithm(pga.models.OneMax(1024), S, seed=1, device="cuda:0", elitism=1)
-        m = IslandModel(ga, migrate_every=ev, migrate_pct=0.01, side_stream=side, overlap=overlap)
+        m = IslandModel(ga, migrate_every=ev, migrate_pct=0.01, side_stream=side, overlap=overlap,
+                        transport=transport)
         m.world, m.rank = 2, 0
+        ga.island.fused_histogram = fused  # what IslandModel sets for world > 1 (constructed here at world 1)
         m._peers = lambda: (0, 0)
         m.connect() if ev else None
         m.run(50)
@@ -129,7 +154,7 @@ def rccl_self_overhead(S=1 << 20, every=10, gens=500):
         b.synchronize()
         out["us_per_gen_" + name] = a.elapsed_time(b) / gens * 1e3
         out["migrations_" + name] = m.migrations
-    for v in ("rccl_self", "rccl_self_noside", "rccl_self_serial"):
+    for v in ("rccl_self", "rccl_self_torch", "rccl_self_torch_side", "rccl_self_serial", "rccl_self_nofused"):
         out["overhead_pct_" + v] = 100.0 * (out["us_per_gen_" + v] / out["us_per_gen_none"] - 1.0)
     out.update(pop=S, every=every)
     emit(out)

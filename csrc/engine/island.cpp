@@ -74,7 +74,8 @@ Island::~Island() {
   Buffer* all[] = {&rows_[0],   &rows_[1],     &scores_[0],   &scores_[1],  &best_[0],  &best_[1],   &mut_thr_,
                    &obj_data_[0], &obj_data_[1], &keys_[0], &keys_[1], &elite_idx_, &cumfit_, &cum_ws_, &roul_guide_, &topk_ws_, &stats_,
                    &out_best_,  &scratch_, &compat_rand_, &ev_parts_, &gen_dev_, &rank_order_, &rank_ws_, &qubo_qt_,
-                   &knap_tab_, &stats_parts_[0], &stats_parts_[1], &hist_, &qk_ws_, &tp_pool_, &obj_aux_};
+                   &knap_tab_, &stats_parts_[0], &stats_parts_[1], &hist_, &qk_ws_, &tp_pool_, &obj_aux_,
+                   &fhist_[0], &fhist_[1], &fhist_[2]};
   drop_graph();
   if (cap_stream_) (void)hipStreamDestroy(cap_stream_);
   for (Buffer* b : all) {
@@ -169,6 +170,7 @@ void Island::set_operators(const Config& c) {
   const int32_t old_mut = cfg_.mutation;
   cfg_ = c;
   if (!mut_thr_.ptr || old_rate != c.mut_rate || old_mut != c.mutation) rebuild_mut_table();
+  fhist_on_ = fhist_user_ || cfg_.n_elite > 1;  // elitism > 1 selects top-k every generation
   if (cfg_.n_elite > 1 && elite_idx_.bytes < 4ull * cfg_.n_elite) {
     release(elite_idx_);
     elite_idx_ = alloc(4ull * cfg_.n_elite);
@@ -177,7 +179,7 @@ void Island::set_operators(const Config& c) {
     cumfit_ = alloc(4ull * cfg_.S);
     if (on_gpu()) {
       cum_ws_ = alloc(4ull * roulette_workspace_floats(cfg_.S));
-      roul_guide_ = alloc(4ull * (cfg_.S + 1));
+      roul_guide_ = alloc(4ull * roulette_guide_words(cfg_.S));
     }
   }
   if (cfg_.selection == SEL_RANK && !rank_order_.ptr) {
@@ -365,6 +367,7 @@ GenArgs Island::make_args(int mode) {
 }
 
 uint32_t Island::launch(int mode, const GenArgs& a, unsigned long long* parts) {
+  if (mode != MODE_GEN && a.cur == rows_[cur_].ptr) fhist_of_[0] = fhist_of_[1] = -1;  // staged / init / eval
   if (on_gpu()) return encoding_launch(mode, a, parts, stream);
   return cpu::encoding_run(mode, a, parts);
 }
@@ -412,7 +415,8 @@ void Island::rebest() {
 bool Island::real_qk() const {
   // quantized tournament keys feed only the two-phase kernel (real_gen_tp),
   // which small populations do not take: there they would cost a launch
-  return on_gpu() && cfg_.encoding == ENC_REAL && cfg_.objective != OBJ_NONE && !jit_ &&
+  return on_gpu() && cfg_.encoding == ENC_REAL && cfg_.objective != OBJ_NONE && cfg_.objective != OBJ_USER_FNPTR &&
+         !jit_ &&
          cfg_.S * batch_n_ >= real_tp_min_population();
 }
 
@@ -480,6 +484,7 @@ void Island::run(uint32_t n) {
       n -= 2;
     }
     const uint32_t reps = n / graph_g_;
+    fhist_of_[0] = fhist_of_[1] = -1;  // replays do not produce the fused histograms
     if (run_graph(reps, fresh)) n -= reps * graph_g_;
   }
   run_plain(n);
@@ -500,7 +505,10 @@ bool Island::run_tiny(uint32_t n) {
   // the kernel keeps the population in LDS between generations: only the
   // last generation's buffers (the new current parity) are written
   for (uint32_t i = 0; i < n; ++i) swap();
-  n_best_[cur_] = n_best_[cur_ ^ 1] = 1;
+  // the previous parity's rows / scores / partials were never written (its
+  // generations lived in LDS): no valid partials there until a kernel writes them
+  n_best_[cur_] = 1;
+  n_best_[cur_ ^ 1] = 0;
   stats_ok_[cur_] = a.stats_parts != nullptr;
   stats_ok_[cur_ ^ 1] = false;
   qk_valid_[0] = qk_valid_[1] = false;
@@ -517,8 +525,25 @@ void Island::run_plain(uint32_t n) {
       if (hist_on_ && !hist_manual_ && !capturing_) append_history();
       continue;
     }
+    const bool fh = fhist_ready_for(a);
+    if (fh) {  // this generation also writes the value histogram of its keys (GenArgs::key_hist)
+      a.key_hist = (uint32_t*)fhist_[fhist_rot_ % 3].ptr;
+      a.hist_zero = (uint32_t*)fhist_[(fhist_rot_ + 1) % 3].ptr;
+      a.hist_bins = cfg_.L + 1;
+      a.hist_zero_words = fused_hist_words(cfg_.L + 1);
+    }
     n_best_[cur_ ^ 1] = launch(MODE_GEN, a, (unsigned long long*)best_[cur_ ^ 1].ptr);
     stats_ok_[cur_ ^ 1] = a.stats_parts != nullptr;
+    if (fh) {
+      const int w = (int)(fhist_rot_ % 3), z = (int)((fhist_rot_ + 1) % 3);
+      ++fhist_rot_;
+      fhist_of_[cur_ ^ 1] = w;
+      fhist_clean_[w] = true;   // zeroed (bins and status) by the launch before this one
+      fhist_clean_[z] = true;   // zeroed by this launch
+      if (fhist_of_[cur_] == z) fhist_of_[cur_] = -1;
+    } else {
+      fhist_of_[cur_ ^ 1] = -1;
+    }
     qk_valid_[cur_ ^ 1] = a.qk != nullptr && !jit_;  // every REAL GEN kernel writes the keys it is given
     if (jit_) {
       n_best_[cur_ ^ 1] = jit_eval(rows_[cur_ ^ 1].ptr, (float*)scores_[cur_ ^ 1].ptr, cfg_.S,
@@ -605,6 +630,7 @@ bool Island::run_batched(const std::vector<Island*>& isls, uint32_t n, hipStream
       I.n_best_[nx] = grid;
       I.stats_ok_[nx] = args[k].stats_parts != nullptr;
       I.qk_valid_[nx] = real && args[k].qk != nullptr;  // the REAL kernel writes the keys it is given
+      I.fhist_of_[nx] = -1;  // the batched launch produces no fused histogram
       I.swap();
     }
   }
@@ -730,7 +756,9 @@ void Island::topk(uint32_t k, bool largest, uint32_t* idx_out, bool sorted) {
   if (on_gpu()) {
     ensure_topk_ws(k);
     const uint16_t* k16 = integer_objective(cfg_.objective, cfg_.L) ? (const uint16_t*)keys_[cur_].ptr : nullptr;
-    topk_launch(sc, k16, cfg_.L + 1, cfg_.S, k, largest, sorted, idx_out, topk_ws_.ptr, stream);
+    TopkFused f;
+    topk_launch(sc, k16, cfg_.L + 1, cfg_.S, k, largest, sorted, idx_out, topk_ws_.ptr, stream, nullptr,
+                sorted || !k16 ? nullptr : fused_select(f));
   } else {
     cpu::topk(sc, cfg_.S, k, largest, idx_out, sorted);
   }
@@ -802,8 +830,9 @@ void Island::emigrate(uint32_t k, void* out_rows, float* out_scores) {
     mv.src_scores = (const float*)scores_[cur_].ptr;
     mv.dst_rows = (uint4*)out_rows;
     mv.dst_scores = out_scores;
+    TopkFused f;
     topk_launch((const float*)scores_[cur_].ptr, k16, cfg_.L + 1, cfg_.S, k, true, false, nullptr, topk_ws_.ptr, stream,
-                &mv);
+                &mv, fused_select(f));
     return;
   }
   uint32_t* idx = (uint32_t*)scratch(4ull * k);
@@ -814,6 +843,8 @@ void Island::emigrate(uint32_t k, void* out_rows, float* out_scores) {
 void Island::immigrate(uint32_t k, const void* in_rows, const float* in_scores) {
   TraceRange tr("pga.migrate.immigrate");
   if (k == 0) return;
+  TopkFused f;
+  const TopkFused* fsel = fused_select(f);  // the victims' selection, before the keys change
   invalidate_qk();
   if (k > cfg_.S) throw std::invalid_argument("k exceeds population size");
   uint16_t* k16 = integer_objective(cfg_.objective, cfg_.L) ? (uint16_t*)keys_[cur_].ptr : nullptr;
@@ -841,7 +872,7 @@ void Island::immigrate(uint32_t k, const void* in_rows, const float* in_scores) 
     mv.dst_scores = (float*)scores_[cur_].ptr;
     mv.dst_keys = k16;
     topk_launch((const float*)scores_[cur_].ptr, k16, cfg_.L + 1, cfg_.S, k, false, false, nullptr, topk_ws_.ptr,
-                stream, &mv);
+                stream, &mv, fsel);
     // the victims' keys were written with their rows: only the best partials follow
     n_best_[cur_] = best_of_scores_launch((const float*)scores_[cur_].ptr, cfg_.S,
                                           (unsigned long long*)best_[cur_].ptr, stream, nullptr);
@@ -851,6 +882,41 @@ void Island::immigrate(uint32_t k, const void* in_rows, const float* in_scores) 
   uint32_t* idx = (uint32_t*)scratch(4ull * k);
   topk(k, false, idx, false);
   scatter(idx, k, in_rows, in_scores);
+}
+
+void Island::set_fused_histogram(bool on) {
+  fhist_user_ = on;
+  fhist_on_ = on || cfg_.n_elite > 1;
+}
+
+bool Island::fhist_ready_for(const GenArgs& a) const {
+  // the conditions under which binary_gen_tp runs with u16 keys (binary_gs.hip
+  // launch_mode), so the launch really produces the histogram
+  if (!fhist_on_ || !on_gpu() || capturing_ || jit_ || cfg_.encoding != ENC_BINARY) return false;
+  if (!integer_objective(cfg_.objective, cfg_.L) || cfg_.L + 1 > kHistMaxBins || a.key_cur == nullptr) return false;
+  if (cfg_.objective == OBJ_KNAPSACK) return false;
+  uint32_t gs = 0;
+  bool full = false, dense = false;
+  if (!binary_tp_plan(a, gs, full, dense)) return false;
+  if (!fhist_[0].ptr) {  // allocated zeroed on first use
+    Island* self = const_cast<Island*>(this);
+    for (auto& b : self->fhist_) {
+      b = self->alloc(4ull * fused_hist_words(cfg_.L + 1));
+      PGA_HIP_CHECK(hipMemsetAsync(b.ptr, 0, b.bytes, stream));
+    }
+  }
+  return true;
+}
+
+const TopkFused* Island::fused_select(TopkFused& f) {
+  const int b = on_gpu() ? fhist_of_[cur_] : -1;
+  if (b < 0) return nullptr;
+  f.hist = (const uint32_t*)fhist_[b].ptr;
+  f.status = (uint32_t*)fhist_[b].ptr + (cfg_.L + 1 + 3) / 4 * 4;
+  if (!fhist_clean_[b])  // a selection on this population already used its status words
+    PGA_HIP_CHECK(hipMemsetAsync(f.status, 0, 4ull * kTopkStatusWords, stream));
+  fhist_clean_[b] = false;
+  return &f;
 }
 
 bool Island::evaluate_rows(void* rows, float* scores, uint32_t n) {
@@ -1024,6 +1090,7 @@ void Island::save(const std::string& path) {
 
 void Island::load(const std::string& path) {
   TraceRange tr("pga.checkpoint.load");
+  invalidate();
   FILE* f = std::fopen(path.c_str(), "rb");
   if (!f) throw std::runtime_error("cannot open checkpoint: " + path);
   CkptHeader h;

@@ -417,6 +417,16 @@ __device__ unsigned long long pga_tp_clk[kMaxGrid * 4][8];
 #ifndef PGA_TP_NOKEYS
 #define PGA_TP_NOKEYS 0
 #endif
+// Small tail units (experiment builds: -DPGA_TP_SMALL=1): the last NW
+// units' worth of a 16-wave block's round as 16-child units, so the CU's
+// waves end within one small unit of each other.  Measured slower (round 5,
+// interleaved A/B: 93.4 / 93.5 / 92.7 vs 91.8 / 91.7 / 92.3 us/gen on the
+// driver's early generations, 90.3 vs 89.8 converged): a small unit's
+// RESOLVE (64 lanes of child records for 16 children) and the refill of the
+// PD-deep row pipeline at every unit cost more than the tail they remove.
+#ifndef PGA_TP_SMALL
+#define PGA_TP_SMALL 0
+#endif
 
 __device__ __forceinline__ uint32_t pos16(uint4 r1, uint32_t k) {  // k-th packed 16-bit position
   const uint32_t w = sel4(u32x4{r1.x, r1.y, r1.z, r1.w}, k >> 1);
@@ -450,6 +460,7 @@ __device__ __forceinline__ void binary_gen_tp_body(GenArgs a, unsigned long long
   __shared__ unsigned long long lds_red[kTpMaxWaves];
   __shared__ uint32_t lds_next;   // the round's next unbred unit
   __shared__ uint32_t lds_tnext;  // the round's next tournament segment
+  __shared__ uint32_t lds_role;   // the round's producer tickets (tp_producers)
   __shared__ uint32_t lds_ready[kTpMaxSegs];  // per segment: its parents are in LDS
   constexpr bool KMF = OBJ == kObjKnapMfma;
   __shared__ uint4 lds_kscr[KMF ? kTpMaxWaves : 1][kKnapScratch];      // knapsack: per-wave chunk / C scratch
@@ -462,6 +473,10 @@ __device__ __forceinline__ void binary_gen_tp_body(GenArgs a, unsigned long long
   // ahead -- since vector memory counters retire in order: a drained pipeline
   // per unit (110.8 vs 89.8 us/gen); LDS reads wait on their own counter.
   constexpr bool JIT = OBJ == kObjJit;
+  // fused key histogram (GenArgs::key_hist): an LDS histogram of the keys the
+  // block writes, after the round's parents in dynamic LDS (the launcher adds
+  // hist_bins words), flushed with one global atomic per non-empty bin
+  constexpr bool HISTK = KEY && !JIT;
 
   const uint32_t lane = lane_id(), wid = threadIdx.x >> 6;
   const uint32_t q = lane & (GS - 1), gbase = lane & ~(uint32_t)(GS - 1), g = lane / GS;
@@ -491,12 +506,16 @@ __device__ __forceinline__ void binary_gen_tp_body(GenArgs a, unsigned long long
 
   // this block's children [bbegin, bend) (tp.hpp)
   const uint32_t U = tp_unit(a, NG);  // children per breed unit (tp.hpp)
+  constexpr uint32_t USMALL = PD * NG > 16u ? PD * NG : 16u;  // the round's tail units (a power of two <= 64)
   uint32_t bbegin, bend;
   tp_block_range(S, U, bbegin, bend, a.tp_skew);
   const uint32_t pcap = tp_par_cap(NW);
   // JIT staging after the parents: kJitStageSteps KB per wave (jit.cpp adds it to the launch's LDS)
   uint4* lds_stage = (uint4*)(pga_dyn_lds + NW * 4096u + pcap * 8u) + wid * (kJitStageSteps * 64u);
   (void)lds_stage;
+  uint32_t* lds_hist = (uint32_t*)(pga_dyn_lds + NW * 4096u + pcap * 8u);  // (never with the JIT staging)
+  const bool hist = HISTK && a.key_hist != nullptr;  // block-uniform
+  const uint32_t hmax = a.hist_bins - 1u;
   // the pair pool (tp.hpp): one round, tournament or random selection; the
   // block's own units end at own_end, the last P units are the pair's
   const uint32_t P = a.tp_pool_units;
@@ -509,23 +528,26 @@ __device__ __forceinline__ void binary_gen_tp_body(GenArgs a, unsigned long long
   const uint32_t own_end = pool_on ? tp_pool_start(bbegin, bend, U, P) : bend;
   const uint32_t pair = blockIdx.x & ~1u, npair = pair + 1u < gridDim.x ? 2u : 1u;
 
-  // elite sources of children [0, n_elite) (n_elite <= kTpMaxElite), for the
-  // block that holds any of them
-  if (a.n_elite > 0 && bbegin < a.n_elite) {
-    if (a.elite_idx) {
-      for (uint32_t i = threadIdx.x; i < a.n_elite; i += blockDim.x) lds_el[i] = a.elite_idx[i];
-    } else {
-      unsigned long long b = block_reduce_parts_n(a.best_cur, a.n_best_cur, lds_red, NW);
-      if (threadIdx.x == 0) lds_el[0] = (uint32_t)best_index(b);
-    }
-  }
-  if (bitflip)
-    for (uint32_t i = threadIdx.x; i < kMutCap; i += blockDim.x) lds_thr[i] = a.mut_thr[i];
+  // The elite sources of children [0, n_elite) (n_elite <= kTpMaxElite, for
+  // the block that holds any of them) and the mutation table are loaded by
+  // wave 0 AFTER the round's first barrier and published by a flag that only
+  // RESOLVE waits on: the tournaments never need them, and the barrier no
+  // longer waits for their global round trips (nor block 0 for the reduction
+  // of every block's best partial)
+  __shared__ uint32_t lds_pro;  // 1: lds_el / lds_thr are loaded
+  bool pro_ok = false;          // wave-uniform: this wave has seen lds_pro set
   if (KMF)
     for (uint32_t i = threadIdx.x; i < kKnapSlices * 4 * kKnapMaxCols; i += blockDim.x)
       lds_ktab[i] = ((const uint4*)a.knap_tab)[i];
-  if (threadIdx.x == 0) lds_next = lds_tnext = 0;
+  if (threadIdx.x == 0) lds_next = lds_tnext = lds_role = lds_pro = 0;
   if (threadIdx.x < kTpMaxSegs) lds_ready[threadIdx.x] = 0;
+  if (hist) {
+    for (uint32_t i = threadIdx.x; i < a.hist_bins; i += blockDim.x) lds_hist[i] = 0;
+    if (a.hist_zero)  // a later generation's histogram starts from zero
+      for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < a.hist_zero_words; i += gridDim.x * blockDim.x)
+        a.hist_zero[i] = 0;
+  }
+  const uint32_t nprod = tp_producers(NW);
 
   unsigned long long my_best = 0;
   ScoreStats st;
@@ -533,127 +555,53 @@ __device__ __forceinline__ void binary_gen_tp_body(GenArgs a, unsigned long long
   static_assert(sizeof(lds_rec[0]) >= kSegBatches * 64 * sizeof(uint4), "contestant staging");
 #ifdef PGA_TP_TIMING
   const unsigned long long clk0 = clock64(), rt0 = wall_clock64();
-  unsigned long long clk_t = 0, clk_b = 0, n_bred = 0;
+  unsigned long long clk_t = 0, clk_b = 0, n_bred = 0, clk_spin = 0;
 #endif
   for (uint32_t rbeg = bbegin; rbeg < bend; rbeg += pcap) {  // block-uniform rounds
     const uint32_t rend0 = rbeg + pcap < bend ? rbeg + pcap : bend;
     const uint32_t rend = rend0 < own_end ? rend0 : own_end;                // the round's own children
-    const uint32_t nb = (rend - rbeg + U - 1) / U;                          // the round's units
+    // the round's units: U children each (PGA_TP_SMALL: the last NW units'
+    // worth of a 16-wave block as small units of USMALL >= PD steps)
+    const uint32_t nu = (rend - rbeg + U - 1) / U;
+    const bool tail_small = PGA_TP_SMALL && USMALL < U && NW == kTpMaxWaves && !pool_on && nu >= 2u * NW;
+    const uint32_t nbig = tail_small ? nu - NW : nu;
+    const uint32_t nb = nbig + (tail_small ? (rend - rbeg - nbig * U + USMALL - 1) / USMALL : 0u);
     const uint32_t nseg = (rend - rbeg + kSegBatches * 64 - 1) / (kSegBatches * 64);  // its tournament segments
-    __syncthreads();  // tables / elites / counter visible; the previous round's records and parents released
+    __syncthreads();  // tables / counters visible; the previous round's records and parents released
 #ifdef PGA_TP_TIMING
     const unsigned long long clkA = clock64();
 #endif
+    if (rbeg == bbegin && wid == 0) {  // wave-uniform: the prologue loads (lds_pro)
+      if (a.n_elite > 0 && bbegin < a.n_elite) {
+        if (a.elite_idx) {
+          for (uint32_t i = lane; i < a.n_elite; i += 64) lds_el[i] = a.elite_idx[i];
+        } else {
+          const unsigned long long b = wave_reduce_parts(a.best_cur, a.n_best_cur);
+          if (lane == 0) lds_el[0] = (uint32_t)best_index(b);
+        }
+      }
+      if (bitflip)
+        for (uint32_t i = lane; i < kMutCap; i += 64) lds_thr[i] = a.mut_thr[i];
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+      tp_flag_set(&lds_pro);
+    }
 
     // TOURNAMENTS of the round, one segment of <= kSegBatches batches at a
     // time per wave, segments pulled from a counter: all key loads of a
     // segment in flight at once; the contestants wait in the wave's record
     // ring (free until it breeds).  A wave breeds as soon as no segment is
     // left; a unit's RESOLVE waits for its segment's flag (no block barrier)
-    for (;;) {
+    const bool produce = nprod >= NW || tp_ticket(&lds_role, lane) < nprod;  // wave-uniform
+    while (produce) {
       const uint32_t sg = tp_ticket(&lds_tnext, lane);
       if (sg >= nseg) break;
       const uint32_t begin = rbeg + sg * kSegBatches * 64u;
       const uint32_t end = begin + kSegBatches * 64u < rend ? begin + kSegBatches * 64u : rend;
-      const uint32_t nbatch = (end - begin + 63) / 64;
       uint2* par = lds_par + sg * kSegBatches * 64u;
-      uint4* ixs = &rec[0][0][0];  // [B * 64 + lane]: 4 x 64 x 16 B = the ring's 4 KiB
-      // raw keys (u16 zero-extended, or f32 scores), compared only after every
-      // load of the segment is issued: a conversion here would make hipcc wait
-      // for each batch's loads before issuing the next batch's
-      using KT = typename std::conditional<KEY, uint32_t, float>::type;
-      KT k0[kSegBatches], k1[kSegBatches], k2[kSegBatches], k3[kSegBatches];
-#pragma unroll
-      for (uint32_t B = 0; B < kSegBatches; ++B) {
-        const uint32_t tc = begin + B * 64u + lane;
-        const uint32_t cc = tc < end ? tc : end - 1;
-        u32x4 blk{0u, 0u, 0u, 0u};
-        if (B < nbatch) blk = draw<true>(a.key, ST_SEL, cc, 0);  // wave-uniform; batches past the end load line 0
-        const uint4 ix = make_uint4(word_to_index(blk.x, S), word_to_index(blk.y, S), word_to_index(blk.z, S),
-                                    word_to_index(blk.w, S));
-        ixs[B * 64u + lane] = ix;
-        const uint4 j = tourn ? ix : make_uint4(0, 0, 0, 0);
-        if (roul) {  // wave-uniform: the two selection words, searched below for every batch at once
-          k0[B] = __builtin_bit_cast(KT, blk.x);
-          k1[B] = __builtin_bit_cast(KT, blk.y);
-        } else if (rank) {  // wave-uniform: linear ranking, the two parents straight from the rank order
-          const u32x4 b1 = draw<true>(a.key, ST_SEL, cc, 1);
-          const uint32_t ra = rank_pick(blk.x, blk.y, blk.z, S, a.rank_thresh);
-          const uint32_t rb = rank_pick(blk.w, b1.x, b1.y, S, a.rank_thresh);
-          k0[B] = __builtin_bit_cast(KT, ELEM(const uint32_t, a.rank_order, ra));
-          k1[B] = __builtin_bit_cast(KT, ELEM(const uint32_t, a.rank_order, rb));
-        } else if constexpr (KEY && PGA_TP_NOKEYS) {  // experiment: tournaments without key reads
-          k0[B] = j.x & 1023u;
-          k1[B] = j.y & 1023u;
-          k2[B] = j.z & 1023u;
-          k3[B] = j.w & 1023u;
-        } else if constexpr (KEY) {
-          k0[B] = ELEM(const uint16_t, a.key_cur, j.x);
-          k1[B] = ELEM(const uint16_t, a.key_cur, j.y);
-          k2[B] = ELEM(const uint16_t, a.key_cur, j.z);
-          k3[B] = ELEM(const uint16_t, a.key_cur, j.w);
-        } else {
-          k0[B] = ELEM(const float, a.score_cur, j.x);
-          k1[B] = ELEM(const float, a.score_cur, j.y);
-          k2[B] = ELEM(const float, a.score_cur, j.z);
-          k3[B] = ELEM(const float, a.score_cur, j.w);
-        }
-        // no early exit past the segment's last batch: straight-line loads keep
-        // every key in a register (a wave-uniform break spilled the last four);
-        // the extra batches skip the Philox draw and are never bred (their
-        // parents land inside the round's slots: tp_par_cap holds whole segments)
-      }
-      if (roul) {
-        // fitness-proportional, by the guide table: the pick is the smallest i
-        // with cumfit[i] >= u * total (roulette_pick's binary search); the guide
-        // entry of the target's bucket is a lower bound for it, so one guide load,
-        // one cumfit load and (rarely) a short forward scan find it.  The
-        // 2 x kSegBatches picks of a lane advance in lock step.
-        constexpr uint32_t NS = 2 * kSegBatches;
-        const float total = a.cumfit[S - 1];
-        const float scale = *a.roul_scale;
-        uint32_t ix[NS];
-        float tg[NS];
-#pragma unroll
-        for (uint32_t i = 0; i < NS; ++i) {
-          const uint32_t w = __builtin_bit_cast(uint32_t, (i & 1u) ? k1[i >> 1] : k0[i >> 1]);
-          tg[i] = word_to_unit(w) * total;
-          ix[i] = total > 0.f ? ELEM(const uint32_t, a.roul_guide, roulette_bucket(tg[i], scale, S)) : word_to_index(w, S);
-        }
-        float v[NS];
-#pragma unroll
-        for (uint32_t i = 0; i < NS; ++i) v[i] = ELEM(const float, a.cumfit, ix[i]);
-        for (uint32_t it = 0; it < S; ++it) {  // wave-uniform: until every pick of every lane is resolved
-          bool more = false;
-#pragma unroll
-          for (uint32_t i = 0; i < NS; ++i) more |= total > 0.f && v[i] < tg[i];
-          if (!__any(more)) break;
-#pragma unroll
-          for (uint32_t i = 0; i < NS; ++i) {
-            const bool adv = total > 0.f && v[i] < tg[i];
-            ix[i] += adv ? 1u : 0u;
-            v[i] = ELEM(const float, a.cumfit, ix[i]);
-          }
-        }
-#pragma unroll
-        for (uint32_t B = 0; B < kSegBatches; ++B) {
-          k0[B] = __builtin_bit_cast(KT, ix[2 * B]);
-          k1[B] = __builtin_bit_cast(KT, ix[2 * B + 1]);
-        }
-      }
-#pragma unroll
-      for (uint32_t B = 0; B < kSegBatches; ++B) {
-        const uint4 ix = ixs[B * 64u + lane];
-        uint32_t pa = ix.x, pb = ix.y;
-        if (tourn) {
-          pa = k0[B] < k1[B] ? ix.y : ix.x;
-          pb = k2[B] < k3[B] ? ix.w : ix.z;
-        } else if (rank || roul) {
-          pa = __builtin_bit_cast(uint32_t, k0[B]);
-          pb = __builtin_bit_cast(uint32_t, k1[B]);
-        }
-        par[B * 64u + lane] = make_uint2(pa, pb);
-      }
+      // the contestants wait in the wave's record ring (4 x 64 x 16 B = its
+      // 4 KiB, free until it breeds); every key load of the segment in flight
+      // at once (tp.hpp, the one definition shared with real_gen_tp)
+      tp_select_segment<KEY ? (PGA_TP_NOKEYS ? TP_NOKEY : TP_KEY16) : TP_F32>(a, begin, end, lane, &rec[0][0][0], par);
       // publish: the segment's parents (this wave's LDS stores, in order)
       // before its flag
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
@@ -668,18 +616,33 @@ __device__ __forceinline__ void binary_gen_tp_body(GenArgs a, unsigned long long
     clk_t += clkB - clkA;
 #endif
 
+#ifdef PGA_TP_TIMING
+#define PGA_TP_SPIN0 const unsigned long long sp0_ = clock64();
+#define PGA_TP_SPIN1 clk_spin += clock64() - sp0_;
+#else
+#define PGA_TP_SPIN0
+#define PGA_TP_SPIN1
+#endif
     // RESOLVE: parents, crossover plan and flip positions of the round's unit
     // BI -> the records of ring slot SL (lanes past the unit: unused copies)
 #define PGA_TP_RESOLVE(US, UE, SL)                                                                              \
   {                                                                                                             \
+    if (!pro_ok) { /* the prologue loads of wave 0 (once per wave) */                                          \
+      while (__hip_atomic_load(&lds_pro, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == 0u)                 \
+        __builtin_amdgcn_s_sleep(1);                                                                            \
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");                                                    \
+      pro_ok = true;                                                                                            \
+    }                                                                                                           \
     const uint32_t tc = (US) + lane;                                                                            \
     const uint32_t cc = tc < (UE) ? tc : (UE) - 1;                                                              \
     uint32_t pa, pb;                                                                                            \
     if ((US) - rbeg < rend - rbeg) { /* an own unit: parents from the round's tournaments */                    \
       /* its segment is done (wave-uniform spin, rare) */                                                       \
       const uint32_t sg_ = ((US) - rbeg) / (kSegBatches * 64u);                                                 \
+      PGA_TP_SPIN0                                                                                              \
       while (__hip_atomic_load(&lds_ready[sg_], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == 0u)          \
         __builtin_amdgcn_s_sleep(1);                                                                            \
+      PGA_TP_SPIN1                                                                                              \
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");                                                    \
       const uint2 pp = lds_par[cc - rbeg];                                                                      \
       pa = pp.x;                                                                                                \
@@ -763,14 +726,19 @@ __device__ __forceinline__ void binary_gen_tp_body(GenArgs a, unsigned long long
     // units from its LDS counter, then pool units from the pair's counter
     constexpr uint32_t kNoUnit = 0xFFFFFFFFu;
     bool steal = false;  // wave-uniform: own units exhausted, pulling pool units
-#define PGA_TP_NEXT(US, UE)                                                                                 \
+#define PGA_TP_NEXT(US, UE, UN)                                                                             \
   {                                                                                                         \
     US = kNoUnit;                                                                                           \
+    UN = U / NG;                                                                                            \
     if (!steal) {                                                                                           \
       const uint32_t tk_ = tp_ticket(&lds_next, lane);                                                      \
-      if (tk_ < nb) {                                                                                       \
+      if (tk_ < nbig) {                                                                                     \
         US = rbeg + tk_ * U;                                                                                \
         UE = US + U < rend ? US + U : rend;                                                                 \
+      } else if (tk_ < nb) { /* a small tail unit */                                                        \
+        US = rbeg + nbig * U + (tk_ - nbig) * USMALL;                                                       \
+        UE = US + USMALL < rend ? US + USMALL : rend;                                                       \
+        UN = USMALL / NG;                                                                                   \
       } else {                                                                                              \
         steal = pool_on;                                                                                    \
       }                                                                                                     \
@@ -791,20 +759,20 @@ __device__ __forceinline__ void binary_gen_tp_body(GenArgs a, unsigned long long
     }                                                                                                       \
   }
 
-    uint32_t ns, ne = 0;  // the wave's next unit (prefetched ticket)
-    PGA_TP_NEXT(ns, ne)
+    uint32_t ns, ne = 0, nn = 0;  // the wave's next unit and its steps (prefetched ticket)
+    PGA_TP_NEXT(ns, ne, nn)
     if (ns != kNoUnit) {
       // breed cursor: ring slot, step, its unit [bs, be) and steps.  Every
-      // unit takes U / NG steps, a partial one (only ever at S) too: its
-      // children past S write the padding rows, and a unit never holds fewer
-      // steps than the PD the load cursor runs ahead
-      const uint32_t nst = U / NG;
+      // unit takes its full size / NG steps, a partial one (only ever at S)
+      // too: its children past S write the padding rows, and a unit never
+      // holds fewer steps than the PD the load cursor runs ahead
+      uint32_t nst = nn;
       uint32_t slot = 0, i = 0, bs = ns, be = ne;
-      PGA_TP_NEXT(ns, ne)
+      PGA_TP_NEXT(ns, ne, nn)
       PGA_TP_RESOLVE(bs, be, 0u)
       // load cursor; lpend: at the end of its unit with unit ns next;
       // lmore = false: past the wave's last step
-      uint32_t lslot = 0, li = 0, lbs = bs, lbe = be;
+      uint32_t lslot = 0, li = 0, lbs = bs, lbe = be, lnst = nst;
       bool lpend = false, lmore = true, done = false;
 
       // LOAD the parent rows of the load cursor's step into (YA, YB) and
@@ -817,13 +785,14 @@ __device__ __forceinline__ void binary_gen_tp_body(GenArgs a, unsigned long long
       li = 0;                                                                                               \
       lbs = ns;                                                                                             \
       lbe = ne;                                                                                             \
+      lnst = nn;                                                                                            \
       lpend = false;                                                                                        \
-      PGA_TP_NEXT(ns, ne)                                                                                   \
+      PGA_TP_NEXT(ns, ne, nn)                                                                               \
     }                                                                                                       \
     const uint4 r = rec[lmore ? lslot : slot][(lmore ? li : i) * NG + g][0];                                \
     YA = ROW(cur, r.x, qq);                                                                                 \
     YB = ROW(cur, r.y, qq);                                                                                 \
-    if (lmore && ++li == nst) {                                                                             \
+    if (lmore && ++li == lnst) {                                                                            \
       lpend = ns != kNoUnit;                                                                                \
       lmore = lpend;                                                                                        \
     }                                                                                                       \
@@ -882,6 +851,11 @@ __device__ __forceinline__ void binary_gen_tp_body(GenArgs a, unsigned long long
     if (EVALS && !JIT) { /* every lane of the group stores the same score */                                \
       ELEM(float, a.score_next, c) = sc;                                                                    \
       if (KEY) ELEM(uint16_t, a.key_next, c) = (uint16_t)sc;                                                \
+      if (hist && q == 0u && c < S) {                                                                       \
+        const uint32_t kb = (uint16_t)sc;                                                                   \
+        __hip_atomic_fetch_add(&lds_hist[kb < hmax ? kb : hmax], 1u, __ATOMIC_RELAXED,                      \
+                               __HIP_MEMORY_SCOPE_WORKGROUP);                                               \
+      }                                                                                                     \
       const unsigned long long pk = c < S ? pack_best(sc, c) : 0ull;                                        \
       my_best = pk > my_best ? pk : my_best;                                                                \
       st.add_if(q == 0u && c < S, sc);                                                                      \
@@ -895,6 +869,7 @@ __device__ __forceinline__ void binary_gen_tp_body(GenArgs a, unsigned long long
         i = 0;                                                                                              \
         bs = lbs;                                                                                           \
         be = lbe;                                                                                           \
+        nst = lnst;                                                                                         \
       }                                                                                                     \
     }                                                                                                       \
   }
@@ -967,12 +942,14 @@ __device__ __forceinline__ void binary_gen_tp_body(GenArgs a, unsigned long long
 #undef PGA_TP_COUNT
     }
 #undef PGA_TP_RESOLVE
+#undef PGA_TP_SPIN0
+#undef PGA_TP_SPIN1
 #ifdef PGA_TP_TIMING
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this round's stores issued and done
     clk_b += clock64() - clkB;
 #endif
     __syncthreads();  // every wave out of the round's counters before they are reset
-    if (threadIdx.x == 0) lds_next = lds_tnext = 0;
+    if (threadIdx.x == 0) lds_next = lds_tnext = lds_role = 0;
     if (threadIdx.x < kTpMaxSegs) lds_ready[threadIdx.x] = 0;
   }
 #undef ROW
@@ -987,8 +964,14 @@ __device__ __forceinline__ void binary_gen_tp_body(GenArgs a, unsigned long long
     pga_tp_clk[wv][4] = rt0;
     pga_tp_clk[wv][5] = wall_clock64();
     pga_tp_clk[wv][6] = __builtin_amdgcn_s_getreg((3 << 11) | 20);  // HW_REG_XCC_ID[3:0]
+    pga_tp_clk[wv][7] = clk_spin;  // cycles a breeding wave waited for a segment's flag
   }
 #endif
+  if (hist)  // every wave passed the last round's barrier: the block's counts are complete
+    for (uint32_t i = threadIdx.x; i < a.hist_bins; i += blockDim.x) {
+      const uint32_t v = lds_hist[i];
+      if (v) __hip_atomic_fetch_add(&a.key_hist[i], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
   if (EVALS && best_parts) {  // block-uniform
     unsigned long long bb = block_max_u64_n(my_best, lds_red, NW);
     if (threadIdx.x == 0) best_parts[blockIdx.x] = bb;

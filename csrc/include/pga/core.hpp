@@ -272,9 +272,13 @@ struct GenArgs {
   int32_t selection;
   uint32_t tour_k;
   const float* cumfit;  // roulette: inclusive prefix sums of shifted scores (S)
-  // roulette guide table (util.hip roulette_guide_launch): roul_guide[b] = the
-  // first individual whose cumfit bucket is >= b, bucket(t) =
-  // roulette_bucket(t, *roul_scale, S); nullptr: binary search only
+  // roulette guide table (util.hip roulette_guide_launch), 4 words per bucket
+  // b: {g = the first individual whose cumfit bucket is >= b, cumfit[g] as
+  // f32 bits, g + 1 when g + 1 is the first individual of bucket b + 1 (else
+  // ~0), 0}, bucket(t) = roulette_bucket(t, *roul_scale, S).  A pick of
+  // target t in bucket b is g when t <= cumfit[g], else g + 1 when the third
+  // word says so (one 16-byte load per pick), else the smallest i > g with
+  // cumfit[i] >= t.  nullptr: binary search only
   const uint32_t* roul_guide;
   const float* roul_scale;
   const uint32_t* rank_order;  // rank: individuals by ascending (score_key, index)
@@ -368,7 +372,19 @@ struct GenArgs {
   // full matrix)
   const void* obj_aux;
   uint32_t obj_aux_kind, obj_aux_bytes;
+  // fused key histogram (binary_gen_tp, integer objectives): when set, the
+  // generation kernel adds the histogram of the u16 keys it writes (each
+  // clamped to hist_bins - 1) to key_hist, which is zero before the launch,
+  // and zeroes hist_zero[0, hist_zero_words) — a later generation's buffer
+  // and its selection status words (the Island rotates three buffers).  Exact top-k / bottom-k selections (migration,
+  // elitism, pga_get_best_top) then need no histogram pass over the keys.
+  uint32_t* key_hist;
+  uint32_t* hist_zero;
+  uint32_t hist_bins, hist_zero_words;
 };
+// the fused histogram's LDS bins (binary_gen_tp): objectives with more key
+// values use the separate histogram pass
+constexpr uint32_t kHistMaxBins = 2048;
 
 PGA_HD uint32_t sel_words(const GenArgs& a) {
   return a.selection == SEL_TOURNAMENT ? 2u * a.tour_k : (a.selection == SEL_RANK ? 6u : 2u);

@@ -70,6 +70,18 @@ __device__ __forceinline__ unsigned long long block_reduce_parts(const unsigned 
   return block_max_u64<BLK>(v, lds4);
 }
 
+// one wave's max over an array of packed bests (every lane gets it)
+__device__ __forceinline__ unsigned long long wave_reduce_parts(const unsigned long long* parts, uint32_t n) {
+  unsigned long long v = 0;
+  for (uint32_t i = lane_id(); i < n; i += 64) v = parts[i] > v ? parts[i] : v;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    unsigned long long w = shfl_xor_u64(v, o);
+    v = w > v ? w : v;
+  }
+  return v;
+}
+
 // the same two for a block of `nw` waves chosen at launch (nw <= 16; lds:
 // nw entries)
 __device__ __forceinline__ unsigned long long block_max_u64_n(unsigned long long v, unsigned long long* lds,

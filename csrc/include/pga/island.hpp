@@ -22,6 +22,10 @@
 #include "pga/jit.hpp"
 
 namespace pga {
+struct TopkFused;  // ops.hpp
+}
+
+namespace pga {
 
 struct Config {
   int32_t encoding = ENC_BINARY;
@@ -151,6 +155,16 @@ class Island {
   // score n external rows (e.g. received migrants) with this island's
   // objective, in place; false when the objective is not native (OBJ_NONE)
   bool evaluate_rows(void* rows, float* scores, uint32_t n);
+  // Fused key histogram (GenArgs::key_hist): when on, the BINARY generation
+  // kernel of an integer objective also produces the value histogram of the
+  // keys it writes, and the exact top-k / bottom-k selections of that
+  // population (migration, elitism > 1, unsorted top-k) skip their histogram
+  // pass over the keys.  On by default with elitism > 1; island models turn it
+  // on for migration.  Results are identical either way.
+  void set_fused_histogram(bool on);
+  bool fused_histogram() const { return fhist_on_; }
+  // a fused histogram of the current population is available (tests, benches)
+  bool fused_histogram_ready() const { return fhist_of_[cur_] >= 0; }
 
   // raw buffers (cur = current generation)
   void* rows(int which) { return rows_[which ^ cur_].ptr; }
@@ -212,7 +226,10 @@ class Island {
   // generation (+ score_stats workspace), the range the GEN kernel quantizes
   // the next generation's keys over
   bool real_qk() const;
-  void invalidate_qk() { qk_valid_[cur_] = false; }
+  void invalidate_qk() {
+    qk_valid_[cur_] = false;
+    fhist_of_[cur_] = -1;  // the keys of the current population change
+  }
   Buffer qk_ws_;
   bool qk_valid_[2] = {false, false};
   Buffer qubo_qt_;               // QUBO: int8 Q^T packed from objective data slot 0 (GPU)
@@ -255,7 +272,20 @@ class Island {
   bool run_graph(uint32_t reps, bool fresh);
   bool capture_graph();
   void drop_graph();
-  void invalidate() { ++version_; }
+  void invalidate() {
+    ++version_;
+    fhist_of_[0] = fhist_of_[1] = -1;
+  }
+  // fused key histograms: three buffers of fused_hist_words(L + 1) words
+  // rotated by the generations that produce one (each zeroes the next);
+  // fhist_of_[p] = the buffer with the histogram of parity p's population
+  Buffer fhist_[3];
+  int fhist_of_[2] = {-1, -1};
+  bool fhist_clean_[3] = {true, true, true};  // its selection status words are still zero
+  uint32_t fhist_rot_ = 0;
+  bool fhist_on_ = false, fhist_user_ = false;
+  bool fhist_ready_for(const GenArgs& a) const;  // this GEN launch produces the histogram
+  const TopkFused* fused_select(TopkFused& f);    // the current population's histogram for a select
   uint32_t graph_g_ = 0, version_ = 0;
   bool graph_broken_ = false, capturing_ = false;
   uint32_t capture_base_ = 0;

@@ -25,6 +25,10 @@ namespace dev {
 
 constexpr uint32_t kSegBatches = PGA_TP_SEG;
 constexpr int kObjJit = 1001;  // launcher-only objective id: a linked user objective (jitgen*.hip)
+// launcher-only objective id: the reference ABI's obj_f device function
+// pointer (GenArgs::user_fn), called on the staged LDS row like a linked
+// objective (real_dev.hpp)
+constexpr int kObjUserFn = 1002;
 constexpr uint32_t kTpMaxElite = 64;  // elites the transposed kernels route through their records
 
 // element i of a buffer with a 32-bit byte offset (uniform base + one VGPR)
@@ -36,7 +40,8 @@ __device__ __forceinline__ T ld32(const void* base, uint32_t i) {
 // Tournament key modes: the f32 scores; the u16 keys of an integer
 // objective (exact); or quantized u16 keys of a float objective (core.hpp
 // qkey: equal keys fall back to the f32 scores, the exact result either way)
-enum TpKeys : int { TP_F32 = 0, TP_KEY16 = 1, TP_QKEY16 = 2 };
+// (TP_NOKEY: experiment builds only, tournaments on fake keys without loads)
+enum TpKeys : int { TP_F32 = 0, TP_KEY16 = 1, TP_QKEY16 = 2, TP_NOKEY = 3 };
 
 // Parents (A, B) of children [begin + 64 B + lane] for the segment's batches
 // B < kSegBatches -> par[B * 64 + lane].  ixs: 4 x 64 uint4 of LDS scratch
@@ -74,6 +79,11 @@ __device__ __forceinline__ void tp_select_segment(const GenArgs& a, uint32_t beg
       const uint32_t rb = rank_pick(blk.w, b1.x, b1.y, S, a.rank_thresh);
       k0[B] = __builtin_bit_cast(KT, ld32<uint32_t>(a.rank_order, ra));
       k1[B] = __builtin_bit_cast(KT, ld32<uint32_t>(a.rank_order, rb));
+    } else if constexpr (KM == TP_NOKEY) {
+      k0[B] = j.x & 1023u;
+      k1[B] = j.y & 1023u;
+      k2[B] = j.z & 1023u;
+      k3[B] = j.w & 1023u;
     } else if constexpr (KEY) {
       k0[B] = ld32<uint16_t>(a.key_cur, j.x);
       k1[B] = ld32<uint16_t>(a.key_cur, j.y);
@@ -93,34 +103,51 @@ __device__ __forceinline__ void tp_select_segment(const GenArgs& a, uint32_t beg
   }
   if (roul) {
     // fitness-proportional, by the guide table: the pick is the smallest i
-    // with cumfit[i] >= u * total (roulette_pick's binary search); the guide
-    // entry of the target's bucket is a lower bound for it, so one guide load,
-    // one cumfit load and (rarely) a short forward scan find it.  The
-    // 2 x kSegBatches picks of a lane advance in lock step.
+    // with cumfit[i] >= u * total (roulette_pick's binary search).  One
+    // 16-byte entry of the target's bucket (core.hpp GenArgs::roul_guide)
+    // holds the lower bound g, cumfit[g] and whether g + 1 opens the next
+    // bucket: t <= cumfit[g] -> g, else g + 1 when it does; the rest (rare)
+    // scans on from g + 1.  Round 4 loaded the guide index, THEN cumfit[g]:
+    // two dependent random loads per pick.  The 2 x kSegBatches picks of a
+    // lane advance in lock step.
     constexpr uint32_t NS = 2 * kSegBatches;
     const float total = a.cumfit[S - 1];
     const float scale = *a.roul_scale;
     uint32_t ix[NS];
     float tg[NS];
+    uint4 e[NS];
     #pragma unroll
     for (uint32_t i = 0; i < NS; ++i) {
       const uint32_t w = __builtin_bit_cast(uint32_t, (i & 1u) ? k1[i >> 1] : k0[i >> 1]);
       tg[i] = word_to_unit(w) * total;
-      ix[i] = total > 0.f ? ld32<uint32_t>(a.roul_guide, roulette_bucket(tg[i], scale, S)) : word_to_index(w, S);
+      const uint32_t b = total > 0.f ? roulette_bucket(tg[i], scale, S) : 0u;
+      e[i] = ld32<uint4>(a.roul_guide, b);
+      ix[i] = total > 0.f ? 0u : word_to_index(w, S);
     }
-    float v[NS];
+    bool open[NS];  // still unresolved: scan cumfit from ix
+    bool any_open = false;
     #pragma unroll
-    for (uint32_t i = 0; i < NS; ++i) v[i] = ld32<float>(a.cumfit, ix[i]);
-    for (uint32_t it = 0; it < S; ++it) {  // wave-uniform: until every pick of every lane is resolved
-      bool more = false;
+    for (uint32_t i = 0; i < NS; ++i) {
+      const bool in = tg[i] <= __builtin_bit_cast(float, e[i].y);
+      open[i] = total > 0.f && !in && e[i].z != e[i].x + 1u;
+      if (total > 0.f) ix[i] = in ? e[i].x : e[i].x + 1u;
+      any_open |= open[i];
+    }
+    if (__any(any_open)) {  // wave-uniform
+      float v[NS];
       #pragma unroll
-      for (uint32_t i = 0; i < NS; ++i) more |= total > 0.f && v[i] < tg[i];
-      if (!__any(more)) break;
-      #pragma unroll
-      for (uint32_t i = 0; i < NS; ++i) {
-        const bool adv = total > 0.f && v[i] < tg[i];
-        ix[i] += adv ? 1u : 0u;
-        v[i] = ld32<float>(a.cumfit, ix[i]);
+      for (uint32_t i = 0; i < NS; ++i) v[i] = ld32<float>(a.cumfit, ix[i] < S ? ix[i] : S - 1);
+      for (uint32_t it = 0; it < S; ++it) {  // until every open pick of every lane is resolved
+        bool more = false;
+        #pragma unroll
+        for (uint32_t i = 0; i < NS; ++i) more |= open[i] && v[i] < tg[i];
+        if (!__any(more)) break;
+        #pragma unroll
+        for (uint32_t i = 0; i < NS; ++i) {
+          const bool adv = open[i] && v[i] < tg[i];
+          ix[i] += adv ? 1u : 0u;
+          v[i] = ld32<float>(a.cumfit, ix[i] < S ? ix[i] : S - 1);
+        }
       }
     }
     #pragma unroll
@@ -200,6 +227,22 @@ __device__ __forceinline__ uint32_t tp_unit(const GenArgs& a, uint32_t NG) {
   return u >= lo && u <= 64u && (u & (u - 1u)) == 0u ? u : 64u;
 }
 
+// PRODUCER waves (one 16-wave block per CU): only the first nprod waves of a
+// round run its tournament segments, the others breed from the start, each
+// unit waiting for its segment's flag.  With every wave producing, the whole
+// GPU runs its L2-bound random key reads first (~14 us at the headline, no
+// row traffic) and its HBM-bound row gathers after (phase clocks, round 4);
+// a few producers keep ahead of the breeders (a segment of 256 children per
+// ~1.5 us of key latency against ~70 children per us consumed by a CU) and
+// the two kinds of traffic overlap.  The key reads stay concentrated in the
+// first ~20 us of the kernel, so the 2 MiB key array stays L2-resident.
+#ifndef PGA_TP_PROD
+#define PGA_TP_PROD 0
+#endif
+__device__ __forceinline__ uint32_t tp_producers(uint32_t nw) {
+  return PGA_TP_PROD > 0 && nw == kTpMaxWaves ? (uint32_t)PGA_TP_PROD : nw;
+}
+
 // One ticket per wave from an LDS counter, with no lane divergence: every
 // lane of the (full, converged) wave adds one — the atomic optimizer folds
 // the uniform add into ONE ds_add of 64 and hands the first lane the old
@@ -210,6 +253,9 @@ __device__ __forceinline__ uint32_t tp_unit(const GenArgs& a, uint32_t NG) {
 // optimizer scan the wave with a 64-step scalar loop.
 __device__ __forceinline__ uint32_t tp_ticket(uint32_t* ctr, uint32_t lane) {
   (void)lane;
+#ifdef PGA_DEBUG  // the steps of 64 need a full, converged wave at every call
+  if (__builtin_amdgcn_read_exec() != ~0ull) __builtin_trap();
+#endif
   const uint32_t t = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
   return __builtin_amdgcn_readfirstlane(t) >> 6;
 }

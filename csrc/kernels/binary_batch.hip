@@ -26,6 +26,7 @@ uint32_t batch_go(GenBatch& b, uint32_t n, uint64_t S, bool full, bool dense, hi
   for (uint32_t i = 0; i < n; ++i) {
     b.a[i].tp_unit = t.unit;
     b.a[i].tp_pool_units = b.a[i].tp_pool ? tp_pool_units(t, S) : 0u;
+    b.a[i].key_hist = nullptr;  // no fused histogram in the batched launch (no LDS for it)
   }
   const dim3 grid(t.grid, n);
   if (full) {

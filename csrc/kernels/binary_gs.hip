@@ -35,7 +35,10 @@ uint32_t go_tp(K kernel, const GenArgs& a0, unsigned long long* parts, hipStream
   a.tp_unit = t.unit;
   a.tp_pool_units = a.tp_pool ? tp_pool_units(t, a.S) : 0u;
   a.tp_skew = tp_skew_units(t, a.S);
-  hipLaunchKernelGGL(kernel, t.grid, t.block, t.lds, s, a, parts);
+  // the fused key histogram's LDS bins follow the round's parents
+  const bool hist = a.key_hist != nullptr && a.hist_bins > 0 && a.hist_bins <= kHistMaxBins;
+  if (!hist) a.key_hist = nullptr;
+  hipLaunchKernelGGL(kernel, t.grid, t.block, t.lds + (hist ? 4u * a.hist_bins : 0u), s, a, parts);
   return t.grid;
 }
 
@@ -126,6 +129,20 @@ extern "C" void pga_tp_timing_dump(uint32_t nwaves) {
     rt_max = std::max(rt_max, h[i][5]);
     st_max = std::max(st_max, h[i][4]);
     nw = i + 1;
+  }
+  {  // producers (waves that ran tournaments) vs breed-only waves
+    double c[2][5] = {{0}};
+    for (uint32_t i = 0; i < nwaves && i < kMaxGrid * 4; ++i) {
+      if (h[i][2] == 0) continue;
+      const int k = h[i][0] > 0 ? 0 : 1;
+      c[k][0] += 1; c[k][1] += (double)h[i][0]; c[k][2] += (double)h[i][1]; c[k][3] += (double)h[i][7];
+      c[k][4] += (double)h[i][3];
+    }
+    for (int k = 0; k < 2; ++k)
+      if (c[k][0] > 0)
+        std::printf("{\"tp_%s\": {\"waves\": %.0f, \"tourn_cycles\": %.0f, \"breed_cycles\": %.0f, \"spin_cycles\": %.0f, "
+                    "\"children\": %.0f}}\n", k ? "breeders" : "producers", c[k][0], c[k][1] / c[k][0],
+                    c[k][2] / c[k][0], c[k][3] / c[k][0], c[k][4] / c[k][0]);
   }
   std::printf("{\"tp_timing\": {\"waves\": %.0f, \"tourn_cycles\": %.0f, \"breed_cycles\": %.0f, "
               "\"wave_cycles\": %.0f, \"max_wave_cycles\": %.0f, \"tourn_frac\": %.3f, "

@@ -513,8 +513,10 @@ __device__ __forceinline__ void perm_gen_fast_body(GenArgs a, unsigned long long
   }
 }
 
+// the LDS-table variants launch up to 1024 threads (one table per CU); the L2
+// path and the batch kernel launch kBlock, so they keep kBlock's register cap
 template <int GS, int OBJ, int TBL = 0>
-__global__ __launch_bounds__(1024) void perm_gen_fast(GenArgs a, unsigned long long* best_parts) {
+__global__ __launch_bounds__(TBL ? 1024 : kBlock) void perm_gen_fast(GenArgs a, unsigned long long* best_parts) {
   perm_gen_fast_body<GS, OBJ, TBL>(a, best_parts);
 }
 
@@ -529,7 +531,7 @@ struct PermBatch {
   unsigned long long* parts[kPermMaxBatch];
 };
 template <int GS, int OBJ>
-__global__ __launch_bounds__(1024) void perm_gen_fast_batch(PermBatch b) {
+__global__ __launch_bounds__(kBlock) void perm_gen_fast_batch(PermBatch b) {
   perm_gen_fast_body<GS, OBJ, 0>(b.a[blockIdx.y], b.parts[blockIdx.y]);
 }
 
@@ -540,8 +542,7 @@ template <int MODE, int OBJ>
 uint32_t go_long(const GenArgs& a, unsigned long long* parts, hipStream_t s) {
   const size_t lds = perm_lds_bytes(64, a.chunks, OBJ == OBJ_TSP_EUC, 64);
   auto k = perm_kernel<64, MODE, OBJ, 64>;
-  static size_t avail = 0;
-  if (!avail) avail = allow_dynamic_lds((const void*)k);
+  const size_t avail = allow_dynamic_lds((const void*)k);
   if (lds > avail)
     throw std::invalid_argument("PERMUTATION genome too long for the LDS-resident crossover (" + std::to_string(a.L) +
                                 " genes; at most " + std::to_string(perm_max_length(OBJ == OBJ_TSP_EUC)) + ")");
@@ -560,11 +561,7 @@ uint32_t go(const GenArgs& a, unsigned long long* parts, hipStream_t s) {
   if (GS == 64 && a.L > kPermMaxL) return go_long<MODE, OBJ>(a, parts, s);
   const size_t lds = perm_lds_bytes(GS, a.chunks, OBJ == OBJ_TSP_EUC);
   auto k = perm_kernel<GS, MODE, OBJ>;
-  static bool configured = false;
-  if (!configured) {
-    allow_dynamic_lds((const void*)k);
-    configured = true;
-  }
+  (void)allow_dynamic_lds((const void*)k);
   const uint32_t gpb = kBlock / GS;
   const uint64_t need = (a.S + gpb - 1) / gpb;
   int per_cu = 0;
@@ -581,8 +578,10 @@ template <int GS, int OBJ, int TBL>
 uint32_t go_fast_blk(const GenArgs& a, unsigned long long* parts, hipStream_t s, uint32_t blk) {
   const size_t lds = perm_lds_bytes(GS, a.chunks, OBJ == OBJ_TSP_EUC, blk) + (TBL ? a.obj_aux_bytes : 0);
   auto k = perm_gen_fast<GS, OBJ, TBL>;
-  static size_t avail = 0;
-  if (!avail) avail = allow_dynamic_lds((const void*)k);
+  const size_t avail = allow_dynamic_lds((const void*)k);
+  if constexpr (TBL != 0) {  // the table did not fit this device's limit: the L2 matrix path
+    if (lds > avail) return go_fast_blk<GS, OBJ, 0>(a, parts, s, kBlock);
+  }
   const uint32_t gpb = blk / GS;
   const uint64_t need = (a.S + gpb - 1) / gpb;
   int per_cu = 0;

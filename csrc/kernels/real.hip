@@ -520,11 +520,9 @@ __global__ __launch_bounds__(kBlock) void real_long_kernel(GenArgs a, unsigned l
 template <typename K>
 uint32_t launch_occ(K k, uint32_t children_per_block, size_t lds, const GenArgs& a, unsigned long long* parts,
                     hipStream_t s, bool& configured) {
-  if (!configured) {
-    // only the dynamic-LDS kernels may need more than the default 64 KiB
-    if (lds > 0) allow_dynamic_lds((const void*)k);
-    configured = true;
-  }
+  (void)configured;
+  // only the dynamic-LDS kernels may need more than the default 64 KiB (per device)
+  if (lds > 0) (void)allow_dynamic_lds((const void*)k);
   uint64_t need = (a.S + children_per_block - 1) / children_per_block;
   int per_cu = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)k, kBlock, lds) != hipSuccess || per_cu <= 0)
@@ -548,12 +546,14 @@ uint32_t go(const GenArgs& a, unsigned long long* parts, hipStream_t s) {
 }
 
 template <typename K>
-uint32_t go_tp(K kernel, const GenArgs& a0, unsigned long long* parts, hipStream_t s, bool rot) {
+uint32_t go_tp(K kernel, const GenArgs& a0, unsigned long long* parts, hipStream_t s, bool rot, bool stage = false) {
   const TpGeom t = tp_geometry(a0.S, 1, (const void*)kernel, 64 / group_size(a0.chunks), rot ? 6 : 7);
   GenArgs a = a0;
   a.tp_unit = t.unit;
   a.tp_skew = tp_skew_units(t, a.S);
-  hipLaunchKernelGGL(kernel, t.grid, t.block, t.lds, s, a, parts);
+  // stage: the children's rows are staged in LDS for an out-of-line objective
+  const uint32_t lds = t.lds + (stage ? tp_jit_stage_bytes(t.block / 64) : 0u);
+  hipLaunchKernelGGL(kernel, t.grid, t.block, lds, s, a, parts);
   return t.grid;
 }
 
@@ -575,7 +575,11 @@ namespace {
 bool real_tp_eligible(const GenArgs& a, uint32_t GS, bool rot) {
   if (force_generic_kernels()) return false;
   if (a.S < real_tp_min_population()) return false;
-  if (a.objective == OBJ_USER_FNPTR || a.objective == OBJ_TSP_RANDOM_KEY) return false;
+  if (a.objective == OBJ_TSP_RANDOM_KEY) return false;
+  // the user function pointer: a user mutation / crossover callback runs the
+  // compat kernels instead; tournaments on the f32 scores (no keys)
+  const bool ufn = a.objective == OBJ_USER_FNPTR;
+  if (ufn && (rot || a.user_fn == nullptr || a.user_xo_fn || a.user_mut_fn)) return false;
   if (rot && GS != 4 && GS != 8) return false;
   const bool sel_ok = (a.selection == SEL_TOURNAMENT && a.tour_k == 2) || a.selection == SEL_RANDOM ||
                       (a.selection == SEL_RANK && a.rank_order != nullptr) ||
@@ -583,7 +587,7 @@ bool real_tp_eligible(const GenArgs& a, uint32_t GS, bool rot) {
   if (!sel_ok) return false;
   if (a.n_elite > kTpMaxElite || (a.n_elite > 1 && a.elite_idx == nullptr)) return false;
   // evaluating instances tournament on quantized keys (the Island keeps them)
-  if (a.objective != OBJ_NONE && (!a.key_cur || !a.key_next || !a.qk)) return false;
+  if (a.objective != OBJ_NONE && !ufn && (!a.key_cur || !a.key_next || !a.qk)) return false;
   // 32-bit offsets: the (S + kRowPad)-row buffers must stay below 4 GiB
   return (a.S + kRowPad) * (uint64_t)a.row_words * 4u <= 0xFFFFFFFFull;
 }
@@ -633,6 +637,7 @@ uint32_t launch_tp(const GenArgs& a, unsigned long long* parts, hipStream_t s) {
       case OBJ_SCHWEFEL: return go_tp(real_gen_tp<GS, OBJ_SCHWEFEL, false>, a, parts, s, ROT);
       case OBJ_LINEAR: return go_tp(real_gen_tp<GS, OBJ_LINEAR, false>, a, parts, s, ROT);
       case OBJ_KNAPSACK_REAL: return go_tp(real_gen_tp<GS, OBJ_KNAPSACK_REAL, false>, a, parts, s, ROT);
+      case OBJ_USER_FNPTR: return go_tp(real_gen_tp<GS, kObjUserFn, false>, a, parts, s, ROT, true);
       default: return go_tp(real_gen_tp<GS, OBJ_NONE, false>, a, parts, s, ROT);
     }
   }

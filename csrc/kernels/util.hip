@@ -65,22 +65,25 @@ bool force_generic_kernels() {
 }
 
 size_t allow_dynamic_lds(const void* kernel) {
+  // once per (kernel, device): the attribute is per device, so a process that
+  // drives a second GPU raises it there too
+  static std::mutex mu;
+  static std::map<std::pair<const void*, int>, size_t> raised;
+  int dev = 0;
+  PGA_HIP_CHECK(hipGetDevice(&dev));
+  std::lock_guard<std::mutex> g(mu);
+  auto it = raised.find({kernel, dev});
+  if (it != raised.end()) return it->second;
   hipFuncAttributes at;
   PGA_HIP_CHECK(hipFuncGetAttributes(&at, kernel));
   const size_t avail = 160 * 1024 - at.sharedSizeBytes;
   PGA_HIP_CHECK(hipFuncSetAttribute(kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)avail));
+  raised[{kernel, dev}] = avail;
   return avail;
 }
 
 TpGeom tp_geometry(uint64_t S, uint32_t islands, const void* kernel, uint32_t ng, uint32_t pseg) {
-  {  // the 16-wave launch's dynamic LDS is above the default limit
-    static std::mutex mu;
-    static std::set<std::pair<const void*, int>> raised;
-    int dev = 0;
-    PGA_HIP_CHECK(hipGetDevice(&dev));
-    std::lock_guard<std::mutex> g(mu);
-    if (raised.insert({kernel, dev}).second) (void)allow_dynamic_lds(kernel);
-  }
+  (void)allow_dynamic_lds(kernel);  // the 16-wave launch's dynamic LDS is above the default limit
   return tp_geometry_occ(S, islands, occupancy_blocks(kernel, 256, dev::tp_dyn_lds(4, pseg)), ng, pseg);
 }
 
@@ -331,12 +334,16 @@ __global__ __launch_bounds__(kBlock) void prefix_final_kernel(const float* s, ui
   }
 }
 
-// guide[b] = i for every bucket b in (bucket(cumfit[i-1]), bucket(cumfit[i])].
-// Spans of 32 buckets or more (one individual holding >= 32/S of the total
-// weight) are queued in LDS and filled by the whole block, so no thread loops
-// over a heavy individual's buckets.
+// entry[b] = {i, cumfit[i], next, 0} for every bucket b in (bucket(cumfit[i-1]),
+// bucket(cumfit[i])] (GenArgs::roul_guide): next = i + 1 in the last of them
+// when individual i + 1 opens the following bucket (the usual case: the
+// slices are of similar size), else ~0 — the buckets before the last never
+// need it (every target in them is <= cumfit[i]).  Spans of 32 buckets or
+// more (one individual holding >= 32/S of the total weight) are queued in LDS
+// and filled by the whole block, so no thread loops over a heavy
+// individual's buckets.
 __global__ __launch_bounds__(kBlock) void roulette_guide_kernel(const float* c, uint64_t S, const float* meta,
-                                                                 uint32_t* guide) {
+                                                                 uint4* guide) {
   __shared__ uint4 spans[kBlock];
   __shared__ uint32_t nsp;
   const float scale = meta[0];
@@ -345,14 +352,19 @@ __global__ __launch_bounds__(kBlock) void roulette_guide_kernel(const float* c, 
     if (threadIdx.x == 0) nsp = 0;
     __syncthreads();
     const uint64_t i = t0 + threadIdx.x;
+    uint32_t cf = 0;
     if (i < S) {
-      const uint32_t hi = roulette_bucket(c[i], scale, B);
+      const float ci = c[i];
+      cf = __float_as_uint(ci);
+      const uint32_t hi = roulette_bucket(ci, scale, B);
       const uint32_t lo = i ? roulette_bucket(c[i - 1], scale, B) + 1u : 0u;
+      const uint32_t nx = i + 1 < S && roulette_bucket(c[i + 1], scale, B) > hi ? (uint32_t)i + 1u : 0xFFFFFFFFu;
       if (hi >= lo) {
         if (hi - lo < 32u) {
-          for (uint32_t b = lo; b <= hi; ++b) guide[b] = (uint32_t)i;
+          for (uint32_t b = lo; b <= hi; ++b) guide[b] = make_uint4((uint32_t)i, cf, b == hi ? nx : 0xFFFFFFFFu, 0u);
         } else {
-          spans[atomicAdd(&nsp, 1u)] = make_uint4(lo, hi, (uint32_t)i, 0u);
+          spans[atomicAdd(&nsp, 1u)] = make_uint4(lo, hi, (uint32_t)i, cf);
+          guide[hi] = make_uint4((uint32_t)i, cf, nx, 0u);
         }
       }
     }
@@ -360,7 +372,7 @@ __global__ __launch_bounds__(kBlock) void roulette_guide_kernel(const float* c, 
     const uint32_t n = nsp;
     for (uint32_t k = 0; k < n; ++k) {
       const uint4 sp = spans[k];
-      for (uint32_t b = sp.x + threadIdx.x; b <= sp.y; b += kBlock) guide[b] = sp.z;
+      for (uint32_t b = sp.x + threadIdx.x; b < sp.y; b += kBlock) guide[b] = make_uint4(sp.z, sp.w, 0xFFFFFFFFu, 0u);
     }
     __syncthreads();
   }
@@ -702,10 +714,14 @@ __global__ __launch_bounds__(kBlock) void topk_offsets_kernel(uint32_t* cnt, uin
 // order: the strictly-beyond-threshold keys, then the first ties).
 constexpr uint64_t kLbAgg = 1ull << 62, kLbMask31 = 0x7FFFFFFFull;
 
+// G in bin space (bin = key for the largest, R - 1 - key for the smallest)
+// unless grev: then G is a value-order histogram read only (the generation
+// kernel's fused histogram, GenArgs::key_hist), bin b at G[R - 1 - b] for the
+// smallest, and nothing re-zeroes it
 __global__ __launch_bounds__(kBlock) void topk16_select_kernel(const uint16_t* k16, uint64_t S, uint64_t per_block,
                                                                uint32_t R, bool largest, uint32_t k, uint32_t* G,
                                                                uint64_t* status, uint32_t* ctr, uint32_t nblocks,
-                                                               uint32_t* idx_out, TopkMove mv) {
+                                                               uint32_t* idx_out, TopkMove mv, bool fused) {
   __shared__ uint32_t gl[kTopkMaxRange];  // this block's copy of the histogram
   __shared__ uint32_t sel_pos[kTopkMoveSlots], sel_src[kTopkMoveSlots];  // row moves: output position, source
   __shared__ uint32_t sh_T, sh_need, sh_b;
@@ -717,7 +733,7 @@ __global__ __launch_bounds__(kBlock) void topk16_select_kernel(const uint16_t* k
   for (uint32_t j = 0; j < per; ++j) {
     const int64_t b = (int64_t)R - 1 - (int64_t)threadIdx.x * per - j;
     if (b >= 0) {
-      const uint32_t c = G[b];
+      const uint32_t c = G[fused && !largest ? R - 1 - b : b];
       gl[b] = c;  // re-read below by this same thread only
       mine += c;
     }
@@ -782,7 +798,7 @@ __global__ __launch_bounds__(kBlock) void topk16_select_kernel(const uint16_t* k
   pe = block_reduce(pe, lds, add);
   // every other block published its aggregate, hence had read the histogram:
   // the last ticket zeroes it for the next selection
-  if (b == nblocks - 1)
+  if (b == nblocks - 1 && !fused)
     for (uint32_t i = threadIdx.x; i < R; i += kBlock) G[i] = 0;
   uint32_t gpos = pg + og, epos = pe + oe;
   // with a row move, the block's selections are listed in LDS first (slot:
@@ -1123,7 +1139,8 @@ void roulette_prefix_launch(const float* scores, uint64_t S, const float* parts,
 
 void roulette_guide_launch(const float* cumfit, uint64_t S, uint32_t* guide, float* ws, hipStream_t s) {
   const uint32_t grid = launch_grid(S, kBlock);
-  hipLaunchKernelGGL(roulette_guide_kernel, grid, kBlock, 0, s, cumfit, S, (const float*)(ws + kRoulScale), guide);
+  hipLaunchKernelGGL(roulette_guide_kernel, grid, kBlock, 0, s, cumfit, S, (const float*)(ws + kRoulScale),
+                     (uint4*)guide);
   PGA_HIP_CHECK(hipGetLastError());
 }
 
@@ -1180,7 +1197,8 @@ bool topk_move_supported(const uint16_t* keys16, uint32_t key_range, uint64_t S)
 }
 
 void topk_launch(const float* scores, const uint16_t* keys16, uint32_t key_range, uint64_t S, uint32_t k,
-                 bool largest, bool sorted, uint32_t* idx_out, void* ws, hipStream_t s, const TopkMove* mv) {
+                 bool largest, bool sorted, uint32_t* idx_out, void* ws, hipStream_t s, const TopkMove* mv,
+                 const TopkFused* fused) {
   if (k == 0) return;
   if (k > S) throw std::runtime_error("topk: k > S");
   if (mv && (sorted || !topk_move_supported(keys16, key_range, S)))
@@ -1200,11 +1218,21 @@ void topk_launch(const float* scores, const uint16_t* keys16, uint32_t key_range
     const uint32_t cgrid = grid > 1024 ? 1024 : grid;
     const uint64_t per_block = (S + cgrid - 1) / cgrid;
     uint64_t* status = (uint64_t*)cnt;  // cgrid aggregate words, then 2 ticket counters
-    if (S < (1ull << 31)) {  // fused histogram + ticketed select; 4-kernel path beyond
-      hipLaunchKernelGGL(topk16_hist_kernel, grid, kBlock, 4 * R, s, keys16, S, R, largest, G, status, cgrid);
+    if (S < (1ull << 31)) {  // histogram + ticketed select; 4-kernel path beyond
       const uint64_t pb16 = (per_block + 15) / 16 * 16;  // aligned 16-key chunks for every thread
+      if (fused && fused->hist && fused->status) {
+        // the generation kernel's histogram of these keys, its status words
+        // zeroed by that kernel: the select alone (one pass over the keys)
+        uint64_t* fst = (uint64_t*)fused->status;
+        hipLaunchKernelGGL(topk16_select_kernel, cgrid, kBlock, 0, s, keys16, S, pb16, R, largest, k,
+                           const_cast<uint32_t*>(fused->hist), fst, (uint32_t*)(fst + cgrid), cgrid, idx_out,
+                           mv ? *mv : TopkMove{}, true);
+        PGA_HIP_CHECK(hipGetLastError());
+        return;
+      }
+      hipLaunchKernelGGL(topk16_hist_kernel, grid, kBlock, 4 * R, s, keys16, S, R, largest, G, status, cgrid);
       hipLaunchKernelGGL(topk16_select_kernel, cgrid, kBlock, 0, s, keys16, S, pb16, R, largest, k, G, status,
-                         (uint32_t*)(status + cgrid), cgrid, idx_out, mv ? *mv : TopkMove{});
+                         (uint32_t*)(status + cgrid), cgrid, idx_out, mv ? *mv : TopkMove{}, false);
       PGA_HIP_CHECK(hipGetLastError());
       return;
     }

@@ -47,6 +47,8 @@ void check_tensor(const torch::Tensor& t, const Island& isl, torch::ScalarType s
 
 }  // namespace
 
+void bind_comm(py::module& m);  // comm_bind.cpp: the engine's RCCL communicator
+
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "MI355X-native parallel genetic algorithm engine (gfx950 HIP kernels + CPU reference)";
 
@@ -194,6 +196,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def_property_readonly("graph_replays", &Island::graph_replays)
       .def_property_readonly("knapsack_digits", &Island::knapsack_digits)
       .def_property("migration_policy", &Island::migration_policy, &Island::set_migration_policy)
+      .def_property("fused_histogram", &Island::fused_histogram, &Island::set_fused_histogram)
+      .def_property_readonly("fused_histogram_ready", &Island::fused_histogram_ready)
       .def("config", [](Island& i) { return i.config(); })
       .def("set_operators", [](Island& i, const pga::Config& c) { bind_stream(i); i.set_operators(c); })
       .def("set_objective_data",
@@ -319,4 +323,5 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("save", [](Island& i, const std::string& p) { bind_stream(i); i.save(p); })
       .def("load", [](Island& i, const std::string& p) { bind_stream(i); i.load(p); })
       .def("synchronize", [](Island& i) { bind_stream(i); i.synchronize(); });
+  bind_comm(m);
 }

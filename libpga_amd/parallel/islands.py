@@ -101,6 +101,7 @@ class IslandModel:
         timeout_s: Optional[float] = None,
         fault_hook: Optional[Callable[[torch.Tensor, int], bool]] = None,
         policy: str = "topk",
+        transport: str = "auto",
     ):
         if topology not in TOPOLOGIES:
             raise ValueError(f"topology must be one of {TOPOLOGIES}")
@@ -127,6 +128,10 @@ class IslandModel:
             self.k = per * (self.world - 1)
         isl = ga.island
         isl.migration_policy = migration_policy(policy)  # stripe: one pass each way; topk: exact
+        if policy == "topk" and self.world > 1 and self.k > 0 and migrate_every > 0:
+            # exact top-k / bottom-k from the generation kernel's fused key
+            # histogram: no histogram pass per selection (integer objectives)
+            isl.fused_histogram = True
         self.rw = int(isl.row_words)
         dev = isl.rows(0).device
         n = self.k * (self.rw + 1)
@@ -144,6 +149,20 @@ class IslandModel:
         # overlaps the next generation either way.
         use_side = side_stream and dev.type == "cuda" and ga.operators.elitism <= 1
         self._side = torch.cuda.Stream(dev) if use_side else None
+        # transport: "torch" = torch.distributed P2P ops (any backend);
+        # "engine" = the engine's own RCCL communicator (comm_bind.cpp: one
+        # native call packs and posts an epoch, one completes it — a fraction
+        # of batch_isend_irecv's host time); "auto" = engine on GPU islands
+        # of an RCCL process group for the ring / random topologies (no
+        # side stream, fault hook or permutation sanitiser, which need the
+        # python path)
+        if transport not in ("auto", "torch", "engine"):
+            raise ValueError("transport must be 'auto', 'torch' or 'engine'")
+        self._ec = None
+        self._use_engine = transport == "engine" or (
+            transport == "auto" and self.distributed and dev.type == "cuda" and topology in ("ring", "random")
+            and self._side is None and fault_hook is None and ga.problem.encoding != "permutation"
+            and dist.get_backend(group) == "nccl" and os.environ.get("PGA_MIGRATION_TRANSPORT", "") != "torch")
         # test-only fault: post the receive but withhold the matching send, so
         # the exchange can never complete (exercises the deadline + abort path)
         self._withhold_send = False
@@ -176,9 +195,37 @@ class IslandModel:
         return perm[(pos + 1) % w], perm[(pos - 1) % w]
 
     # ----------------------------------------------------------- migration --
+    def _engine(self):
+        """The engine communicator (collective: every rank creates it at the
+        same migration point, or in connect())."""
+        if self._ec is None:
+            from .. import _ext
+
+            C = _ext.load()
+            uid = [C.rccl_unique_id() if self.rank == 0 else None]
+            dist.broadcast_object_list(uid, src=dist.get_global_rank(self.group, 0) if self.group else 0,
+                                       group=self.group)
+            # the process group's own size and rank (tests pretend a peer on a 1-rank group)
+            self._ec = C.EngineComm(dist.get_world_size(self.group), dist.get_rank(self.group), uid[0],
+                                    self.send.device.index)
+        return self._ec
+
     def start_migration(self) -> None:
         """Pack the top-k emigrants and post the exchange (asynchronous)."""
         if self.world == 1 or self.k == 0 or self.degraded:
+            return
+        if self._use_engine and not self._withhold_send:
+            dst, src = self._peers()
+            srows, sscores = self._views(self.send)
+            rrows, rscores = self._views(self.recv)
+            try:
+                self._engine().post(self.ga.island, self.k, srows, sscores, rrows, rscores, dst, src)
+            except Exception as e:  # noqa: BLE001 — any comm failure degrades
+                self._fail(e)
+                return
+            self._pending = "engine"
+            self._epoch += 1
+            self.bytes_sent += self.send.numel() * 4
             return
         if self._side is not None:
             self._side.wait_stream(torch.cuda.current_stream(self._side.device))
@@ -249,6 +296,19 @@ class IslandModel:
     def finish_migration(self) -> None:
         """Wait for the exchange and replace the worst individuals."""
         if self._pending is None:
+            return
+        if isinstance(self._pending, str):  # the engine communicator's epoch
+            self._pending = None
+            t = self.timeout.total_seconds() if self.timeout is not None else 0.0
+            try:
+                ok = self._ec.finish(self.ga.island, self.k, t, self.validate)
+            except Exception as e:  # noqa: BLE001
+                self._fail(e)
+                return
+            if not ok:
+                self._fail(TimeoutError(f"migration epoch {self._epoch} failed or exceeded its deadline"))
+                return
+            self.migrations += 1
             return
         if self._side is not None:
             # the next generation must not overwrite rows the side stream still packs
@@ -346,6 +406,8 @@ class IslandModel:
         connections lazily on the first exchange, so benchmarks call this
         before timing."""
         if self.world > 1 and self.k > 0:
+            if self._use_engine:
+                self._engine()
             self.start_migration()
             self.finish_migration()
 

@@ -51,6 +51,8 @@ class LocalIslands:
         ]
         for ga in self.islands:
             ga.island.migration_policy = migration_policy(policy)
+            if policy == "topk" and n_islands > 1:
+                ga.island.fused_histogram = True  # exact selections without a histogram pass
         self.device = self.islands[0].device
         self.migrate_every = int(migrate_every)
         self.topology = topology

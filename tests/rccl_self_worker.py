@@ -41,13 +41,14 @@ def main(port: int) -> None:
 
     torch.cuda.set_device(0)
     dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
-    for side in (False, True):
-        match(pga, IslandModel, side)
+    for transport, side in (("engine", False), ("torch", False), ("torch", True)):
+        match(pga, IslandModel, side, transport)
     dist.destroy_process_group()
 
 
-def match(pga, IslandModel, side: bool) -> None:
-    a = model(pga, IslandModel, side_stream=side)
+def match(pga, IslandModel, side: bool, transport: str) -> None:
+    a = model(pga, IslandModel, side_stream=side, transport=transport)
+    assert a._use_engine == (transport == "engine")
     a.run(31)
     torch.cuda.synchronize()
 
@@ -62,7 +63,7 @@ def match(pga, IslandModel, side: bool) -> None:
     dist.batch_isend_irecv = fake_batch
     dist.P2POp = lambda op, t, peer, group=None: types.SimpleNamespace(op=op, tensor=t)
     try:
-        b = model(pga, IslandModel, side_stream=side)
+        b = model(pga, IslandModel, side_stream=side, transport="torch")
         b.run(31)
         torch.cuda.synchronize()
     finally:
@@ -72,7 +73,7 @@ def match(pga, IslandModel, side: bool) -> None:
     assert not a.degraded and a.failures == 0
     assert torch.equal(a.ga.rows, b.ga.rows), "RCCL self-exchange diverged from the loopback exchange"
     assert torch.equal(a.ga.scores, b.ga.scores)
-    print("rccl self-exchange ok", "side stream" if side else "compute stream", a.migrations, a.bytes_sent)
+    print("rccl self-exchange ok", transport, "side stream" if side else "compute stream", a.migrations, a.bytes_sent)
 
 
 def withhold(port: int) -> None:
@@ -88,10 +89,14 @@ def withhold(port: int) -> None:
 
     torch.cuda.set_device(0)
     dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
-    m = model(pga, IslandModel, timeout_s=2.0)
+    engine = len(sys.argv) > 3 and sys.argv[3] == "engine"
+    m = model(pga, IslandModel, timeout_s=2.0, transport="engine" if engine else "torch")
+    if engine:  # the engine communicator's own fault injection: the 3rd exchange's sends withheld
+        m._engine().set_fault(3, 3)
     m.run(7)  # epochs at generations 3 and 6 complete
     assert m.migrations == 2 and not m.degraded
-    m._withhold_send = True
+    if not engine:
+        m._withhold_send = True
     t0 = time.monotonic()
     m.run(10)  # epoch at generation 9 times out; generations 9..16 still run
     best = m.ga.best_score()
@@ -99,7 +104,7 @@ def withhold(port: int) -> None:
     assert m.degraded and m.failures == 1 and m.migrations == 2, (m.degraded, m.failures, m.migrations)
     assert m.ga.generation == 17 and best > 0
     assert dt < 30, dt
-    print("rccl withheld send ok", round(dt, 2))
+    print("rccl withheld send ok", "engine" if engine else "torch", round(dt, 2))
     sys.stdout.flush()
     os._exit(0)  # the aborted group is not torn down again
 

@@ -5,6 +5,7 @@ CPU tests drive libpga.so through ctypes on the CPU reference backend
 examples E1/E2/E3 (user __device__ callbacks, linked from libpga.a with
 -fgpu-rdc) and the plain-C headline example."""
 import ctypes as C
+import json
 import os
 import subprocess
 
@@ -286,6 +287,26 @@ def run_ex(args, inp=None, timeout=300):
 def test_example_e1_user_objective():
     rc, out = run_ex([os.path.join(EX, "e1_onemax_float"), "100"])
     assert rc == 0, out
+
+
+@pytest.mark.gpu
+def test_example_e1_fnptr_two_phase_matches_generic():
+    """The reference user model (a __device__ obj_f function pointer) runs on
+    the two-phase kernel at E1's size (test/test.cu:22-43: S = 40,000,
+    L = 100); the generic kernel (forced by a population threshold above S)
+    calls the same function on the same rows, so every score is identical."""
+    def run(extra):
+        env = dict(os.environ, PGA_SEED="77", **extra)
+        r = subprocess.run([os.path.join(EX, "e1_onemax_float"), "30"], capture_output=True, text=True,
+                           timeout=300, env=env)
+        assert r.returncode == 0, r.stdout + r.stderr
+        h = [ln for ln in r.stdout.splitlines() if ln.startswith("E1 scores hash")]
+        t = [json.loads(ln) for ln in r.stdout.splitlines() if ln.startswith("{")]
+        return h[0], t[0]["e1_fnptr_us_per_gen"]
+    h_tp, us_tp = run({})
+    h_gen, us_gen = run({"PGA_TP_MIN_S": "1000000000"})
+    assert h_tp == h_gen
+    print(f"E1 fn-ptr: two-phase {us_tp:.1f} us/gen, generic {us_gen:.1f} us/gen")
 
 
 @pytest.mark.gpu

@@ -116,7 +116,8 @@ def test_rccl_self_exchange_matches_loopback_gpu():
     r = subprocess.run([sys.executable, os.path.join(HERE, "rccl_self_worker.py"), str(free_port())], env=env,
                        capture_output=True, text=True, timeout=110)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
-    assert r.stdout.count("rccl self-exchange ok") == 2  # compute-stream and side-stream emigrant packing
+    # the engine's RCCL communicator, torch P2P ops on the compute stream and on the side stream
+    assert r.stdout.count("rccl self-exchange ok") == 3
 
 
 @pytest.mark.gpu
@@ -129,3 +130,15 @@ def test_rccl_withheld_send_degrades_gpu():
                        env=env, capture_output=True, text=True, timeout=110)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
     assert "rccl withheld send ok" in r.stdout
+
+
+@pytest.mark.gpu
+def test_rccl_engine_withheld_send_degrades_gpu():
+    """The same failure through the engine's own RCCL communicator
+    (comm_bind.cpp): its withheld 3rd exchange expires the deadline, the
+    communicator is aborted, the island runs on degraded."""
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    r = subprocess.run([sys.executable, os.path.join(HERE, "rccl_self_worker.py"), str(free_port()), "withhold",
+                        "engine"], env=env, capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    assert "rccl withheld send ok engine" in r.stdout

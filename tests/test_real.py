@@ -128,8 +128,6 @@ EXACT = {
     "sphere30": lambda: M.Sphere(30),          # GS 8, the Rastrigin-30D geometry
     "rosen30": lambda: M.Rosenbrock(30),       # neighbour gene across lanes
     "sum30": lambda: M.SumGenes(30),
-    "sphere30_rot": lambda: M.Sphere(30, rotate=True, shift=True, seed=2),  # wave-local MFMA rotation
-    "rosen13_rot": lambda: M.Rosenbrock(13, rotate=True, seed=3),          # GS 4 rotation
     "sphere100": lambda: M.Sphere(100),        # GS 32
     "sphere256": lambda: M.Sphere(256),        # GS 64, every lane a chunk
     "sphere3": lambda: M.Sphere(3),            # GS 1
@@ -184,6 +182,34 @@ def test_gpu_tp_bitexact_geometries(name):
     p = EXACT[name]()
     for mut in ("gaussian", "reset_one"):
         _exact_pair(p, 2500, 3, seed=5, elitism=3, crossover="blend", mutation=mut)
+
+
+# rotated objectives through the transposed kernel: the wave's children are
+# rotated by v_mfma_f32_16x16x4f32 (four k per instruction), so scores agree
+# with the CPU's sequential fma chain to float rounding; the rows stay the
+# CPU's except where two contestants' scores lie within that rounding
+ROTATED = {
+    "sphere30_rot": lambda: M.Sphere(30, rotate=True, shift=True, seed=2),      # GS 8: two steps per MFMA batch
+    "rosen13_rot": lambda: M.Rosenbrock(13, rotate=True, seed=3),              # GS 4: one step, neighbour dim
+    "rastrigin30_rot": lambda: M.Rastrigin(30, rotate=True, shift=True, seed=4),  # BASELINE config 3
+    "griewank16_rot": lambda: M.Griewank(16, rotate=True, seed=9),
+}
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", list(ROTATED))
+def test_gpu_tp_rotated_mfma_close(name):
+    p = ROTATED[name]()
+    g = pga.GeneticAlgorithm(p, 2500, seed=5, device="cuda:0", elitism=3, crossover="blend")
+    c = pga.GeneticAlgorithm(p, 2500, seed=5, device="cpu", elitism=3, crossover="blend")
+    for k in range(3):
+        g.run(1)
+        c.run(1)
+        torch.cuda.synchronize()
+        same = (g.rows.cpu() == c.rows).all(-1)
+        assert same.float().mean().item() > 0.99, f"rows diverged after generation {k + 1}"
+        assert close(g.scores.cpu()[same], c.scores[same], rel=1e-5, abs_=1e-4)
+    assert close(p.reference_fitness(g.genomes().cpu()), g.scores.cpu(), rel=1e-4, abs_=1e-3)
 
 
 @pytest.mark.gpu

@@ -36,7 +36,7 @@ KERNELS = ["csrc/kernels/binary.hip", "csrc/kernels/real.hip", "csrc/kernels/per
 HOST = ["csrc/engine/island.cpp", "csrc/engine/trace.cpp", "csrc/engine/jit.cpp", "csrc/cpu/cpu_ops.cpp", "csrc/cpu/cpu_real.cpp", "csrc/cpu/cpu_perm.cpp", "csrc/cpu/parallel.cpp"]
 CAPI = ["csrc/capi/pga_capi.cpp", "csrc/capi/comm.cpp", "csrc/capi/comm_rccl.cpp"]
 COMPAT = []
-BINDINGS = ["csrc/python/bindings.cpp"]
+BINDINGS = ["csrc/python/bindings.cpp", "csrc/python/comm_bind.cpp"]
 
 
 def torch_paths():
@@ -210,9 +210,12 @@ def write_ninja(opt: str, with_torch: bool) -> str:
             lines.append(f"  extra = {tflags} -DTORCH_EXTENSION_NAME=_C -DTORCH_API_INCLUDE_EXTENSION_H "
                          f"-D_GLIBCXX_USE_CXX11_ABI={abi} -Wno-deprecated-declarations")
             bind_objs.append(o)
-        lines.append(f"build libpga_amd/_C.so: link_so {' '.join(core_objs + bind_objs)}")
+        # the engine's RCCL transport (comm_bind.cpp): librccl.so.1 resolves to
+        # the copy torch has already loaded (same soname), one RCCL per process
+        comm_objs = [obj_path(s, "h") for s in ("csrc/capi/comm.cpp", "csrc/capi/comm_rccl.cpp")]
+        lines.append(f"build libpga_amd/_C.so: link_so {' '.join(core_objs + bind_objs + comm_objs)}")
         lines.append(f"  ldflags = -L{lib} -Wl,-rpath,{lib} -lc10 -lc10_hip -ltorch -ltorch_cpu -ltorch_hip "
-                     f"-ltorch_python")
+                     f"-ltorch_python -L/opt/rocm/lib -lrccl")
         defaults.insert(0, "libpga_amd/_C.so")
     lines.append("default " + " ".join(defaults))
     path = os.path.join(BUILD, "build.ninja")
