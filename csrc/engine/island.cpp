@@ -179,7 +179,7 @@ void Island::set_operators(const Config& c) {
     cumfit_ = alloc(4ull * cfg_.S);
     if (on_gpu()) {
       cum_ws_ = alloc(4ull * roulette_workspace_floats(cfg_.S));
-      roul_guide_ = alloc(4ull * roulette_guide_words(cfg_.S));
+      roul_guide_ = alloc(4ull * (cfg_.S + 1));
     }
   }
   if (cfg_.selection == SEL_RANK && !rank_order_.ptr) {
@@ -871,11 +871,14 @@ void Island::immigrate(uint32_t k, const void* in_rows, const float* in_scores) 
     mv.dst_rows = (uint4*)rows_[cur_].ptr;
     mv.dst_scores = (float*)scores_[cur_].ptr;
     mv.dst_keys = k16;
-    topk_launch((const float*)scores_[cur_].ptr, k16, cfg_.L + 1, cfg_.S, k, false, false, nullptr, topk_ws_.ptr,
-                stream, &mv, fsel);
-    // the victims' keys were written with their rows: only the best partials follow
-    n_best_[cur_] = best_of_scores_launch((const float*)scores_[cur_].ptr, cfg_.S,
-                                          (unsigned long long*)best_[cur_].ptr, stream, nullptr);
+    mv.best_parts = (unsigned long long*)best_[cur_].ptr;  // the new per-block bests, from the selection itself
+    const uint32_t nb = topk_launch((const float*)scores_[cur_].ptr, k16, cfg_.L + 1, cfg_.S, k, false, false,
+                                    nullptr, topk_ws_.ptr, stream, &mv, fsel);
+    // the victims' keys were written with their rows; the best partials came
+    // with the selection (else one pass over the scores)
+    n_best_[cur_] = nb ? nb
+                       : best_of_scores_launch((const float*)scores_[cur_].ptr, cfg_.S,
+                                               (unsigned long long*)best_[cur_].ptr, stream, nullptr);
     stats_ok_[cur_] = false;
     return;
   }

@@ -272,13 +272,9 @@ struct GenArgs {
   int32_t selection;
   uint32_t tour_k;
   const float* cumfit;  // roulette: inclusive prefix sums of shifted scores (S)
-  // roulette guide table (util.hip roulette_guide_launch), 4 words per bucket
-  // b: {g = the first individual whose cumfit bucket is >= b, cumfit[g] as
-  // f32 bits, g + 1 when g + 1 is the first individual of bucket b + 1 (else
-  // ~0), 0}, bucket(t) = roulette_bucket(t, *roul_scale, S).  A pick of
-  // target t in bucket b is g when t <= cumfit[g], else g + 1 when the third
-  // word says so (one 16-byte load per pick), else the smallest i > g with
-  // cumfit[i] >= t.  nullptr: binary search only
+  // roulette guide table (util.hip roulette_guide_launch): roul_guide[b] = the
+  // first individual whose cumfit bucket is >= b, bucket(t) =
+  // roulette_bucket(t, *roul_scale, S); nullptr: binary search only
   const uint32_t* roul_guide;
   const float* roul_scale;
   const uint32_t* rank_order;  // rank: individuals by ascending (score_key, index)
@@ -376,8 +372,9 @@ struct GenArgs {
   // generation kernel adds the histogram of the u16 keys it writes (each
   // clamped to hist_bins - 1) to key_hist, which is zero before the launch,
   // and zeroes hist_zero[0, hist_zero_words) — a later generation's buffer
-  // and its selection status words (the Island rotates three buffers).  Exact top-k / bottom-k selections (migration,
-  // elitism, pga_get_best_top) then need no histogram pass over the keys.
+  // and its selection status words (the Island rotates three buffers).
+  // Exact top-k / bottom-k selections (migration, elitism,
+  // pga_get_best_top) then need no histogram pass over the keys.
   uint32_t* key_hist;
   uint32_t* hist_zero;
   uint32_t hist_bins, hist_zero_words;

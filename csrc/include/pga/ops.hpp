@@ -168,8 +168,7 @@ void score_stats_launch(const float* scores, uint64_t S, float* stats, hipStream
 void stats_from_parts_launch(const float* parts, const unsigned long long* best, uint32_t n, uint64_t S, float* out,
                              hipStream_t s);
 // roulette: cumfit = inclusive prefix sum of max(score - min, 0); then the
-// guide table (4 words x (S + 1) buckets, GenArgs::roul_guide) for picks of
-// one 16-byte load (roulette_guide_words).  workspace:
+// guide table guide[0..S] for O(1) picks (GenArgs::roul_guide).  workspace:
 // roulette_workspace_floats(S); its word kRoulScale holds the bucket scale.
 // The minimum comes from the generation kernel's fused {min, sum} partials
 // (parts, nparts blocks) when given, else from a score pass.
@@ -177,7 +176,6 @@ constexpr uint32_t kRoulScale = 4 + 3 * 1024 + 1024;
 size_t roulette_workspace_floats(uint64_t S);
 void roulette_prefix_launch(const float* scores, uint64_t S, const float* parts, uint32_t nparts, float* cumfit,
                             float* workspace, hipStream_t s);
-inline uint64_t roulette_guide_words(uint64_t S) { return 4ull * (S + 1); }
 void roulette_guide_launch(const float* cumfit, uint64_t S, uint32_t* guide, float* workspace, hipStream_t s);
 // stable LSD radix sort (sort.hip: reduce-then-scan, digits of up to 8 bits,
 // count / scan / scatter launches per pass): (keys, vals) by the low `bits`
@@ -213,6 +211,11 @@ struct TopkMove {
   uint4* dst_rows = nullptr;
   float* dst_scores = nullptr;
   uint16_t* dst_keys = nullptr;
+  // SCATTER (integer objectives: key == score): when set, the selection also
+  // writes the population's new per-block packed bests (one per selection
+  // block, topk_launch returns their count): the best survivor of each block
+  // and the immigrants placed in it — no pass over the scores afterwards
+  unsigned long long* best_parts = nullptr;
 };
 bool topk_move_supported(const uint16_t* keys16, uint32_t key_range, uint64_t S);
 // A value histogram of the keys produced by the generation kernel (GenArgs::
@@ -226,9 +229,10 @@ struct TopkFused {
 // words of a fused-histogram buffer: key_range bins + the select kernel's status
 constexpr uint32_t kTopkStatusWords = 2 * 1024 + 4;
 inline uint32_t fused_hist_words(uint32_t key_range) { return (key_range + 3u) / 4u * 4u + kTopkStatusWords; }
-void topk_launch(const float* scores, const uint16_t* keys16, uint32_t key_range, uint64_t S, uint32_t k, bool largest,
-                 bool sorted, uint32_t* idx_out, void* workspace, hipStream_t s, const TopkMove* mv = nullptr,
-                 const TopkFused* fused = nullptr);
+// returns the packed-best partials written (TopkMove::best_parts), else 0
+uint32_t topk_launch(const float* scores, const uint16_t* keys16, uint32_t key_range, uint64_t S, uint32_t k,
+                     bool largest, bool sorted, uint32_t* idx_out, void* workspace, hipStream_t s,
+                     const TopkMove* mv = nullptr, const TopkFused* fused = nullptr);
 // rows: out[i] = rows[idx[i]] (row_words 32-bit words per row), optional scores
 // MIG_STRIPE migration (util.hip): stripe i of k = individuals [i*S/k, (i+1)*S/k).
 // emigrate: the best of every stripe (ties: lowest index) -> out rows/scores[i].

@@ -104,54 +104,49 @@ __device__ __forceinline__ void real_sparse_group(const GenArgs& a, uint64_t chi
 // meta: K (8 bits) | next mutation word j (16 bits) << 8 | xo << 30 | elite << 31
 //
 // ROT (GS 4 or 8, L <= 32): rotated objective f(M (x - o)) on the matrix
-// cores, wave-local: the children of RB = 16 / NG steps (16 rows) are staged
-// in a private 16 x 36 LDS tile and multiplied by M^T with
-// v_mfma_f32_16x16x4f32 (rot_tile16), then scored together.  Round 4 used
-// v_mfma_f32_4x4x1_16b_f32, one k per instruction (the CPU's exact fma
-// chain): 32 dependent MFMAs, 16 LDS tile reads and 4 wave syncs per step.
+// cores, wave-local: the wave's 64/GS children are transposed through a
+// private 16 x 36 LDS tile and multiplied by M^T with v_mfma_f32_4x4x1_16b_f32
+// (rot_tile4: 16 independent 4x4 blocks = 64/GS children x 4 GS dims, no
+// wasted rows), the same k-ordered fma chain as the CPU reference.
 // ---------------------------------------------------------------------------
 constexpr uint32_t kRotTW = 36;  // tile row stride (floats): conflict-free column reads, 16-byte rows
 
-__device__ __forceinline__ void rot_tile_sync() { wave_lds_sync(); }
+__device__ __forceinline__ void rot_tile4_sync() { wave_lds_sync(); }
 
-// this lane's 4 shifted genes (zero past L) -> row `row` of the wave's tile
-__device__ __forceinline__ void rot_stage_row(float* xw, uint32_t row, uint32_t q, const float v[4],
-                                              const float sh[4], uint32_t L) {
-  float z[4];
-#pragma unroll
-  for (uint32_t j = 0; j < 4; ++j) z[j] = 4 * q + j < L ? v[j] - sh[j] : 0.f;
-  *(float4*)(xw + row * kRotTW + 4 * q) = make_float4(z[0], z[1], z[2], z[3]);
-}
-
-// The 16 staged children of the wave's tile (rows = children, DP = 4 GS
-// padded dims) -> rotated in place: Z = X M^T with v_mfma_f32_16x16x4f32,
-// DP / 16 output tiles of 16 dims, DP / 4 k-steps each, the tiles' chains
-// interleaved.  A[i][k] = X[i][k0 + k] and B[k][j] = M[j][k0 + k] from LDS
-// (row stride kRotTW = 36: 2-way bank sharing at most); D lands back in the
-// tile once every A read is done (one wave's LDS operations run in order).
-// k is summed four at a time inside the MFMA, so the rotated scores agree
-// with the CPU reference's sequential fma chain to float rounding.
+// z (4 genes of this lane's chunk, shifted) -> rotated z, in place.  One k
+// per instruction: each output is the same sequential fma chain as the CPU
+// reference.  A = X[child][k] and B = M[n][k] come from LDS as dwordx4 runs
+// of 4 k (xw: this wave's tile, ms: the block's M tile, row stride kRotTW).
 template <int GS>
-__device__ __forceinline__ void rot_tile16(float* xw, const float* ms) {
-  constexpr uint32_t DP = 4 * GS, NT = DP / 16;
+__device__ __forceinline__ void rot_tile4(float* xw, const float* ms, float z[4]) {
+  constexpr int DP = 4 * GS;
   const uint32_t lane = lane_id();
-  const uint32_t r = lane & 15u, kk = lane >> 4;
-  rot_tile_sync();  // every lane's staged row
-  floatx4 acc[NT];
+  const uint32_t row = lane / GS, q = lane % GS;
+  const uint32_t b = lane >> 2, rg = b / GS, cg = b % GS;
+  const uint32_t ca = 4 * rg + (lane & 3);   // A row (child) of this lane
+  const uint32_t nb = 4 * cg + (lane & 3);   // B column (output dim) of this lane
+  *(float4*)(xw + row * kRotTW + 4 * q) = make_float4(z[0], z[1], z[2], z[3]);
+  rot_tile4_sync();
+  floatx4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-  for (uint32_t t = 0; t < NT; ++t) acc[t] = floatx4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-  for (uint32_t k0 = 0; k0 < DP; k0 += 4) {
-    const float xa = xw[r * kRotTW + k0 + kk];
-#pragma unroll
-    for (uint32_t t = 0; t < NT; ++t)
-      acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(xa, ms[(t * 16 + r) * kRotTW + k0 + kk], acc[t], 0, 0, 0);
+  for (int k4 = 0; k4 < DP / 4; ++k4) {
+    const float4 xa = *(const float4*)(xw + ca * kRotTW + 4 * k4);
+    const float4 mb = *(const float4*)(ms + nb * kRotTW + 4 * k4);
+    acc = __builtin_amdgcn_mfma_f32_4x4x1f32(xa.x, mb.x, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_4x4x1f32(xa.y, mb.y, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_4x4x1f32(xa.z, mb.z, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_4x4x1f32(xa.w, mb.w, acc, 0, 0, 0);
   }
+  rot_tile4_sync();
 #pragma unroll
-  for (uint32_t t = 0; t < NT; ++t)
-#pragma unroll
-    for (uint32_t v = 0; v < 4; ++v) xw[(4 * kk + v) * kRotTW + t * 16 + r] = acc[t][v];
-  rot_tile_sync();
+  for (int i = 0; i < 4; ++i) xw[(4 * rg + i) * kRotTW + nb] = acc[i];
+  rot_tile4_sync();
+  const float4 r = *(const float4*)(xw + row * kRotTW + 4 * q);
+  z[0] = r.x;
+  z[1] = r.y;
+  z[2] = r.z;
+  z[3] = r.w;
+  rot_tile4_sync();
 }
 
 // experiment builds only (tools/variants.sh "p0:-DPGA_RTP_PROBE=0" ...): the
@@ -170,7 +165,6 @@ __device__ __forceinline__ void real_gen_tp_body(GenArgs a, unsigned long long* 
   constexpr uint32_t NG = 64 / GS;      // children per wave per step
   constexpr uint32_t PD = tp_prefetch_depth(GS);  // steps of parent rows in flight (tp.hpp)
   constexpr uint32_t PSEG = ROT ? 6 : 7;  // tp_par_cap segments: the rotation tiles take static LDS
-  constexpr uint32_t RB = ROT ? 16 / NG : 1;  // steps per 16-child rotation batch (GS 8: 2, GS 4: 1)
   constexpr bool EVALS = OBJ != OBJ_NONE;
   // JIT (a linked user objective, jitgen_real.hip): the steps also stage
   // their children in the wave's LDS slice; every kJitStageSteps steps one
@@ -436,36 +430,10 @@ __device__ __forceinline__ void real_gen_tp_body(GenArgs a, unsigned long long* 
       lds_stage[(i % kJitStageSteps) * 64u + lane] = make_float4(v[0], v[1], v[2], v[3]);                   \
       if (i % kJitStageSteps == kJitStageSteps - 1u || i + 1u == nst) PGA_RTP_JIT_EVAL                      \
     }                                                                                                       \
-    if constexpr (BUILTIN && ROT) { /* rotated: staged in the wave's tile, scored per 16 children */        \
-      rot_stage_row(xw, i % RB * NG + g, q, v, sh, L);                                                      \
-      if (i % RB == RB - 1u || i + 1u == nst) {                                                             \
-        rot_tile16<GS>(xw, ms);                                                                             \
-        const uint32_t ns_ = i % RB + 1u;                                                                   \
-        _Pragma("unroll") for (uint32_t s_ = 0; s_ < RB; ++s_) {                                            \
-          if (s_ < ns_) {                                                                                   \
-            const uint32_t cs = bs + (i + 1u - ns_ + s_) * NG + g;                                          \
-            const float* zr = xw + (s_ * NG + g) * kRotTW + 4 * q;                                          \
-            RealAcc acc{0.f, 0.f, 1.f};                                                                     \
-            _Pragma("unroll") for (uint32_t j = 0; j < 4; ++j) {                                            \
-              if (j < clen) real_obj_term_w(a, 4 * q + j, zr[j], zr[j + 1], 0.f, w0[j], w1[j], acc);        \
-            }                                                                                               \
-            acc.s0 = group_sum<GS>(acc.s0);                                                                 \
-            acc.s1 = group_sum<GS>(acc.s1);                                                                 \
-            acc.s2 = group_prod<GS>(acc.s2);                                                                \
-            const float sc = real_obj_finish(a, acc);                                                       \
-            RELEM(float, a.score_next, cs) = sc;                                                            \
-            RELEM(uint16_t, a.key_next, cs) = (uint16_t)qkey(sc, qlo, qscale);                              \
-            const unsigned long long pk = cs < S ? pack_best(sc, cs) : 0ull;                                \
-            my_best = pk > my_best ? pk : my_best;                                                          \
-            st.add_if(q == 0u && cs < S, sc);                                                               \
-          }                                                                                                 \
-        }                                                                                                   \
-        rot_tile_sync(); /* the next step rewrites the tile */                                              \
-      }                                                                                                     \
-    }                                                                                                       \
-    if constexpr (BUILTIN && !ROT) {                                                                        \
+    if constexpr (BUILTIN) {                                                                                \
       float z[4], zn[4];                                                                                    \
       _Pragma("unroll") for (uint32_t j = 0; j < 4; ++j) z[j] = 4 * q + j < L ? v[j] - sh[j] : 0.f;         \
+      if constexpr (ROT) rot_tile4<GS>(xw, ms, z);                                                          \
       zn[0] = z[1];                                                                                         \
       zn[1] = z[2];                                                                                         \
       zn[2] = z[3];                                                                                         \

@@ -103,51 +103,34 @@ __device__ __forceinline__ void tp_select_segment(const GenArgs& a, uint32_t beg
   }
   if (roul) {
     // fitness-proportional, by the guide table: the pick is the smallest i
-    // with cumfit[i] >= u * total (roulette_pick's binary search).  One
-    // 16-byte entry of the target's bucket (core.hpp GenArgs::roul_guide)
-    // holds the lower bound g, cumfit[g] and whether g + 1 opens the next
-    // bucket: t <= cumfit[g] -> g, else g + 1 when it does; the rest (rare)
-    // scans on from g + 1.  Round 4 loaded the guide index, THEN cumfit[g]:
-    // two dependent random loads per pick.  The 2 x kSegBatches picks of a
-    // lane advance in lock step.
+    // with cumfit[i] >= u * total (roulette_pick's binary search); the guide
+    // entry of the target's bucket is a lower bound for it, so one guide load,
+    // one cumfit load and (rarely) a short forward scan find it.  The
+    // 2 x kSegBatches picks of a lane advance in lock step.
     constexpr uint32_t NS = 2 * kSegBatches;
     const float total = a.cumfit[S - 1];
     const float scale = *a.roul_scale;
     uint32_t ix[NS];
     float tg[NS];
-    uint4 e[NS];
     #pragma unroll
     for (uint32_t i = 0; i < NS; ++i) {
       const uint32_t w = __builtin_bit_cast(uint32_t, (i & 1u) ? k1[i >> 1] : k0[i >> 1]);
       tg[i] = word_to_unit(w) * total;
-      const uint32_t b = total > 0.f ? roulette_bucket(tg[i], scale, S) : 0u;
-      e[i] = ld32<uint4>(a.roul_guide, b);
-      ix[i] = total > 0.f ? 0u : word_to_index(w, S);
+      ix[i] = total > 0.f ? ld32<uint32_t>(a.roul_guide, roulette_bucket(tg[i], scale, S)) : word_to_index(w, S);
     }
-    bool open[NS];  // still unresolved: scan cumfit from ix
-    bool any_open = false;
+    float v[NS];
     #pragma unroll
-    for (uint32_t i = 0; i < NS; ++i) {
-      const bool in = tg[i] <= __builtin_bit_cast(float, e[i].y);
-      open[i] = total > 0.f && !in && e[i].z != e[i].x + 1u;
-      if (total > 0.f) ix[i] = in ? e[i].x : e[i].x + 1u;
-      any_open |= open[i];
-    }
-    if (__any(any_open)) {  // wave-uniform
-      float v[NS];
+    for (uint32_t i = 0; i < NS; ++i) v[i] = ld32<float>(a.cumfit, ix[i]);
+    for (uint32_t it = 0; it < S; ++it) {  // wave-uniform: until every pick of every lane is resolved
+      bool more = false;
       #pragma unroll
-      for (uint32_t i = 0; i < NS; ++i) v[i] = ld32<float>(a.cumfit, ix[i] < S ? ix[i] : S - 1);
-      for (uint32_t it = 0; it < S; ++it) {  // until every open pick of every lane is resolved
-        bool more = false;
-        #pragma unroll
-        for (uint32_t i = 0; i < NS; ++i) more |= open[i] && v[i] < tg[i];
-        if (!__any(more)) break;
-        #pragma unroll
-        for (uint32_t i = 0; i < NS; ++i) {
-          const bool adv = open[i] && v[i] < tg[i];
-          ix[i] += adv ? 1u : 0u;
-          v[i] = ld32<float>(a.cumfit, ix[i] < S ? ix[i] : S - 1);
-        }
+      for (uint32_t i = 0; i < NS; ++i) more |= total > 0.f && v[i] < tg[i];
+      if (!__any(more)) break;
+      #pragma unroll
+      for (uint32_t i = 0; i < NS; ++i) {
+        const bool adv = total > 0.f && v[i] < tg[i];
+        ix[i] += adv ? 1u : 0u;
+        v[i] = ld32<float>(a.cumfit, ix[i]);
       }
     }
     #pragma unroll

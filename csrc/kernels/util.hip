@@ -334,16 +334,12 @@ __global__ __launch_bounds__(kBlock) void prefix_final_kernel(const float* s, ui
   }
 }
 
-// entry[b] = {i, cumfit[i], next, 0} for every bucket b in (bucket(cumfit[i-1]),
-// bucket(cumfit[i])] (GenArgs::roul_guide): next = i + 1 in the last of them
-// when individual i + 1 opens the following bucket (the usual case: the
-// slices are of similar size), else ~0 — the buckets before the last never
-// need it (every target in them is <= cumfit[i]).  Spans of 32 buckets or
-// more (one individual holding >= 32/S of the total weight) are queued in LDS
-// and filled by the whole block, so no thread loops over a heavy
-// individual's buckets.
+// guide[b] = i for every bucket b in (bucket(cumfit[i-1]), bucket(cumfit[i])].
+// Spans of 32 buckets or more (one individual holding >= 32/S of the total
+// weight) are queued in LDS and filled by the whole block, so no thread loops
+// over a heavy individual's buckets.
 __global__ __launch_bounds__(kBlock) void roulette_guide_kernel(const float* c, uint64_t S, const float* meta,
-                                                                 uint4* guide) {
+                                                                 uint32_t* guide) {
   __shared__ uint4 spans[kBlock];
   __shared__ uint32_t nsp;
   const float scale = meta[0];
@@ -352,19 +348,14 @@ __global__ __launch_bounds__(kBlock) void roulette_guide_kernel(const float* c, 
     if (threadIdx.x == 0) nsp = 0;
     __syncthreads();
     const uint64_t i = t0 + threadIdx.x;
-    uint32_t cf = 0;
     if (i < S) {
-      const float ci = c[i];
-      cf = __float_as_uint(ci);
-      const uint32_t hi = roulette_bucket(ci, scale, B);
+      const uint32_t hi = roulette_bucket(c[i], scale, B);
       const uint32_t lo = i ? roulette_bucket(c[i - 1], scale, B) + 1u : 0u;
-      const uint32_t nx = i + 1 < S && roulette_bucket(c[i + 1], scale, B) > hi ? (uint32_t)i + 1u : 0xFFFFFFFFu;
       if (hi >= lo) {
         if (hi - lo < 32u) {
-          for (uint32_t b = lo; b <= hi; ++b) guide[b] = make_uint4((uint32_t)i, cf, b == hi ? nx : 0xFFFFFFFFu, 0u);
+          for (uint32_t b = lo; b <= hi; ++b) guide[b] = (uint32_t)i;
         } else {
-          spans[atomicAdd(&nsp, 1u)] = make_uint4(lo, hi, (uint32_t)i, cf);
-          guide[hi] = make_uint4((uint32_t)i, cf, nx, 0u);
+          spans[atomicAdd(&nsp, 1u)] = make_uint4(lo, hi, (uint32_t)i, 0u);
         }
       }
     }
@@ -372,7 +363,7 @@ __global__ __launch_bounds__(kBlock) void roulette_guide_kernel(const float* c, 
     const uint32_t n = nsp;
     for (uint32_t k = 0; k < n; ++k) {
       const uint4 sp = spans[k];
-      for (uint32_t b = sp.x + threadIdx.x; b < sp.y; b += kBlock) guide[b] = make_uint4(sp.z, sp.w, 0xFFFFFFFFu, 0u);
+      for (uint32_t b = sp.x + threadIdx.x; b <= sp.y; b += kBlock) guide[b] = sp.z;
     }
     __syncthreads();
   }
@@ -806,6 +797,10 @@ __global__ __launch_bounds__(kBlock) void topk16_select_kernel(const uint16_t* k
   // afterwards, 16 bytes per lane, rows contiguous: one thread per row was
   // 3x slower than the separate gather / scatter kernels
   const bool move = mv.mode != TopkMove::NONE;
+  // SCATTER with best_parts: the best survivor (max key, lowest index: the
+  // pack_best order, key == score) and the best immigrant placed here
+  const bool bests = mv.mode == TopkMove::SCATTER && mv.best_parts != nullptr;
+  unsigned long long keep_best = 0, imm_best = 0;
   uint32_t lg = og, le = bg + oe;
   for (uint64_t c0 = t0; c0 < t1; c0 += 16) {
     uint32_t kv[16];
@@ -827,6 +822,15 @@ __global__ __launch_bounds__(kBlock) void topk16_select_kernel(const uint16_t* k
         ++epos;
         ++le;
       }
+      if (bests) {
+        if (pos == 0xFFFFFFFFu) {
+          const unsigned long long kb = ((unsigned long long)min(kv[e], R - 1) << 32) | (0xFFFFFFFFull - (uint32_t)(c0 + e));
+          keep_best = kb > keep_best ? kb : keep_best;
+        } else {
+          const unsigned long long ib = pack_best(mv.src_scores[pos], c0 + e);
+          imm_best = ib > imm_best ? ib : imm_best;
+        }
+      }
       if (pos == 0xFFFFFFFFu) continue;
       if (idx_out) idx_out[pos] = (uint32_t)(c0 + e);
       if (move && slot < kTopkMoveSlots) {
@@ -835,6 +839,20 @@ __global__ __launch_bounds__(kBlock) void topk16_select_kernel(const uint16_t* k
       } else if (move) {
         topk_emit(mv, nullptr, pos, c0 + e);  // beyond the LDS list (huge blocks): per thread
       }
+    }
+  }
+  if (bests) {  // block-uniform: the block's new packed best
+    __shared__ unsigned long long red[kBlock / 64];
+    const unsigned long long kb = block_max_u64(keep_best, red);
+    const unsigned long long ib = block_max_u64(imm_best, red);
+    if (threadIdx.x == 0) {
+      unsigned long long pb = ib;
+      if (kb) {  // the survivor's own score (key == score for the integer objectives)
+        const uint64_t i = 0xFFFFFFFFull - (uint32_t)kb;
+        const unsigned long long sb = pack_best(mv.dst_scores[i], i);
+        pb = sb > pb ? sb : pb;
+      }
+      mv.best_parts[b] = pb;
     }
   }
   if (!move) return;
@@ -1139,8 +1157,7 @@ void roulette_prefix_launch(const float* scores, uint64_t S, const float* parts,
 
 void roulette_guide_launch(const float* cumfit, uint64_t S, uint32_t* guide, float* ws, hipStream_t s) {
   const uint32_t grid = launch_grid(S, kBlock);
-  hipLaunchKernelGGL(roulette_guide_kernel, grid, kBlock, 0, s, cumfit, S, (const float*)(ws + kRoulScale),
-                     (uint4*)guide);
+  hipLaunchKernelGGL(roulette_guide_kernel, grid, kBlock, 0, s, cumfit, S, (const float*)(ws + kRoulScale), guide);
   PGA_HIP_CHECK(hipGetLastError());
 }
 
@@ -1196,10 +1213,10 @@ bool topk_move_supported(const uint16_t* keys16, uint32_t key_range, uint64_t S)
   return keys16 && key_range >= 2 && key_range <= kTopkMaxRange && S < (1ull << 31);
 }
 
-void topk_launch(const float* scores, const uint16_t* keys16, uint32_t key_range, uint64_t S, uint32_t k,
-                 bool largest, bool sorted, uint32_t* idx_out, void* ws, hipStream_t s, const TopkMove* mv,
-                 const TopkFused* fused) {
-  if (k == 0) return;
+uint32_t topk_launch(const float* scores, const uint16_t* keys16, uint32_t key_range, uint64_t S, uint32_t k,
+                     bool largest, bool sorted, uint32_t* idx_out, void* ws, hipStream_t s, const TopkMove* mv,
+                     const TopkFused* fused) {
+  if (k == 0) return 0;
   if (k > S) throw std::runtime_error("topk: k > S");
   if (mv && (sorted || !topk_move_supported(keys16, key_range, S)))
     throw std::invalid_argument("topk: fused row moves need the u16-key selection-order path");
@@ -1228,13 +1245,13 @@ void topk_launch(const float* scores, const uint16_t* keys16, uint32_t key_range
                            const_cast<uint32_t*>(fused->hist), fst, (uint32_t*)(fst + cgrid), cgrid, idx_out,
                            mv ? *mv : TopkMove{}, true);
         PGA_HIP_CHECK(hipGetLastError());
-        return;
+        return mv && mv->mode == TopkMove::SCATTER && mv->best_parts ? cgrid : 0u;
       }
       hipLaunchKernelGGL(topk16_hist_kernel, grid, kBlock, 4 * R, s, keys16, S, R, largest, G, status, cgrid);
       hipLaunchKernelGGL(topk16_select_kernel, cgrid, kBlock, 0, s, keys16, S, pb16, R, largest, k, G, status,
                          (uint32_t*)(status + cgrid), cgrid, idx_out, mv ? *mv : TopkMove{}, false);
       PGA_HIP_CHECK(hipGetLastError());
-      return;
+      return mv && mv->mode == TopkMove::SCATTER && mv->best_parts ? cgrid : 0u;
     }
     hipLaunchKernelGGL(topk16_hist_kernel, grid, kBlock, 4 * R, s, keys16, S, R, largest, G, (uint64_t*)nullptr, 0u);
     hipLaunchKernelGGL(topk16_count_kernel, cgrid, kBlock, 0, s, keys16, S, per_block, R, largest, k, G, st, cnt);
@@ -1242,12 +1259,13 @@ void topk_launch(const float* scores, const uint16_t* keys16, uint32_t key_range
     hipLaunchKernelGGL(topk_write_kernel<16>, cgrid, kBlock, 0, s, TopkKeys<16>{scores, keys16, largest, R - 1}, S,
                        per_block, st, cnt, cgrid, (uint32_t*)nullptr, idx_out);
     PGA_HIP_CHECK(hipGetLastError());
-    return;
+    return 0;
   }
   if (keys16)
     topk_run<16>(TopkKeys<16>{scores, keys16, largest}, S, k, sorted, idx_out, ws, s);
   else
     topk_run<32>(TopkKeys<32>{scores, keys16, largest}, S, k, sorted, idx_out, ws, s);
+  return 0;
 }
 
 void gather_rows_launch(const void* rows, const float* scores, uint32_t row_words, const uint32_t* idx, uint32_t n,

@@ -137,6 +137,10 @@ class IslandModel:
         n = self.k * (self.rw + 1)
         self.send = torch.empty(n, dtype=torch.int32, device=dev)
         self.recv = torch.empty(n, dtype=torch.int32, device=dev)
+        # the (rows, scores) views of both buffers, made once: a view costs
+        # microseconds of host time, and an epoch's host path is short
+        self._send_views = self._views(self.send)
+        self._recv_views = self._views(self.recv)
         self._pending = None
         # side_stream=True runs emigrant selection + packing on a side stream,
         # concurrently with the next generation kernel (they only read the
@@ -216,10 +220,8 @@ class IslandModel:
             return
         if self._use_engine and not self._withhold_send:
             dst, src = self._peers()
-            srows, sscores = self._views(self.send)
-            rrows, rscores = self._views(self.recv)
             try:
-                self._engine().post(self.ga.island, self.k, srows, sscores, rrows, rscores, dst, src)
+                self._engine().post(self.ga.island, self.k, *self._send_views, *self._recv_views, dst, src)
             except Exception as e:  # noqa: BLE001 — any comm failure degrades
                 self._fail(e)
                 return

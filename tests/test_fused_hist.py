@@ -100,3 +100,28 @@ def test_fused_histogram_local_islands_migration():
         res.append([ga.rows.cpu() for ga in li.islands])
     for a, b in zip(*res):
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("L,gens", [(1024, 3), (64, 150)])
+def test_immigrate_best_partials_exact(L, gens):
+    """The bottom-k selection writes the population's new per-block packed
+    bests itself (no pass over the scores): best() is the max score at its
+    lowest index, also in a converged population where the victims are ties
+    of the best score (L = 64 after 150 generations)."""
+    S, k = 65536, 1311
+    ga = _ga(S, L=L, seed=12)
+    ga.run(gens)
+    isl = ga.island
+    rw = int(isl.row_words)
+    rows = torch.empty(k * rw, dtype=torch.int32, device=DEV)
+    sc = torch.empty(k, dtype=torch.float32, device=DEV)
+    isl.emigrate(k, rows, sc)
+    ga.run(1)
+    isl.evaluate_rows(rows, sc)
+    isl.immigrate(k, rows, sc)
+    torch.cuda.synchronize()
+    s = ga.scores.cpu()
+    best, idx = isl.best()
+    assert best == s.max().item()
+    assert idx == int(torch.nonzero(s == s.max())[0])
+    assert torch.equal(ga.problem.reference_fitness(ga.genomes().cpu()), s)

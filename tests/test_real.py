@@ -126,6 +126,8 @@ def test_gpu_matches_cpu(name):
 # scores equal the CPU backend's bit for bit, generation after generation
 EXACT = {
     "sphere30": lambda: M.Sphere(30),          # GS 8, the Rastrigin-30D geometry
+    "sphere30_rot": lambda: M.Sphere(30, rotate=True, shift=True, seed=2),  # wave-local MFMA rotation
+    "rosen13_rot": lambda: M.Rosenbrock(13, rotate=True, seed=3),          # GS 4 rotation
     "rosen30": lambda: M.Rosenbrock(30),       # neighbour gene across lanes
     "sum30": lambda: M.SumGenes(30),
     "sphere100": lambda: M.Sphere(100),        # GS 32
@@ -184,13 +186,11 @@ def test_gpu_tp_bitexact_geometries(name):
         _exact_pair(p, 2500, 3, seed=5, elitism=3, crossover="blend", mutation=mut)
 
 
-# rotated objectives through the transposed kernel: the wave's children are
-# rotated by v_mfma_f32_16x16x4f32 (four k per instruction), so scores agree
-# with the CPU's sequential fma chain to float rounding; the rows stay the
-# CPU's except where two contestants' scores lie within that rounding
+# rotated objectives with transcendental terms through the transposed kernel:
+# the rotation is the CPU's fma chain bit for bit, the cos / exp terms agree to
+# float rounding, so the rows stay the CPU's except where two contestants'
+# scores lie within that rounding
 ROTATED = {
-    "sphere30_rot": lambda: M.Sphere(30, rotate=True, shift=True, seed=2),      # GS 8: two steps per MFMA batch
-    "rosen13_rot": lambda: M.Rosenbrock(13, rotate=True, seed=3),              # GS 4: one step, neighbour dim
     "rastrigin30_rot": lambda: M.Rastrigin(30, rotate=True, shift=True, seed=4),  # BASELINE config 3
     "griewank16_rot": lambda: M.Griewank(16, rotate=True, seed=9),
 }
