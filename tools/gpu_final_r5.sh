@@ -8,6 +8,8 @@ set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd "$R"; export TMPDIR=/tmp
 O=$R/gpurun_out/final5; mkdir -p $O
+PART=${PART:-a}   # a: tests, bench, configs, islands; b: E1 fn-ptr, migration, host probe, kernel traces
+if [ "$PART" = a ]; then
 timeout -k 10 300 python -u __graft_entry__.py smoke > $O/smoke.log 2>&1 || { cat $O/smoke.log; exit 1; }
 tail -1 $O/smoke.log
 timeout -k 10 1000 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/pytest.log 2>&1 || { tail -30 $O/pytest.log; exit 1; }
@@ -22,6 +24,8 @@ for p in onemax rastrigin30 tsp128; do
   timeout -k 10 200 python bench/bench_islands.py --problem $p >> $O/islands.jsonl 2>> $O/islands.err || { tail -20 $O/islands.err; exit 1; }
 done
 echo islands done
+exit 0
+fi
 timeout -k 5 60 build/examples/e1_onemax_float 200 > $O/e1_fnptr.log 2>&1 || { cat $O/e1_fnptr.log; exit 1; }
 head -1 $O/e1_fnptr.log
 PGA_OUT=$O/mig_epoch.json timeout -k 10 200 python bench/migration_cost.py > $O/mig_epoch.log 2>&1 || { tail -20 $O/mig_epoch.log; exit 1; }
