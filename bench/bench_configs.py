@@ -8,7 +8,8 @@ Configs (BASELINE.md "Targets" table):
   onemax1024        OneMax 1024-bit, pop=1M, one GPU (the headline island)
   rastrigin30       Rastrigin-30D float, pop=1M (blend + gaussian)
   rastrigin30_rot   Rastrigin-30D rotated, pop=1M (fitness through MFMA tiles)
-  tsp256_ox / _pmx  TSP-256 permutation, pop=256K, OX / PMX crossover (distance matrix)
+  tsp256_ox / _pmx  TSP-256 permutation, pop=256K, OX / PMX crossover (symmetric f32 distance matrix)
+  tsp256_asym_*     the same with an asymmetric f32 matrix (L2-gathered)
   tsp256_euc_*      the same instance as city coordinates (TSPEuclidean)
   tsp256_int_*      an integer EUC_2D matrix (u16 copy in LDS)
   e1_sum100_refops  reference example E1 (S=40000, L=100) with the reference's
@@ -83,7 +84,21 @@ def make(name: str):
     if name in ("tsp256_ox", "tsp256_pmx"):
         g = torch.Generator().manual_seed(7)
         xy = torch.rand(256, 2, generator=g)
-        d = torch.cdist(xy, xy)
+        # the exact pairwise distances (no matmul expansion: through it cdist
+        # returns a matrix that is not symmetric bit for bit and has a
+        # non-zero diagonal, up to 5e-4); a symmetric float matrix is staged
+        # in LDS as its f32 triangle (perm.hip TBL 3), an asymmetric one is
+        # gathered from L2 (tsp256_asym_* below)
+        d = torch.cdist(xy, xy, compute_mode="donot_use_mm_for_euclid_dist")
+        xo = "ox" if name.endswith("ox") else "pmx"
+        return M.TSP(d), 1 << 18, None, dict(elitism=1, crossover=xo), 50
+    if name in ("tsp256_asym_ox", "tsp256_asym_pmx"):
+        # an asymmetric float matrix (each direction of an edge scaled apart):
+        # the f32 L2 gather path of the kernel
+        g = torch.Generator().manual_seed(7)
+        xy = torch.rand(256, 2, generator=g)
+        d = torch.cdist(xy, xy, compute_mode="donot_use_mm_for_euclid_dist")
+        d = d * (1 + 0.1 * torch.rand(256, 256, generator=g))
         xo = "ox" if name.endswith("ox") else "pmx"
         return M.TSP(d), 1 << 18, None, dict(elitism=1, crossover=xo), 50
     if name == "maxcut512_qubo":
@@ -105,7 +120,7 @@ def make(name: str):
 
 
 NAMES = ["onemax64_cpu", "onemax1024", "rastrigin30", "rastrigin30_rot", "tsp256_ox", "tsp256_pmx", "tsp256_int_ox",
-         "tsp256_int_pmx", "e1_sum100_refops",
+         "tsp256_int_pmx", "tsp256_asym_ox", "tsp256_asym_pmx", "e1_sum100_refops",
          "tsp256_euc_ox", "tsp256_euc_pmx", "e2_knap_refops", "onemax64_gpu", "onemax1024_jit", "rastrigin30_jit", "maxcut512_qubo",
          "qubo1024", "onemax1024_rank", "knapsack1024", "onemax1024_roulette_2pt"]
 

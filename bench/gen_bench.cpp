@@ -2,14 +2,17 @@
 //
 //   gen_bench [--pop N] [--length L] [--gens G] [--warmup W] [--xo uniform|one|two]
 //             [--elitism E] [--encoding binary|real|perm] [--objective N]
+//             [--tsp f32|int|euc] [--pmx 1]
 // Prints one JSON line: us per generation measured with hipEvents around G
 // back-to-back fused generations on the null stream.
 #include <hip/hip_runtime.h>
 
+#include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <vector>
 
 #include "pga/island.hpp"
 #include "pga/ops.hpp"
@@ -26,6 +29,7 @@ int main(int argc, char** argv) {
   c.n_elite = 1;
   c.seed = 1234;
   int gens = 300, warm = 30;
+  std::string tsp;  // PERMUTATION: the bench_configs.py TSP-256 instance kinds
   for (int i = 1; i + 1 < argc; i += 2) {
     std::string k = argv[i], v = argv[i + 1];
     if (k == "--pop") c.S = std::strtoull(v.c_str(), nullptr, 10);
@@ -61,8 +65,31 @@ int main(int argc, char** argv) {
     else if (k == "--xo") c.crossover = v == "uniform" ? pga::XO_UNIFORM : c.crossover;
     else if (k == "--lo") c.lo = std::strtof(v.c_str(), nullptr);
     else if (k == "--hi") c.hi = std::strtof(v.c_str(), nullptr);
+    else if (k == "--pmx") c.crossover = v == "1" ? pga::XO_PMX : pga::XO_OX;
+    else if (k == "--tsp") tsp = v;
   }
+  if (!tsp.empty()) c.objective = tsp == "euc" ? pga::OBJ_TSP_EUC : pga::OBJ_TSP;
   pga::Island isl(c, 0);
+  if (!tsp.empty()) {  // uniform random cities in the unit square (fixed LCG)
+    std::vector<float> xy(2 * c.L), d;
+    uint64_t st = 7;
+    for (auto& x : xy) {
+      st = st * 6364136223846793005ull + 1442695040888963407ull;
+      x = (float)((st >> 40) * (1.0 / 16777216.0));
+    }
+    if (tsp == "euc") {
+      d = xy;
+    } else {
+      d.resize((size_t)c.L * c.L);
+      for (uint32_t i = 0; i < c.L; ++i)
+        for (uint32_t j = 0; j < c.L; ++j) {
+          const float dx = xy[2 * i] - xy[2 * j], dy = xy[2 * i + 1] - xy[2 * j + 1];
+          const float e = std::sqrt(dx * dx + dy * dy);
+          d[(size_t)i * c.L + j] = tsp == "int" ? std::nearbyint(1000.f * e) : e;
+        }
+    }
+    isl.set_objective_data(d.data(), d.size(), 0);
+  }
   isl.initialize();
   isl.run(warm);
   PGA_HIP_CHECK(hipDeviceSynchronize());

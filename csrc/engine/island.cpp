@@ -226,35 +226,51 @@ void Island::prepare_objective() {
   }
   if ((cfg_.objective == OBJ_TSP || cfg_.objective == OBJ_TSP_OPEN) && cfg_.encoding == ENC_PERMUTATION && on_gpu() &&
       aux_version_ != obj_version_) {
-    // an integer matrix (entries in [0, 65535]) as u16 for the LDS-resident
-    // tour evaluation (perm.hip perm_gen_fast TBL): the strict lower triangle
-    // plus the diagonal when symmetric, else the full matrix
+    // the matrix for the LDS-resident tour evaluation (perm.hip perm_gen_fast
+    // TBL): an integer matrix (entries in [0, 65535]) as u16 — the strict
+    // lower triangle plus the diagonal when symmetric (kind 1), else the full
+    // matrix (kind 2); any other symmetric matrix as the f32 triangle plus
+    // diagonal (kind 3); an asymmetric float matrix stays in L2 (kind 0)
     aux_version_ = obj_version_;
     aux_kind_ = aux_bytes_ = 0;
     const uint32_t L = cfg_.L;
     const float* d = obj_host0_.data();
-    bool ok = obj_host0_.size() >= (size_t)L * L && L >= 2, sym = ok;
-    for (size_t i = 0; ok && i < (size_t)L * L; ++i) ok = d[i] >= 0.f && d[i] <= 65535.f && d[i] == std::floor(d[i]);
-    for (uint32_t i = 0; ok && sym && i < L; ++i)
-      for (uint32_t j = 0; sym && j < i; ++j) sym = d[(size_t)i * L + j] == d[(size_t)j * L + i];
-    if (ok) {
-      std::vector<uint16_t> t;
-      if (sym) {
-        t.reserve((size_t)L * (L + 1) / 2 + 8);
-        for (uint32_t i = 1; i < L; ++i)
-          for (uint32_t j = 0; j < i; ++j) t.push_back((uint16_t)d[(size_t)i * L + j]);
-        for (uint32_t i = 0; i < L; ++i) t.push_back((uint16_t)d[(size_t)i * L + i]);
-      } else {
-        for (size_t i = 0; i < (size_t)L * L; ++i) t.push_back((uint16_t)d[i]);
-      }
-      t.resize((t.size() + 7) / 8 * 8, 0);  // whole 16-byte stores
-      if (obj_aux_.bytes < 2 * t.size()) {
+    // (only what can fit one CU's LDS: 160 KiB)
+    const size_t tri = (size_t)L * (L + 1) / 2, lds = 160 * 1024;
+    const bool have = obj_host0_.size() >= (size_t)L * L && L >= 2 && 2 * tri <= lds;
+    bool ints = have, sym = have;
+    for (size_t i = 0; ints && i < (size_t)L * L; ++i) ints = d[i] >= 0.f && d[i] <= 65535.f && d[i] == std::floor(d[i]);
+    for (uint32_t i = 0; sym && i < L; ++i)
+      for (uint32_t j = 0; sym && j < i; ++j)
+        sym = std::memcmp(&d[(size_t)i * L + j], &d[(size_t)j * L + i], sizeof(float)) == 0;
+    std::vector<uint8_t> t;
+    auto put = [&t](const auto v) {
+      const size_t o = t.size();
+      t.resize(o + sizeof(v));
+      std::memcpy(t.data() + o, &v, sizeof(v));
+    };
+    if (ints && sym) {
+      for (uint32_t i = 1; i < L; ++i)
+        for (uint32_t j = 0; j < i; ++j) put((uint16_t)d[(size_t)i * L + j]);
+      for (uint32_t i = 0; i < L; ++i) put((uint16_t)d[(size_t)i * L + i]);
+      aux_kind_ = 1;
+    } else if (ints && 2ull * L * L <= lds) {
+      for (size_t i = 0; i < (size_t)L * L; ++i) put((uint16_t)d[i]);
+      aux_kind_ = 2;
+    } else if (sym && !ints && 4 * tri <= lds) {
+      for (uint32_t i = 1; i < L; ++i)
+        for (uint32_t j = 0; j < i; ++j) put(d[(size_t)i * L + j]);
+      for (uint32_t i = 0; i < L; ++i) put(d[(size_t)i * L + i]);
+      aux_kind_ = 3;
+    }
+    if (aux_kind_) {
+      t.resize((t.size() + 15) / 16 * 16, 0);  // whole 16-byte stores
+      if (obj_aux_.bytes < t.size()) {
         release(obj_aux_);
-        obj_aux_ = alloc(2 * t.size());
+        obj_aux_ = alloc(t.size());
       }
-      copy_to_device(obj_aux_.ptr, t.data(), 2 * t.size());
-      aux_kind_ = sym ? 1u : 2u;
-      aux_bytes_ = (uint32_t)(2 * t.size());
+      copy_to_device(obj_aux_.ptr, t.data(), t.size());
+      aux_bytes_ = (uint32_t)t.size();
     }
   }
   if (cfg_.objective != OBJ_QUBO) return;

@@ -273,9 +273,10 @@ __device__ __forceinline__ void resolve_gen(GenArgs& a) {
   if (a.gen_dev) a.key.gen = *a.gen_dev + a.gen_off;
 }
 
-// Pick two parents.  All selection words are group-uniform.
-template <int GS>
-__device__ __forceinline__ void select_parents(const GenArgs& a, const Pool<GS>& pool, uint64_t child,
+// Pick two parents.  All selection words are group-uniform.  P: the group's
+// Pool, or any view with the same get() (perm.hip LanePool: one lane's child)
+template <int GS, typename P = Pool<GS>>
+__device__ __forceinline__ void select_parents(const GenArgs& a, const P& pool, uint64_t child,
                                                uint32_t& pa, uint32_t& pb) {
   const uint32_t S = (uint32_t)a.S;
   if (a.selection == SEL_TOURNAMENT) {

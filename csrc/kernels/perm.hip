@@ -19,6 +19,7 @@
 // BASELINE config 5.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
 #include <string>
 
 #include "pga/device.hpp"
@@ -30,6 +31,23 @@ namespace {
 
 using namespace dev;
 constexpr uint16_t kNone = 0xFFFF;
+// experiment builds only (tools/variants.sh): tournaments, crossover or the
+// tour evaluation switched off in perm_gen_fast, to split its time
+#ifndef PGA_PERM_NOSEL
+#define PGA_PERM_NOSEL 0
+#endif
+#ifndef PGA_PERM_NOXO
+#define PGA_PERM_NOXO 0
+#endif
+#ifndef PGA_PERM_CHAIN  // PMX chains: 0 first links batched, 3 one gene after another, 1/2 a lane's 8 together
+#define PGA_PERM_CHAIN 0
+#endif
+#ifndef PGA_PERM_PF  // parent rows one step ahead
+#define PGA_PERM_PF 1
+#endif
+#ifndef PGA_PERM_NOEVAL
+#define PGA_PERM_NOEVAL 0
+#endif
 constexpr uint32_t kHdrF = 144;  // floats: red u64[4] (8 floats) | elite | pad  (16-aligned)
 
 inline uint32_t perm_max_length(bool euc) {  // longest genome the one-individual-per-block kernel holds in LDS
@@ -280,13 +298,23 @@ __global__ __launch_bounds__(BLK) void perm_kernel(GenArgs a, unsigned long long
 
 // ---------------------------------------------------------------------------
 // Fast GEN path for rows of at most 64 chunks (L <= 512 cities): one chunk per
-// lane, so a child never leaves its wave.  Everything a child needs from LDS
-// (parent B for PMX chains, the city -> position map, the OX scatter target)
-// is exchanged inside the wave with wave-level barriers instead of
-// __syncthreads: the four waves of a block drift independently and hide each
-// other's latency.  Parent chunks, the child chunk and the tour edges live in
-// registers (one dwordx4 per row per lane; the edge to the next lane's first
-// city is a shuffle).  Same operator semantics as perm_kernel (bit-exact).
+// lane, so a child never leaves its wave.  Two phases per BATCH of 64
+// consecutive children (a wave's unit of work, wave-strided over the grid):
+//   SELECT  one lane per child: the child's selection words (its ST_CHILD
+//           Philox blocks, the words select_parents reads from the group's
+//           pool) and every score load of the 64 tournaments in flight at once;
+//           the parents stay in two VGPRs (lane j: child j of the batch)
+//   BREED   NG = 64 / GS children per step, one chunk per lane; the parent
+//           rows of step t + 1 are loaded before step t's crossover, so a
+//           step waits for no load of its own
+// (before round 5 every step drew its selection words, waited for its four
+// scores, then for its rows: tournaments measured 92 of 273 us per
+// generation at TSP-256 OX).  Everything a child needs from LDS (the PMX
+// mapping, the OX membership bits and scatter target) is exchanged inside the
+// wave with wave-level barriers instead of __syncthreads.  Parent chunks, the
+// child chunk and the tour edges live in registers (one dwordx4 per row per
+// lane; the edge to the next lane's first city is a shuffle).  Same operator
+// semantics as perm_kernel (bit-exact).
 __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
@@ -307,12 +335,35 @@ __device__ __forceinline__ uint4 set16(uint4 v, uint32_t e, uint32_t x) {
   return v;
 }
 
-// TBL (integer distance matrices, the launcher's choice): the matrix as u16
-// in LDS (GenArgs::obj_aux, staged once per block) instead of an f32 L2
-// gather per edge — 1 = a symmetric matrix's strict lower triangle plus its
-// diagonal (65 KB at L = 256, so 1024-thread blocks still fit: 16 waves share
-// one table per CU), 2 = the full matrix.  Entries are exact (u16 -> f32),
-// so the tour sums equal the f32-matrix kernel's bit for bit.
+// One lane's view of its own child's ST_CHILD words (the pool's words, core.hpp
+// child_word): blocks 1 and 2 hold the selection words W_SEL .. W_SEL + 3 of
+// tournament-2, roulette and uniform selection; other words are drawn on demand
+template <int GS>
+struct LanePool {
+  u32x4 b1, b2;
+  __device__ __forceinline__ uint32_t get(uint32_t t, const RngKey& key, uint64_t child) const {
+    if (t / 3u == 1u) return sel3(b1, t % 3u);
+    if (t / 3u == 2u) return sel3(b2, t % 3u);
+    return child_word(key, child, t);
+  }
+};
+
+// Per-group LDS of the fast kernel: one lp-gene u16 array (PMX: the mapping
+// T, then the child for mutation; OX: the scatter target) and 64 bytes of OX
+// membership bits (one per city) — a quarter of perm_kernel's four arrays,
+// so a 16-wave block keeps its 32 groups beside a 131.6 KB f32 triangle
+__host__ __device__ inline size_t perm_fast_group_bytes(uint32_t chunks) { return 16ull * chunks + 64; }
+__host__ __device__ inline size_t perm_fast_lds_bytes(uint32_t GS, uint32_t chunks, bool euc, uint32_t blk) {
+  return 4ull * kHdrF + (euc ? 8ull * chunks * 8 : 0) + (size_t)(blk / GS) * perm_fast_group_bytes(chunks);
+}
+
+// TBL (the launcher's choice from GenArgs::obj_aux): the distance matrix in
+// LDS (staged once per block) instead of an f32 L2 gather per edge — 1 = a
+// symmetric integer matrix's strict lower triangle plus its diagonal as u16
+// (65 KB at L = 256), 2 = a full integer matrix as u16, 3 = a symmetric f32
+// matrix's triangle plus diagonal as f32 (131.6 KB at L = 256: the 16 waves
+// of a CU share one).  Entries are the matrix's own values, so the tour sums
+// equal the f32 L2 path's bit for bit.
 template <int GS, int OBJ, int TBL = 0>
 __device__ __forceinline__ void perm_gen_fast_body(GenArgs a, unsigned long long* best_parts) {
   resolve_gen(a);
@@ -321,20 +372,21 @@ __device__ __forceinline__ void perm_gen_fast_body(GenArgs a, unsigned long long
   uint32_t* lds_elite = (uint32_t*)(smem + 32);
   const uint32_t L = a.L, nch = a.chunks, lp = 8 * nch;
   const uint32_t BLK = blockDim.x, NWv = BLK >> 6;
+  constexpr uint32_t NG = 64 / GS;  // children per wave per step
   float* coords = smem + kHdrF;
-  uint16_t* arena = (uint16_t*)(coords + (OBJ == OBJ_TSP_EUC ? 16 * nch : 0));
-  // the table after the groups' arrays (16-byte aligned: lp is a multiple of 8)
-  uint16_t* tab = arena + (size_t)(BLK / GS) * 4 * lp;
-  const uint32_t tri = L * (L - 1) / 2;  // TBL 1: the diagonal's offset
+  char* arena = (char*)(coords + (OBJ == OBJ_TSP_EUC ? 16 * nch : 0));
+  const size_t gbytes = perm_fast_group_bytes(nch);
+  // the table after the groups' arrays (16-byte aligned: gbytes is a multiple of 16)
+  const uint16_t* tab = (const uint16_t*)(arena + (size_t)(BLK / GS) * gbytes);
+  const float* ftab = (const float*)tab;
+  const uint32_t tri = L * (L - 1) / 2;  // TBL 1, 3: the diagonal's offset
 
   const uint32_t lane = lane_id();
   const uint32_t q = lane & (GS - 1);
   const uint32_t gbase = lane & ~(uint32_t)(GS - 1);
-  const uint32_t GPB = BLK / GS;
-  const uint32_t g = threadIdx.x / GS;
-  uint16_t* B = arena + (size_t)g * 4 * lp + lp;
-  uint16_t* Cc = B + lp;
-  uint16_t* Mp = Cc + lp;
+  const uint32_t g = lane / GS;
+  uint16_t* Cc = (uint16_t*)(arena + (size_t)(threadIdx.x / GS) * gbytes);  // PMX: T, then the child
+  uint32_t* bits = (uint32_t*)((char*)Cc + 16u * nch);                      // OX membership
   const uint64_t rs = a.row_words >> 2;
   const uint4* cur = (const uint4*)a.cur;
   uint4* nxt = (uint4*)a.next;
@@ -352,158 +404,271 @@ __device__ __forceinline__ void perm_gen_fast_body(GenArgs a, unsigned long long
   if (OBJ == OBJ_TSP_EUC)
     for (uint32_t i = threadIdx.x; i < 2 * L; i += BLK) coords[i] = a.obj_data[i];
   if (TBL)
-    for (uint32_t i = threadIdx.x; i < a.obj_aux_bytes / 16; i += BLK) ((uint4*)tab)[i] = ((const uint4*)a.obj_aux)[i];
+    for (uint32_t i = threadIdx.x; i < a.obj_aux_bytes / 16; i += BLK)
+      ((uint4*)tab)[i] = ((const uint4*)a.obj_aux)[i];
   __syncthreads();
 
   unsigned long long my_best = 0;
   ScoreStats st;
-  for (uint64_t base = (uint64_t)blockIdx.x * GPB; base < a.S; base += (uint64_t)gridDim.x * GPB) {
-    const uint64_t child = base + g;
-    const bool valid = child < a.S;  // group-uniform
-    const uint64_t ch = valid ? child : a.S - 1;
-    const Pool<GS> pool{draw(a.key, ST_CHILD, ch, q), gbase};
-    uint32_t pa, pb;
-    select_parents<GS>(a, pool, ch, pa, pb);
-    const bool elite = ch < a.n_elite;
-    if (elite) {
-      pa = a.elite_idx ? a.elite_idx[ch] : *lds_elite;
-      pb = pa;
+  // batches of U children (the launcher's GenArgs::tp_unit: 64, or fewer for
+  // small populations so that every wave gets one)
+  const uint32_t U = a.tp_unit >= NG && a.tp_unit <= 64u && (a.tp_unit & (a.tp_unit - 1u)) == 0u ? a.tp_unit : 64u;
+  const uint32_t TW = gridDim.x * NWv, Wg = blockIdx.x * NWv + (threadIdx.x >> 6);
+  for (uint32_t bb = Wg * U; bb < S32; bb += TW * U) {  // wave-uniform batches (the launcher: S < 2^32)
+    // ---- SELECT: lane j draws for child bb + j (its ST_CHILD words, core.hpp
+    // child_word: block 0 = crossover test and cut words, block 1 = mutation
+    // test and first position word, blocks 1-2 = the tournament words) and
+    // picks its parents; the breed steps fetch the results by lane ----
+    uint32_t PA, PB, PM, PX;  // parents; lo | hi << 10 | xo << 20 | mutate << 21 | elite << 22; i | j << 16
+    {
+      const uint32_t cj = lane < U && bb + lane < S32 ? bb + lane : bb;
+      const u32x4 b0 = draw(a.key, ST_CHILD, cj, 0);
+      const LanePool<GS> lpool{draw(a.key, ST_CHILD, cj, 1), draw(a.key, ST_CHILD, cj, 2)};
+      select_parents<GS, LanePool<GS>>(a, lpool, cj, PA, PB);
+#if PGA_PERM_NOSEL  // experiment builds: parents without tournaments
+      PA = cj;
+      PB = (cj ^ 1u) < S32 ? (cj ^ 1u) : cj;
+#endif
+      const bool elite = cj < a.n_elite;
+      if (elite) {
+        PA = a.elite_idx ? a.elite_idx[cj] : *lds_elite;
+        PB = PA;
+      }
+      const bool xo = !PGA_PERM_NOXO && !elite && xo_kind && do_crossover(a, b0.x);  // W_XOPROB
+      uint32_t lo, hi;
+      perm_segment(b0.y, b0.z, L, lo, hi);  // W_CUT1, W_CUT2
+      const bool mut = !elite && mut_on && lpool.b1.x < a.mut_ind_thresh;  // W_MUTIND
+      uint32_t mi = 0, mj = 0;
+      if (mut) perm_mut_positions(lpool.b1.y, child_word(a.key, cj, W_SEL + sel_words(a)), L, mi, mj);  // W_MUTPOS
+      PM = lo | (hi << 10) | (xo ? 1u << 20 : 0u) | (mut ? 1u << 21 : 0u) | (elite ? 1u << 22 : 0u);
+      PX = mi | (mj << 16);
     }
-    const bool xo = !elite && xo_kind && do_crossover(a, pool.get(W_XOPROB, a.key, ch));
-    uint32_t lo, hi;
-    perm_segment(pool.get(W_CUT1, a.key, ch), pool.get(W_CUT2, a.key, ch), L, lo, hi);
-    // parent / child chunks stay packed (8 x u16 in 4 VGPRs each)
-    const uint4 Av = cur[(uint64_t)pa * rs + qc];
-    const uint4 Bv = cur[(uint64_t)pb * rs + qc];
-    uint4 Cv = Av;
-    float score = 0.f;
-    if (elite) score = a.score_cur[pa];
+    const uint32_t nst = ((S32 - bb < U ? S32 - bb : U) + NG - 1) / NG;
+    uint4 nA, nB;  // the next step's parent chunks
+    if (PGA_PERM_PF) {
+      const uint32_t pa = (uint32_t)__shfl((int)PA, (int)g, 64), pb = (uint32_t)__shfl((int)PB, (int)g, 64);
+      nA = cur[(uint64_t)pa * rs + qc];
+      nB = cur[(uint64_t)pb * rs + qc];
+    }
+    for (uint32_t t = 0; t < nst; ++t) {  // wave-uniform
+      // ---- BREED step t: child bb + NG t + g ----
+      const uint32_t child = bb + NG * t + g;
+      const bool valid = child < S32;  // group-uniform
+      const uint32_t jl = NG * t + g;   // the child's SELECT lane
+      const uint32_t pa = (uint32_t)__shfl((int)PA, (int)jl, 64);
+      if (!PGA_PERM_PF) {
+        const uint32_t pb = (uint32_t)__shfl((int)PB, (int)jl, 64);
+        nA = cur[(uint64_t)pa * rs + qc];
+        nB = cur[(uint64_t)pb * rs + qc];
+      }
+      const uint4 Av = nA, Bv = nB;
+      if (PGA_PERM_PF && t + 1 < nst) {  // wave-uniform: issue step t + 1's rows now
+        const uint32_t j = jl + NG;
+        const uint32_t na = (uint32_t)__shfl((int)PA, (int)j, 64), nb = (uint32_t)__shfl((int)PB, (int)j, 64);
+        nA = cur[(uint64_t)na * rs + qc];
+        nB = cur[(uint64_t)nb * rs + qc];
+      }
+      const uint32_t pm = (uint32_t)__shfl((int)PM, (int)jl, 64);
+      const bool elite = (pm >> 22) & 1u, xo = (pm >> 20) & 1u;
+      const uint32_t lo = pm & 1023u, hi = (pm >> 10) & 1023u;
+      uint4 Cv = Av;
+      float score = 0.f;
+      if (elite) score = a.score_cur[pa];
 
-    if (xo) {  // group-uniform
-      if (have) {
-        *(uint4*)(Mp + 8 * q) = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu);
-        if (pmx) *(uint4*)(B + 8 * q) = Bv;  // PMX follows chains through B
-      }
-      wave_sync();
+      if (xo) {  // group-uniform
+        if (pmx) {
+          // T[city] = the city PMX replaces it by: B's gene at the city's
+          // position in A's segment (kNone outside it); a gene of B outside
+          // the segment follows T until it leaves A's segment
+          uint16_t* T = Cc;
+          if (have) *(uint4*)(T + 8 * q) = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu);
+          wave_sync();
 #pragma unroll
-      for (uint32_t e = 0; e < 8; ++e) {
-        const uint32_t k = 8 * q + e;
-        if (have && k >= lo && k < hi) Mp[get16(Av, e)] = (uint16_t)k;  // city -> its position in A's segment
-      }
-      wave_sync();
-      if (pmx) {
+          for (uint32_t e = 0; e < 8; ++e) {
+            const uint32_t k = 8 * q + e;
+            if (have && k >= lo && k < hi) T[min(get16(Av, e), lp - 1)] = (uint16_t)get16(Bv, e);
+          }
+          wave_sync();
+#if PGA_PERM_CHAIN == 0
+          // the first link of all 8 genes in one batch of LDS reads (most
+          // genes of B are not in A's segment: their chain ends there), the
+          // rest of each chain one gene after another; a chain takes at most
+          // L links
+          uint32_t y0[8];
 #pragma unroll
-        for (uint32_t e = 0; e < 8; ++e) {
-          const uint32_t p = 8 * q + e;
-          uint32_t v = get16(Bv, e);
-          if (p < L && !(p >= lo && p < hi))
-            for (uint32_t guard = 0; Mp[v] != kNone && guard < L; ++guard) v = B[Mp[v]];
-          Cv = set16(Cv, e, p >= L ? 0u : ((p >= lo && p < hi) ? get16(Av, e) : v));
+          for (uint32_t e = 0; e < 8; ++e) y0[e] = T[min(get16(Bv, e), lp - 1)];
+#pragma unroll
+          for (uint32_t e = 0; e < 8; ++e) {
+            const uint32_t p = 8 * q + e;
+            uint32_t v = get16(Bv, e);
+            if (p < L && !(p >= lo && p < hi)) {
+              uint32_t y = y0[e];
+              for (uint32_t guard = 0; y != kNone && guard < L;) {
+                v = y;
+                if (++guard >= L) break;
+                y = T[min(v, lp - 1)];
+              }
+            }
+            Cv = set16(Cv, e, p >= L ? 0u : ((p >= lo && p < hi) ? get16(Av, e) : v));
+          }
+#elif PGA_PERM_CHAIN == 3  // one gene after another (round 4's form)
+#pragma unroll
+          for (uint32_t e = 0; e < 8; ++e) {
+            const uint32_t p = 8 * q + e;
+            uint32_t v = get16(Bv, e);
+            if (p < L && !(p >= lo && p < hi))
+              for (uint32_t guard = 0; guard < L; ++guard) {
+                const uint32_t w = T[min(v, lp - 1)];
+                if (w == kNone) break;
+                v = w;
+              }
+            Cv = set16(Cv, e, p >= L ? 0u : ((p >= lo && p < hi) ? get16(Av, e) : v));
+          }
+#else
+          // the lane's 8 chains advance together (8 independent LDS reads per
+          // step instead of 8 loops each as long as the wave's longest
+          // chain); each chain still takes at most L steps
+          uint32_t v[8], act = 0;
+#pragma unroll
+          for (uint32_t e = 0; e < 8; ++e) {
+            const uint32_t p = 8 * q + e;
+            v[e] = get16(Bv, e);
+            act |= (p < L && !(p >= lo && p < hi)) ? 1u << e : 0u;
+          }
+          for (uint32_t guard = 0; act != 0u && guard < L; ++guard) {
+            uint32_t w[8];
+#pragma unroll
+            for (uint32_t e = 0; e < 8; ++e)
+              w[e] = (PGA_PERM_CHAIN == 2 || ((act >> e) & 1u)) ? (uint32_t)T[min(v[e], lp - 1)] : (uint32_t)kNone;
+#pragma unroll
+            for (uint32_t e = 0; e < 8; ++e) {
+              const bool adv = ((act >> e) & 1u) && w[e] != kNone;
+              v[e] = adv ? w[e] : v[e];
+              act = adv ? act : act & ~(1u << e);
+            }
+          }
+#pragma unroll
+          for (uint32_t e = 0; e < 8; ++e) {
+            const uint32_t p = 8 * q + e;
+            Cv = set16(Cv, e, p >= L ? 0u : ((p >= lo && p < hi) ? get16(Av, e) : v[e]));
+          }
+#endif
+        } else {  // OX1 (same ranks as perm_kernel); membership of A's segment as bits
+          if (q < (nch + 3) / 4) bits[q] = 0u;
+          wave_sync();
+#pragma unroll
+          for (uint32_t e = 0; e < 8; ++e) {
+            const uint32_t k = 8 * q + e, c = get16(Av, e);
+            if (have && k >= lo && k < hi)
+              __hip_atomic_fetch_or(&bits[(c >> 5) & 15u], 1u << (c & 31u), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+          }
+          wave_sync();
+          uint32_t keep = 0, eb_part = 0;
+#pragma unroll
+          for (uint32_t e = 0; e < 8; ++e) {
+            const uint32_t p = 8 * q + e, c = get16(Bv, e);
+            const bool k = have && p < L && !((bits[(c >> 5) & 15u] >> (c & 31u)) & 1u);
+            keep |= k ? (1u << e) : 0u;
+            eb_part += (k && p < hi) ? 1u : 0u;
+          }
+          const uint32_t Eb = group_sum_u<GS>(eb_part);
+          const uint32_t K = L - (hi - lo), tail = L - hi;
+          uint32_t seg_total;
+          uint32_t run = group_excl_scan<GS>(__popc(keep), q, seg_total);
+#pragma unroll
+          for (uint32_t e = 0; e < 8; ++e) {
+            const uint32_t p = 8 * q + e;
+            if (have && p >= L) Cc[p] = 0;
+            if (have && p < L && p >= lo && p < hi) Cc[p] = (uint16_t)get16(Av, e);
+            if ((keep >> e) & 1u) {
+              const uint32_t r = p >= hi ? run - Eb : (K - Eb) + run;
+              const uint32_t pos = r < tail ? hi + r : r - tail;
+              Cc[pos] = (uint16_t)get16(Bv, e);
+              ++run;
+            }
+          }
+          wave_sync();
+          Cv = *(const uint4*)(Cc + 8 * qc);
         }
-      } else {  // OX1 (same ranks as perm_kernel)
-        uint32_t keep = 0, eb_part = 0;
-#pragma unroll
-        for (uint32_t e = 0; e < 8; ++e) {
-          const uint32_t p = 8 * q + e;
-          const bool k = have && p < L && Mp[get16(Bv, e)] == kNone;
-          keep |= k ? (1u << e) : 0u;
-          eb_part += (k && p < hi) ? 1u : 0u;
-        }
-        const uint32_t Eb = group_sum_u<GS>(eb_part);
-        const uint32_t K = L - (hi - lo), tail = L - hi;
-        uint32_t seg_total;
-        uint32_t run = group_excl_scan<GS>(__popc(keep), q, seg_total);
-#pragma unroll
-        for (uint32_t e = 0; e < 8; ++e) {
-          const uint32_t p = 8 * q + e;
-          if (have && p >= L) Cc[p] = 0;
-          if (have && p < L && p >= lo && p < hi) Cc[p] = (uint16_t)get16(Av, e);
-          if ((keep >> e) & 1u) {
-            const uint32_t r = p >= hi ? run - Eb : (K - Eb) + run;
-            const uint32_t pos = r < tail ? hi + r : r - tail;
-            Cc[pos] = (uint16_t)get16(Bv, e);
-            ++run;
+      }
+
+      // (the shuffle before the branch: the SELECT lane may be outside it)
+      const uint32_t px = (uint32_t)__shfl((int)PX, (int)jl, 64);
+      if ((pm >> 21) & 1u) {  // group-uniform: mutation
+        const uint32_t i = px & 0xFFFFu, j = px >> 16;
+        wave_sync();  // earlier readers of C / T are done
+        if (have) *(uint4*)(Cc + 8 * q) = Cv;
+        wave_sync();
+        if (a.mutation == MUT_SWAP) {
+          if (q == 0) {
+            const uint16_t t2 = Cc[i];
+            Cc[i] = Cc[j];
+            Cc[j] = t2;
+          }
+        } else {
+          const uint32_t half = (j - i + 1) / 2;
+          for (uint32_t t2 = q; t2 < half; t2 += GS) {
+            const uint16_t x = Cc[i + t2];
+            Cc[i + t2] = Cc[j - t2];
+            Cc[j - t2] = x;
           }
         }
         wave_sync();
         Cv = *(const uint4*)(Cc + 8 * qc);
       }
-    }
+      wave_sync();  // the next child of this group rewrites C / T / bits
 
-    if (!elite && mut_on && pool.get(W_MUTIND, a.key, ch) < a.mut_ind_thresh) {  // group-uniform
-      uint32_t i, j;
-      perm_mut_positions(pool.get(W_MUTPOS, a.key, ch), pool.get(W_SEL + sel_words(a), a.key, ch), L, i, j);
-      wave_sync();  // earlier readers of C are done
-      if (have) *(uint4*)(Cc + 8 * q) = Cv;
-      wave_sync();
-      if (a.mutation == MUT_SWAP) {
-        if (q == 0) {
-          const uint16_t t = Cc[i];
-          Cc[i] = Cc[j];
-          Cc[j] = t;
-        }
-      } else {
-        const uint32_t half = (j - i + 1) / 2;
-        for (uint32_t t = q; t < half; t += GS) {
-          const uint16_t x = Cc[i + t];
-          Cc[i + t] = Cc[j - t];
-          Cc[j - t] = x;
-        }
-      }
-      wave_sync();
-      Cv = *(const uint4*)(Cc + 8 * qc);
-    }
-    wave_sync();  // the next child of this group rewrites B / C / M
-
-    if (valid && have) nxt[child * rs + q] = Cv;
-    if (!elite) {
-      // edges (p, p+1) and the closing edge; the city after a lane's chunk is
-      // the next lane's first city
-      const uint32_t c0 = Cv.x & 0xFFFFu;
-      const uint32_t next_first = (uint32_t)__shfl((int)c0, (int)(gbase + ((q + 1) & (GS - 1))), 64);
-      const uint32_t first = (uint32_t)__shfl((int)c0, (int)gbase, 64);
-      const uint32_t last = (OBJ == OBJ_TSP_OPEN) ? L - 1 : L;
-      float len = 0.f;
-      if (OBJ == OBJ_TSP_EUC) {
-        // one float2 per city of the chunk (+ the following city), reused by both edge ends
-        const float2* xy = (const float2*)coords;
-        float2 pu = xy[min(get16(Cv, 0), L - 1)];
+      if (valid && have) nxt[(uint64_t)child * rs + q] = Cv;
+      if (!elite && !PGA_PERM_NOEVAL) {
+        // edges (p, p+1) and the closing edge; the city after a lane's chunk is
+        // the next lane's first city
+        const uint32_t c0 = Cv.x & 0xFFFFu;
+        const uint32_t next_first = (uint32_t)__shfl((int)c0, (int)(gbase + ((q + 1) & (GS - 1))), 64);
+        const uint32_t first = (uint32_t)__shfl((int)c0, (int)gbase, 64);
+        const uint32_t last = (OBJ == OBJ_TSP_OPEN) ? L - 1 : L;
+        float len = 0.f;
+        if (OBJ == OBJ_TSP_EUC) {
+          // one float2 per city of the chunk (+ the following city), reused by both edge ends
+          const float2* xy = (const float2*)coords;
+          float2 pu = xy[min(get16(Cv, 0), L - 1)];
 #pragma unroll
-        for (uint32_t e = 0; e < 8; ++e) {
-          const uint32_t p = 8 * q + e;
-          const uint32_t nx = p + 1 < L ? (e < 7 ? get16(Cv, e + 1) : next_first) : first;
-          const float2 pw = xy[min(nx, L - 1)];
-          if (have && p < last) {
-            const float dx = pu.x - pw.x, dy = pu.y - pw.y;
-            len += sqrtf(fmaf(dx, dx, dy * dy));
-          }
-          pu = pw;
-        }
-      } else {
-#pragma unroll
-        for (uint32_t e = 0; e < 8; ++e) {
-          const uint32_t p = 8 * q + e;
-          if (have && p < last) {
+          for (uint32_t e = 0; e < 8; ++e) {
+            const uint32_t p = 8 * q + e;
             const uint32_t nx = p + 1 < L ? (e < 7 ? get16(Cv, e + 1) : next_first) : first;
-            const uint32_t u = min(get16(Cv, e), L - 1), w = min(nx, L - 1);
-            if constexpr (TBL == 1) {
-              const uint32_t hi_ = u > w ? u : w, lo_ = u > w ? w : u;
-              len += (float)tab[hi_ == lo_ ? tri + u : hi_ * (hi_ - 1) / 2 + lo_];
-            } else if constexpr (TBL == 2) {
-              len += (float)tab[u * L + w];
-            } else {
-              len += a.obj_data[u * L + w];
+            const float2 pw = xy[min(nx, L - 1)];
+            if (have && p < last) {
+              const float dx = pu.x - pw.x, dy = pu.y - pw.y;
+              len += sqrtf(fmaf(dx, dx, dy * dy));
+            }
+            pu = pw;
+          }
+        } else {
+#pragma unroll
+          for (uint32_t e = 0; e < 8; ++e) {
+            const uint32_t p = 8 * q + e;
+            if (have && p < last) {
+              const uint32_t nx = p + 1 < L ? (e < 7 ? get16(Cv, e + 1) : next_first) : first;
+              const uint32_t u = min(get16(Cv, e), L - 1), w = min(nx, L - 1);
+              if constexpr (TBL == 1 || TBL == 3) {
+                const uint32_t hi_ = u > w ? u : w, lo_ = u > w ? w : u;
+                const uint32_t ix = hi_ == lo_ ? tri + u : hi_ * (hi_ - 1) / 2 + lo_;
+                len += TBL == 1 ? (float)tab[ix] : ftab[ix];
+              } else if constexpr (TBL == 2) {
+                len += (float)tab[u * L + w];
+              } else {
+                len += a.obj_data[u * L + w];
+              }
             }
           }
         }
+        score = -group_sum<GS>(len);
       }
-      score = -group_sum<GS>(len);
-    }
-    if (valid && q == 0) {
-      a.score_next[child] = score;
-      const unsigned long long pb2 = pack_best(score, child);
-      my_best = pb2 > my_best ? pb2 : my_best;
-      st.add(score);
+      if (valid && q == 0) {
+        a.score_next[child] = score;
+        const unsigned long long pb2 = pack_best(score, child);
+        my_best = pb2 > my_best ? pb2 : my_best;
+        st.add(score);
+      }
     }
   }
   if (best_parts) {
@@ -574,21 +739,42 @@ uint32_t go(const GenArgs& a, unsigned long long* parts, hipStream_t s) {
   return grid;
 }
 
+// children per wave batch (GenArgs::tp_unit of the fast kernel): 64, halved
+// (down to one step) while the batches would leave waves of the grid idle
+template <int GS>
+uint32_t fast_unit(uint64_t S, uint64_t waves) {
+  uint32_t u = 64;
+  while (u > 64u / GS && (S + u - 1) / u < waves) u >>= 1;
+  return u;
+}
+
+// the LDS matrix for PMX too (PGA_PERM_PMX_TBL=0: PMX keeps the L2 matrix
+// path and its 256-thread blocks, for A/B runs)
+inline bool perm_tbl_on(const GenArgs& a) {
+  static const bool pmx_tbl = [] {
+    const char* e = std::getenv("PGA_PERM_PMX_TBL");
+    return !(e && e[0] == '0');
+  }();
+  return a.crossover != XO_PMX || pmx_tbl;
+}
+
 template <int GS, int OBJ, int TBL>
-uint32_t go_fast_blk(const GenArgs& a, unsigned long long* parts, hipStream_t s, uint32_t blk) {
-  const size_t lds = perm_lds_bytes(GS, a.chunks, OBJ == OBJ_TSP_EUC, blk) + (TBL ? a.obj_aux_bytes : 0);
+uint32_t go_fast_blk(const GenArgs& a0, unsigned long long* parts, hipStream_t s, uint32_t blk) {
+  const size_t lds = perm_fast_lds_bytes(GS, a0.chunks, OBJ == OBJ_TSP_EUC, blk) + (TBL ? a0.obj_aux_bytes : 0);
   auto k = perm_gen_fast<GS, OBJ, TBL>;
   const size_t avail = allow_dynamic_lds((const void*)k);
   if constexpr (TBL != 0) {  // the table did not fit this device's limit: the L2 matrix path
-    if (lds > avail) return go_fast_blk<GS, OBJ, 0>(a, parts, s, kBlock);
+    if (lds > avail) return go_fast_blk<GS, OBJ, 0>(a0, parts, s, kBlock);
   }
-  const uint32_t gpb = blk / GS;
-  const uint64_t need = (a.S + gpb - 1) / gpb;
   int per_cu = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)k, (int)blk, lds) != hipSuccess || per_cu <= 0)
     per_cu = 1;
   uint64_t cap = (uint64_t)device_cu_count() * per_cu;
   if (cap > kMaxGrid) cap = kMaxGrid;
+  GenArgs a = a0;
+  const uint32_t nw = blk / 64;
+  a.tp_unit = fast_unit<GS>(a.S, cap * nw);
+  const uint64_t need = ((a.S + a.tp_unit - 1) / a.tp_unit + nw - 1) / nw;
   const uint32_t grid = (uint32_t)(need < cap ? need : cap);
   hipLaunchKernelGGL(k, grid, blk, lds, s, a, parts);
   return grid;
@@ -597,17 +783,15 @@ uint32_t go_fast_blk(const GenArgs& a, unsigned long long* parts, hipStream_t s,
 template <int GS, int OBJ>
 uint32_t go_fast(const GenArgs& a, unsigned long long* parts, hipStream_t s) {
   if constexpr (OBJ == OBJ_TSP || OBJ == OBJ_TSP_OPEN) {
-    // an integer matrix as u16 in LDS: the largest block (up to 16 waves,
-    // one table per CU) whose group arrays fit beside it
-    // (OX / no crossover: TSP-256 OX 3,265 -> 4,013 gens/s; PMX's chain
-    // walks want the 256-thread occupancy more: 2,793 vs 2,650, L2 path kept)
-    if (a.obj_aux && (a.obj_aux_kind == 1 || a.obj_aux_kind == 2) && a.obj_aux_bytes % 16 == 0 &&
-        a.crossover != XO_PMX) {
+    // the matrix in LDS (obj_aux): the largest block (up to 16 waves, one
+    // table per CU) whose group arrays fit beside it
+    if (a.obj_aux && a.obj_aux_kind >= 1 && a.obj_aux_kind <= 3 && a.obj_aux_bytes % 16 == 0 && perm_tbl_on(a)) {
       const size_t avail = 160 * 1024 - 1024;  // less the static LDS (block reductions)
       for (uint32_t blk : {1024u, 512u, 256u}) {
-        if (perm_lds_bytes(GS, a.chunks, false, blk) + a.obj_aux_bytes > avail) continue;
+        if (perm_fast_lds_bytes(GS, a.chunks, false, blk) + a.obj_aux_bytes > avail) continue;
         if (a.obj_aux_kind == 1) return go_fast_blk<GS, OBJ, 1>(a, parts, s, blk);
-        return go_fast_blk<GS, OBJ, 2>(a, parts, s, blk);
+        if (a.obj_aux_kind == 2) return go_fast_blk<GS, OBJ, 2>(a, parts, s, blk);
+        return go_fast_blk<GS, OBJ, 3>(a, parts, s, blk);
       }
     }
   }
@@ -640,18 +824,19 @@ uint32_t launch_obj(int mode, const GenArgs& a, unsigned long long* parts, hipSt
 template <int GS, int OBJ>
 uint32_t batch_go(PermBatch& b, uint32_t n, hipStream_t s) {
   const GenArgs& a0 = b.a[0];
-  const size_t lds = perm_lds_bytes(GS, a0.chunks, OBJ == OBJ_TSP_EUC);
+  const size_t lds = perm_fast_lds_bytes(GS, a0.chunks, OBJ == OBJ_TSP_EUC, kBlock);
   const void* k = (const void*)perm_gen_fast_batch<GS, OBJ>;
   static bool configured = false;
   if (!configured) {
     allow_dynamic_lds(k);
     configured = true;
   }
-  const uint32_t gpb = kBlock / GS;
-  const uint64_t need = (a0.S + gpb - 1) / gpb;
   uint64_t cap = (uint64_t)device_cu_count() * occupancy_blocks(k, kBlock, lds) / n;  // the device split
   if (cap < 1) cap = 1;
   if (cap > kMaxGrid) cap = kMaxGrid;
+  const uint32_t nw = kBlock / 64, u = fast_unit<GS>(a0.S, cap * nw);
+  for (uint32_t i = 0; i < n; ++i) b.a[i].tp_unit = u;
+  const uint64_t need = ((a0.S + u - 1) / u + nw - 1) / nw;
   const uint32_t gx = (uint32_t)(need < cap ? need : cap);
   hipLaunchKernelGGL((perm_gen_fast_batch<GS, OBJ>), dim3(gx, n), kBlock, lds, s, b);
   PGA_HIP_CHECK(hipGetLastError());

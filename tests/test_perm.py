@@ -98,14 +98,20 @@ def test_gpu_bitexact_general_matrix(xo, n, shape):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("xo", ["ox", "pmx"])
-@pytest.mark.parametrize("inst", ["int_euc256", "e3_100", "int_euc100_open"])
+@pytest.mark.parametrize("inst", ["int_euc256", "e3_100", "int_euc100_open", "f32_sym256", "f32_sym100_open"])
 def test_gpu_lds_matrix_bitexact(xo, inst, monkeypatch):
-    """Integer matrices evaluate from a u16 copy in LDS (symmetric: strict
-    triangle + diagonal in 16-wave blocks; asymmetric: the full matrix):
-    rows and scores equal the CPU backend and the f32 L2 path bit for bit."""
+    """Matrices evaluate from a copy in LDS: integer ones as u16 (symmetric:
+    strict triangle + diagonal in 16-wave blocks; asymmetric: the full
+    matrix), other symmetric ones as the f32 triangle + diagonal (131.6 KB at
+    256 cities): rows and scores equal the CPU backend and the f32 L2 path
+    bit for bit."""
     p = {"int_euc256": lambda: M.TSP.random_integer_euclidean(256, seed=2),
          "e3_100": lambda: M.TSP.reference_e3(100, seed=1),
-         "int_euc100_open": lambda: M.TSP.random_integer_euclidean(100, seed=5, open_path=True)}[inst]()
+         "int_euc100_open": lambda: M.TSP.random_integer_euclidean(100, seed=5, open_path=True),
+         "f32_sym256": lambda: M.TSP.random_euclidean(256, seed=2),
+         "f32_sym100_open": lambda: M.TSP.random_euclidean(100, seed=5, open_path=True)}[inst]()
+    if inst.startswith("f32"):
+        assert torch.equal(p.dist, p.dist.T) and not torch.equal(p.dist, p.dist.round())
     kw = dict(seed=8, crossover=xo, mutation="inversion", mutation_rate=0.4, elitism=1)
     g = pga.GeneticAlgorithm(p, 5000, device="cuda:0", **kw)
     c = pga.GeneticAlgorithm(p, 5000, device="cpu", **kw)
