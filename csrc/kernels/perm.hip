@@ -695,9 +695,9 @@ struct PermBatch {
   GenArgs a[kPermMaxBatch];
   unsigned long long* parts[kPermMaxBatch];
 };
-template <int GS, int OBJ>
+template <int GS, int OBJ, int TBL = 0>
 __global__ __launch_bounds__(kBlock) void perm_gen_fast_batch(PermBatch b) {
-  perm_gen_fast_body<GS, OBJ, 0>(b.a[blockIdx.y], b.parts[blockIdx.y]);
+  perm_gen_fast_body<GS, OBJ, TBL>(b.a[blockIdx.y], b.parts[blockIdx.y]);
 }
 
 // Genomes beyond kPermMaxL genes: one 64-lane block per individual, so the
@@ -787,7 +787,12 @@ uint32_t go_fast(const GenArgs& a, unsigned long long* parts, hipStream_t s) {
     // table per CU) whose group arrays fit beside it
     if (a.obj_aux && a.obj_aux_kind >= 1 && a.obj_aux_kind <= 3 && a.obj_aux_bytes % 16 == 0 && perm_tbl_on(a)) {
       const size_t avail = 160 * 1024 - 1024;  // less the static LDS (block reductions)
-      for (uint32_t blk : {1024u, 512u, 256u}) {
+      // populations that fill every wave of 16-wave blocks with 64-child
+      // batches take the largest block that fits (one table per CU); smaller
+      // ones the smallest, so that their few batches spread over every CU
+      const bool big = a.S >= 1024ull * device_cu_count();
+      const uint32_t order[3] = {big ? 1024u : 256u, 512u, big ? 256u : 1024u};
+      for (uint32_t blk : order) {
         if (perm_fast_lds_bytes(GS, a.chunks, false, blk) + a.obj_aux_bytes > avail) continue;
         if (a.obj_aux_kind == 1) return go_fast_blk<GS, OBJ, 1>(a, parts, s, blk);
         if (a.obj_aux_kind == 2) return go_fast_blk<GS, OBJ, 2>(a, parts, s, blk);
@@ -821,11 +826,12 @@ uint32_t launch_obj(int mode, const GenArgs& a, unsigned long long* parts, hipSt
   }
 }
 
-template <int GS, int OBJ>
+template <int GS, int OBJ, int TBL = 0>
 uint32_t batch_go(PermBatch& b, uint32_t n, hipStream_t s) {
   const GenArgs& a0 = b.a[0];
-  const size_t lds = perm_fast_lds_bytes(GS, a0.chunks, OBJ == OBJ_TSP_EUC, kBlock);
-  const void* k = (const void*)perm_gen_fast_batch<GS, OBJ>;
+  // TBL: every island's matrix in its blocks' LDS (the islands' tables have one kind and size)
+  const size_t lds = perm_fast_lds_bytes(GS, a0.chunks, OBJ == OBJ_TSP_EUC, kBlock) + (TBL ? a0.obj_aux_bytes : 0);
+  const void* k = (const void*)perm_gen_fast_batch<GS, OBJ, TBL>;
   static bool configured = false;
   if (!configured) {
     allow_dynamic_lds(k);
@@ -838,16 +844,34 @@ uint32_t batch_go(PermBatch& b, uint32_t n, hipStream_t s) {
   for (uint32_t i = 0; i < n; ++i) b.a[i].tp_unit = u;
   const uint64_t need = ((a0.S + u - 1) / u + nw - 1) / nw;
   const uint32_t gx = (uint32_t)(need < cap ? need : cap);
-  hipLaunchKernelGGL((perm_gen_fast_batch<GS, OBJ>), dim3(gx, n), kBlock, lds, s, b);
+  hipLaunchKernelGGL((perm_gen_fast_batch<GS, OBJ, TBL>), dim3(gx, n), kBlock, lds, s, b);
   PGA_HIP_CHECK(hipGetLastError());
   return gx;
+}
+
+template <int GS, int OBJ>
+uint32_t batch_tbl(PermBatch& b, uint32_t n, hipStream_t s) {
+  if constexpr (OBJ == OBJ_TSP || OBJ == OBJ_TSP_OPEN) {
+    const GenArgs& a0 = b.a[0];
+    bool same = a0.obj_aux && a0.obj_aux_kind >= 1 && a0.obj_aux_kind <= 3 && a0.obj_aux_bytes % 16 == 0 &&
+                perm_tbl_on(a0) &&
+                perm_fast_lds_bytes(GS, a0.chunks, false, kBlock) + a0.obj_aux_bytes <= 160 * 1024 - 1024;
+    for (uint32_t i = 1; same && i < n; ++i)
+      same = b.a[i].obj_aux && b.a[i].obj_aux_kind == a0.obj_aux_kind && b.a[i].obj_aux_bytes == a0.obj_aux_bytes;
+    if (same) {
+      if (a0.obj_aux_kind == 1) return batch_go<GS, OBJ, 1>(b, n, s);
+      if (a0.obj_aux_kind == 2) return batch_go<GS, OBJ, 2>(b, n, s);
+      return batch_go<GS, OBJ, 3>(b, n, s);
+    }
+  }
+  return batch_go<GS, OBJ, 0>(b, n, s);
 }
 
 template <int GS>
 uint32_t batch_obj(PermBatch& b, uint32_t n, hipStream_t s) {
   switch (b.a[0].objective) {
-    case OBJ_TSP: return batch_go<GS, OBJ_TSP>(b, n, s);
-    case OBJ_TSP_OPEN: return batch_go<GS, OBJ_TSP_OPEN>(b, n, s);
+    case OBJ_TSP: return batch_tbl<GS, OBJ_TSP>(b, n, s);
+    case OBJ_TSP_OPEN: return batch_tbl<GS, OBJ_TSP_OPEN>(b, n, s);
     case OBJ_TSP_EUC: return batch_go<GS, OBJ_TSP_EUC>(b, n, s);
     default: return 0;
   }
