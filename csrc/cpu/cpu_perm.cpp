@@ -44,6 +44,16 @@ void perm_crossover(int op, const uint16_t* A, const uint16_t* B, uint32_t L, ui
   }
 }
 
+// every city 0..L-1 exactly once (seen: L scratch entries)
+static bool perm_row_valid(const uint16_t* C, uint32_t L, std::vector<uint16_t>& seen) {
+  std::fill(seen.begin(), seen.begin() + L, (uint16_t)0);
+  for (uint32_t p = 0; p < L; ++p) {
+    if (C[p] >= L || seen[C[p]]) return false;
+    seen[C[p]] = 1;
+  }
+  return true;
+}
+
 uint32_t perm_run(int mode, const GenArgs& a, unsigned long long* best_parts) {
   if (a.L > 65535) throw std::invalid_argument("PERMUTATION encoding supports at most 65535 genes (u16 city ids)");
   const uint32_t L = a.L, nch = a.chunks, lp = 8 * nch, GS = group_size(nch);
@@ -78,6 +88,12 @@ uint32_t perm_run(int mode, const GenArgs& a, unsigned long long* best_parts) {
       }
     } else if (mode == MODE_EVAL || mode == MODE_MUTATE) {
       std::memcpy(C.data(), cur + child * rh, 2ull * lp);
+    }
+    if (mode == MODE_EVAL && !perm_row_valid(C.data(), L, A)) {
+      // not a permutation of 0..L-1 (a corrupted or forged migrant): the
+      // identity tour replaces it, scored below like any other row
+      for (uint32_t p = 0; p < lp; ++p) C[p] = p < L ? (uint16_t)p : (uint16_t)0;
+      std::memcpy(nxt + child * rh, C.data(), 2ull * lp);
     }
     if (!elite && crosses) {
       uint32_t pa, pb;

@@ -541,8 +541,8 @@ void Island::run_plain(uint32_t n) {
       if (hist_on_ && !hist_manual_ && !capturing_) append_history();
       continue;
     }
-    const bool fh = fhist_ready_for(a);
-    if (fh) {  // this generation also writes the value histogram of its keys (GenArgs::key_hist)
+    bool fh = fhist_ready_for(a);
+    if (fh) {  // this generation may also write the value histogram of its keys (GenArgs::key_hist)
       a.key_hist = (uint32_t*)fhist_[fhist_rot_ % 3].ptr;
       a.hist_zero = (uint32_t*)fhist_[(fhist_rot_ + 1) % 3].ptr;
       a.hist_bins = cfg_.L + 1;
@@ -550,6 +550,9 @@ void Island::run_plain(uint32_t n) {
     }
     n_best_[cur_ ^ 1] = launch(MODE_GEN, a, (unsigned long long*)best_[cur_ ^ 1].ptr);
     stats_ok_[cur_ ^ 1] = a.stats_parts != nullptr;
+    // valid only when the launcher reports that its kernel took the histogram
+    // (binary_gs.hip go_tp), not on the conditions predicted above
+    fh = fh && binary_hist_written();
     if (fh) {
       const int w = (int)(fhist_rot_ % 3), z = (int)((fhist_rot_ + 1) % 3);
       ++fhist_rot_;

@@ -77,6 +77,10 @@ uint32_t binary_launch(int mode, const GenArgs& a, unsigned long long* best_part
 // binary_launch for one group size GS (binary_gs.hip, one translation unit per GS)
 template <int GS>
 uint32_t binary_launch_group(int mode, const GenArgs& a, unsigned long long* best_parts, hipStream_t s);
+// whether the last binary_launch on this host thread handed GenArgs::key_hist
+// to its kernel (so the fused key histogram was written and hist_zero
+// cleared); the island marks a histogram valid only on this report
+bool& binary_hist_written();
 // whether a MODE_GEN launch of these arguments takes the hot two-phase kernel
 // (binary_gen_tp) and which variant: group size, full groups, dense mutation.
 // For f32-score objectives (the fused JIT generation kernel, jit.hpp).

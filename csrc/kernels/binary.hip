@@ -94,8 +94,14 @@ bool binary_tp_plan(const GenArgs& a, uint32_t& gs, bool& full, bool& dense) {
   return a.chunks <= 64u && fast && o32 && a.n_elite <= kTpMaxElite;
 }
 
+bool& binary_hist_written() {
+  static thread_local bool w = false;
+  return w;
+}
+
 uint32_t binary_launch(int mode, const GenArgs& a, unsigned long long* best_parts, hipStream_t s) {
   uint32_t grid = 0;
+  binary_hist_written() = false;  // go_tp sets it when its kernel takes the histogram
   switch (group_size(a.chunks)) {  // one translation unit per group size (binary_gs.hip)
     case 1: grid = binary_launch_group<1>(mode, a, best_parts, s); break;
     case 2: grid = binary_launch_group<2>(mode, a, best_parts, s); break;

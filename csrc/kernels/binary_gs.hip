@@ -36,9 +36,13 @@ uint32_t go_tp(K kernel, const GenArgs& a0, unsigned long long* parts, hipStream
   a.tp_pool_units = a.tp_pool ? tp_pool_units(t, a.S) : 0u;
   a.tp_skew = tp_skew_units(t, a.S);
   // the fused key histogram's LDS bins follow the round's parents
-  const bool hist = a.key_hist != nullptr && a.hist_bins > 0 && a.hist_bins <= kHistMaxBins;
+  // (binary_gen_tp's HISTK: the objectives with exact u16 keys)
+  const bool key_obj = a.objective == OBJ_ONEMAX || a.objective == OBJ_LEADING_ONES || a.objective == OBJ_TRAP;
+  const bool hist = key_obj && a.key_cur != nullptr && a.key_hist != nullptr && a.hist_bins > 0 &&
+                    a.hist_bins <= kHistMaxBins;
   if (!hist) a.key_hist = nullptr;
   hipLaunchKernelGGL(kernel, t.grid, t.block, t.lds + (hist ? 4u * a.hist_bins : 0u), s, a, parts);
+  binary_hist_written() = hist;
   return t.grid;
 }
 

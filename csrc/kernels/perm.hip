@@ -156,6 +156,33 @@ __global__ __launch_bounds__(BLK) void perm_kernel(GenArgs a, unsigned long long
       }
     }
     __syncthreads();
+    bool forged = false;
+    if constexpr (MODE == MODE_EVAL) {
+      // a row that is not a permutation of 0..L-1 (a corrupted or forged
+      // migrant) becomes the identity tour and is scored as one: Mp[city] =
+      // a position holding it; a duplicate city leaves one of its positions
+      // unclaimed, a city >= L is rejected outright (cpu_perm.cpp: the same)
+      if (valid)
+        for (uint32_t c = q; c < nch; c += GS) *(uint4*)(Mp + 8 * c) = make_uint4(~0u, ~0u, ~0u, ~0u);
+      __syncthreads();
+      uint32_t bad = 0;
+      if (valid)
+        for (uint32_t p = q; p < L; p += GS) {
+          const uint32_t v = Cc[p];
+          if (v >= L) bad = 1;
+          else Mp[v] = (uint16_t)p;
+        }
+      __syncthreads();
+      if (valid)
+        for (uint32_t p = q; p < L; p += GS) {
+          const uint32_t v = Cc[p];
+          if (v < L && Mp[v] != p) bad = 1;
+        }
+      forged = valid && group_sum_u<GS>(bad) != 0;  // group-uniform
+      if (forged)
+        for (uint32_t p = q; p < lp; p += GS) Cc[p] = p < L ? (uint16_t)p : (uint16_t)0;
+      __syncthreads();
+    }
     // ---- stage 2: crossover into C ----
     if (CROSSES) {
       if (valid && !elite) {
@@ -255,7 +282,7 @@ __global__ __launch_bounds__(BLK) void perm_kernel(GenArgs a, unsigned long long
     }
     // ---- stage 4: store + evaluate ----
     if (valid) {
-      if (MODE != MODE_EVAL)
+      if (MODE != MODE_EVAL || forged)
         for (uint32_t c = q; c < nch; c += GS) nxt[child * rs + c] = *(const uint4*)(Cc + 8 * c);
       if (EVALS && !elite) {
         float len = 0.f;
@@ -807,7 +834,11 @@ template <int GS, int OBJ>
 uint32_t launch_mode(int mode, const GenArgs& a, unsigned long long* parts, hipStream_t s) {
   switch (mode) {
     case MODE_GEN:
-      if (OBJ != OBJ_NONE && a.chunks <= (uint32_t)GS && !force_generic_kernels()) return go_fast<GS, OBJ>(a, parts, s);
+      // the fast kernel walks its batches with 32-bit child indices: the
+      // batch base (at most S + grid * 16 waves * 64 past 0) must not wrap
+      if (OBJ != OBJ_NONE && a.chunks <= (uint32_t)GS && !force_generic_kernels() &&
+          a.S <= 0xFFFFFFFFull - (uint64_t)kMaxGrid * 16 * 64)
+        return go_fast<GS, OBJ>(a, parts, s);
       return go<GS, MODE_GEN, OBJ>(a, parts, s);
     case MODE_INIT: return go<GS, MODE_INIT, OBJ>(a, parts, s);
     case MODE_EVAL: return go<GS, MODE_EVAL, OBJ>(a, parts, s);
@@ -832,11 +863,7 @@ uint32_t batch_go(PermBatch& b, uint32_t n, hipStream_t s) {
   // TBL: every island's matrix in its blocks' LDS (the islands' tables have one kind and size)
   const size_t lds = perm_fast_lds_bytes(GS, a0.chunks, OBJ == OBJ_TSP_EUC, kBlock) + (TBL ? a0.obj_aux_bytes : 0);
   const void* k = (const void*)perm_gen_fast_batch<GS, OBJ, TBL>;
-  static bool configured = false;
-  if (!configured) {
-    allow_dynamic_lds(k);
-    configured = true;
-  }
+  (void)allow_dynamic_lds(k);  // cached per (kernel, device)
   uint64_t cap = (uint64_t)device_cu_count() * occupancy_blocks(k, kBlock, lds) / n;  // the device split
   if (cap < 1) cap = 1;
   if (cap > kMaxGrid) cap = kMaxGrid;
@@ -886,6 +913,7 @@ uint32_t perm_launch_batch(const GenArgs* args, unsigned long long* const* parts
   const GenArgs& a0 = args[0];
   if (a0.objective != OBJ_TSP && a0.objective != OBJ_TSP_OPEN && a0.objective != OBJ_TSP_EUC) return 0;
   if (a0.chunks > 64u || a0.L > 65535) return 0;  // the fast kernel: one chunk per lane
+  if (a0.S > 0xFFFFFFFFull - (uint64_t)kMaxGrid * 16 * 64) return 0;  // its 32-bit batch walk (launch_mode)
   PermBatch b;
   for (uint32_t i = 0; i < n; ++i) {
     const GenArgs& a = args[i];

@@ -102,6 +102,7 @@ class IslandModel:
         fault_hook: Optional[Callable[[torch.Tensor, int], bool]] = None,
         policy: str = "topk",
         transport: str = "auto",
+        self_exchange: bool = False,
     ):
         if topology not in TOPOLOGIES:
             raise ValueError(f"topology must be one of {TOPOLOGIES}")
@@ -120,6 +121,16 @@ class IslandModel:
         self.distributed = dist.is_available() and dist.is_initialized()
         self.rank = dist.get_rank(group) if self.distributed else 0
         self.world = dist.get_world_size(group) if self.distributed else 1
+        self._pg_world = self.world
+        # self_exchange (measurement / test mode): ONE process runs the
+        # 2-island ring against itself, its migrants sent to and received
+        # from its own rank over a 1-rank RCCL communicator, so one GPU pays
+        # everything an N-GPU run pays per epoch except the xGMI wire time
+        self.self_exchange = bool(self_exchange)
+        if self.self_exchange:
+            if not (self.distributed and self.world == 1 and topology == "ring"):
+                raise ValueError("self_exchange needs a 1-rank process group and the ring topology")
+            self.world = 2
         S = ga.pop_size
         k = int(round(migrate_pct * S))
         self.k = max(1, min(k, S // 2)) if migrate_pct > 0 else 0
@@ -158,15 +169,19 @@ class IslandModel:
         # native call packs and posts an epoch, one completes it — a fraction
         # of batch_isend_irecv's host time); "auto" = engine on GPU islands
         # of an RCCL process group for the ring / random topologies (no
-        # side stream, fault hook or permutation sanitiser, which need the
-        # python path)
+        # side stream or fault hook, which need the python path).
+        # Permutation islands take it too: the native re-scoring
+        # (Island.evaluate_rows) turns a received row that is not a
+        # permutation into the identity tour before it can enter.
         if transport not in ("auto", "torch", "engine"):
             raise ValueError("transport must be 'auto', 'torch' or 'engine'")
         self._ec = None
-        self._use_engine = transport == "engine" or (
-            transport == "auto" and self.distributed and dev.type == "cuda" and topology in ("ring", "random")
-            and self._side is None and fault_hook is None and ga.problem.encoding != "permutation"
-            and dist.get_backend(group) == "nccl" and os.environ.get("PGA_MIGRATION_TRANSPORT", "") != "torch")
+        engine_ok, why = self._engine_supported(ga, dev, topology, fault_hook, group)
+        if transport == "engine" and self.distributed and not engine_ok:
+            raise ValueError(f"transport='engine' cannot run this model: {why}")
+        self._use_engine = engine_ok and self.distributed and (
+            transport == "engine" or os.environ.get("PGA_MIGRATION_TRANSPORT", "") != "torch")
+        self.fallbacks = 0  # engine -> torch switches made by connect()
         # test-only fault: post the receive but withhold the matching send, so
         # the exchange can never complete (exercises the deadline + abort path)
         self._withhold_send = False
@@ -183,6 +198,49 @@ class IslandModel:
         self.bytes_sent = 0
 
     # --------------------------------------------------------------- utils --
+    def _engine_supported(self, ga, dev, topology, fault_hook, group) -> Tuple[bool, str]:
+        if dev.type != "cuda":
+            return False, "the engine communicator needs GPU islands"
+        if topology not in ("ring", "random"):
+            return False, f"topology {topology!r} (the engine plan is ring / random peers)"
+        if self._side is not None:
+            return False, "side_stream=True (the engine posts on the island's own stream)"
+        if fault_hook is not None:
+            return False, "a fault_hook (it edits the received buffer in python)"
+        if self.distributed and dist.get_backend(group) != "nccl":
+            return False, f"process-group backend {dist.get_backend(group)!r} (RCCL needed)"
+        return True, ""
+
+    @property
+    def transport(self) -> str:
+        """The migration transport in use: "engine" or "torch"."""
+        return "engine" if self._use_engine else "torch"
+
+    @property
+    def rccl_ranks(self) -> int:
+        """Ranks of the RCCL communicator that carries the migrants: the
+        engine communicator's size, the process group's under backend nccl,
+        0 when no RCCL is involved (gloo, one process)."""
+        if self._use_engine and self._ec is not None:
+            return int(self._ec.nranks)
+        if self.distributed and dist.get_backend(self.group) == "nccl":
+            return self._pg_world
+        return 0
+
+    def reduce_max(self, t: torch.Tensor) -> bool:
+        """In-place all-reduce(max) of ``t`` over the islands, bounded by the
+        migration deadline; False (and degraded) when it failed or expired."""
+        if self.world == 1:
+            return True
+        if self.degraded:
+            return False
+        try:
+            work = dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group, async_op=True)
+        except Exception as e:  # noqa: BLE001
+            self._fail(e)
+            return False
+        return self._bounded(work)
+
     def _views(self, buf: torch.Tensor):
         rows = buf[: self.k * self.rw]
         scores = buf[self.k * self.rw:].view(torch.float32)
@@ -191,6 +249,8 @@ class IslandModel:
     def _peers(self) -> Tuple[int, int]:
         """(send_to, recv_from) for ring / random topologies."""
         r, w = self.rank, self.world
+        if self.self_exchange:
+            return r, r
         if self.topology == "ring":
             return (r + 1) % w, (r - 1) % w
         g = torch.Generator().manual_seed(self.seed * 1000003 + self._epoch)
@@ -277,6 +337,16 @@ class IslandModel:
             for wk in works:
                 wk.wait()
             return
+        if self.distributed and dist.get_backend(self.group) == "gloo":
+            # gloo's P2P works complete only inside wait(), which honours a
+            # timeout itself (CPU islands: nothing to keep off the stream)
+            try:
+                for wk in works:
+                    wk.wait(self.timeout)
+            except Exception:
+                self._abort()
+                raise
+            return
         deadline = time.monotonic() + self.timeout.total_seconds()
         pending = list(works)
         while pending:
@@ -337,23 +407,11 @@ class IslandModel:
             rows, scores = self._views(self.recv)
         rows, scores = rows.contiguous(), scores.contiguous()
         if self.validate:
-            isl.evaluate_rows(rows, scores)  # trust nothing from the wire
-            if self.ga.problem.encoding == "permutation":
-                self._sanitize_perm(rows, scores)
+            # trust nothing from the wire: re-scored with the local objective;
+            # a permutation row that is not one becomes the identity tour
+            isl.evaluate_rows(rows, scores)
         isl.immigrate(self.k, rows, scores)  # bottom-k replaced (fused scatter), best + keys follow
         self.migrations += 1
-
-    def _sanitize_perm(self, rows: torch.Tensor, scores: torch.Tensor) -> None:
-        """Replace received rows that are not permutations by the identity
-        with score -inf (device-side, no host sync)."""
-        L = self.ga.problem.length
-        genes = rows.view(self.k, self.rw).view(torch.int16)[:, :L].to(torch.int32) & 0xFFFF
-        ok = (genes.sort(dim=1).values == torch.arange(L, device=genes.device)).all(dim=1)
-        ident = torch.zeros(self.rw * 2, dtype=torch.int16, device=genes.device)
-        ident[:L] = torch.arange(L, device=genes.device, dtype=torch.int32).to(torch.int16)
-        r16 = rows.view(self.k, self.rw).view(torch.int16)
-        r16.copy_(torch.where(ok[:, None], r16, ident[None, :]))
-        scores.copy_(torch.where(ok, scores, torch.full_like(scores, float("-inf"))))
 
     def _fail(self, e: BaseException) -> None:
         self.failures += 1
@@ -406,12 +464,38 @@ class IslandModel:
     def connect(self) -> None:
         """Run one migration now: RCCL establishes its point-to-point
         connections lazily on the first exchange, so benchmarks call this
-        before timing."""
-        if self.world > 1 and self.k > 0:
-            if self._use_engine:
+        before timing.
+
+        With the engine transport, a communicator that fails to come up or
+        whose first exchange fails on ANY rank (the ranks agree with one
+        all-reduce over the process group) is dropped on every rank, and the
+        islands fall back to torch P2P ops: the model is left healthy, the
+        switch is counted in ``fallbacks``, and nothing is restarted."""
+        if self.world == 1 or self.k == 0:
+            return
+        if self._use_engine:
+            ok = 1.0
+            try:
                 self._engine()
-            self.start_migration()
-            self.finish_migration()
+                self.start_migration()
+                self.finish_migration()
+                ok = 0.0 if self.degraded else 1.0
+            except Exception as e:  # noqa: BLE001 — any setup failure: fall back
+                log.warning("engine communicator setup failed (%s: %s)", type(e).__name__, e)
+                ok = 0.0
+            flag = torch.tensor([ok], dtype=torch.float32,
+                                device=self.send.device if dist.get_backend(self.group) == "nccl" else "cpu")
+            dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=self.group)
+            if float(flag.item()) > 0.0:
+                return
+            log.warning("island %d: engine RCCL transport unavailable, falling back to torch P2P", self.rank)
+            self._use_engine = False
+            self._ec = None
+            self._pending = None
+            self.degraded, self.failures = False, 0
+            self.fallbacks += 1
+        self.start_migration()
+        self.finish_migration()
 
     # -------------------------------------------------------------- queries --
     def _bounded(self, work) -> bool:
@@ -434,7 +518,7 @@ class IslandModel:
             return score, self.rank, genome
         dev = self.send.device
         t = torch.tensor([score, float(self.rank)], dtype=torch.float64, device=dev)
-        allt = [torch.empty_like(t) for _ in range(self.world)]
+        allt = [torch.empty_like(t) for _ in range(self._pg_world)]
         if not self._bounded(dist.all_gather(allt, t, group=self.group, async_op=True)):
             return score, self.rank, genome
         vals = torch.stack(allt).cpu()

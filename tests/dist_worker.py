@@ -91,8 +91,70 @@ def run_faults(rank: int, world: int, port: int, out_dir: str) -> None:
     dist.destroy_process_group()
 
 
+def _problem(name):
+    import libpga_amd as pga
+
+    if name == "tsp":
+        return pga.models.TSP.random_euclidean(40, seed=3)
+    return pga.models.Rastrigin(12)
+
+
+def run_problem(rank: int, world: int, port: int, name: str, topology: str, out_dir: str) -> None:
+    """TSP (u16 permutation rows) and Rastrigin (f32 rows) islands: the exact
+    emigrants arrive, every row stays valid and correctly scored, and the
+    islands migrate on schedule.  name "tsp_forged": the received batch of
+    the first epoch is forged into non-permutations claiming a perfect score
+    (the native re-scoring must turn them into the identity tour)."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    import libpga_amd as pga
+    from libpga_amd.parallel import IslandModel, init_distributed
+
+    init_distributed("gloo")
+    forged = name == "tsp_forged"
+    prob = _problem("tsp" if forged else name)
+    L = prob.length
+
+    def hook(buf, epoch):
+        if epoch == 1:
+            k, rw = model.k, model.rw
+            g16 = buf[: k * rw].view(k, rw).view(torch.int16)
+            g16[0, :L] = 0                        # every gene city 0
+            g16[1, :L] = torch.arange(L, dtype=torch.int16)
+            g16[1, 5] = 7                          # a duplicate city
+            g16[2, :L] = torch.arange(L, dtype=torch.int16)
+            g16[2, 9] = L + 100                    # a city beyond the tour
+            buf[k * rw:] = torch.tensor([1e9], dtype=torch.float32).view(torch.int32)
+        return True
+
+    ga = pga.GeneticAlgorithm(prob, 256, seed=11, island=rank, device="cpu", elitism=1)
+    model = IslandModel(ga, migrate_every=5, migrate_pct=0.05, topology=topology,
+                        fault_hook=hook if forged else None)
+    assert model.transport == "torch" and model.rccl_ranks == 0
+    ga.run(5)
+    sc = ga.scores.clone()
+    k = model.k
+    top_idx = sorted(range(sc.numel()), key=lambda i: (-float(sc[i]), i))[:k]
+    emigrants = ga.genomes().clone()[torch.tensor(top_idx)]
+    model.start_migration()
+    model.finish_migration()
+    after = ga.genomes().clone()
+    scores_after = ga.scores.clone()
+    model.run(30)
+    final = ga.genomes().clone()
+    torch.save({"emigrants": emigrants, "after": after, "scores_after": scores_after,
+                "ref_after": prob.reference_fitness(after), "final": final, "final_scores": ga.scores.clone(),
+                "ref_final": prob.reference_fitness(final), "k": k, "migrations": model.migrations,
+                "degraded": model.degraded, "gen": ga.generation},
+               os.path.join(out_dir, f"prob_{rank}.pt"))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
 if __name__ == "__main__":
-    if sys.argv[4] == "faults":
+    if sys.argv[4] == "problem":
+        run_problem(int(sys.argv[1]), int(sys.argv[2]), int(sys.argv[3]), sys.argv[5], sys.argv[6], sys.argv[7])
+    elif sys.argv[4] == "faults":
         run_faults(int(sys.argv[1]), int(sys.argv[2]), int(sys.argv[3]), sys.argv[5])
     else:
         run(int(sys.argv[1]), int(sys.argv[2]), int(sys.argv[3]), sys.argv[4], sys.argv[5])

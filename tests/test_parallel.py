@@ -69,6 +69,53 @@ def test_island_model_multiprocess(world, topology, tmp_path):
         assert x["best"] > x["b0"]
 
 
+def _is_perm(x: torch.Tensor) -> torch.Tensor:
+    return (x.sort(dim=1).values == torch.arange(x.shape[1])).all(dim=1)
+
+
+@pytest.mark.parametrize("name,world,topology", [("tsp", 2, "ring"), ("tsp", 3, "all_to_all"),
+                                                 ("rastrigin", 2, "ring"), ("rastrigin", 3, "all_to_all"),
+                                                 ("tsp_forged", 2, "ring")])
+def test_island_model_problems_multiprocess(name, world, topology, tmp_path):
+    """Cross-process migration of permutation (u16) and f32 rows, ring and
+    all-to-all (gloo, the same IslandModel code path as RCCL)."""
+    port = free_port()
+    procs = [subprocess.Popen([sys.executable, os.path.join(HERE, "dist_worker.py"), str(r), str(world), str(port),
+                               "problem", name, topology, str(tmp_path)]) for r in range(world)]
+    for p in procs:
+        assert p.wait(timeout=300) == 0
+    res = [torch.load(tmp_path / f"prob_{r}.pt", weights_only=True) for r in range(world)]
+    L = res[0]["after"].shape[1]
+    for r, x in enumerate(res):
+        assert not x["degraded"] and x["gen"] == 35 and x["migrations"] == 7
+        for key in ("after", "final"):
+            ref = x["ref_" + key]
+            got = x["scores_after" if key == "after" else "final_scores"]
+            # every stored score is the local objective's (ulp-level: the
+            # native sum order differs from torch's)
+            assert torch.allclose(got, ref, rtol=1e-5, atol=1e-4), (key, (got - ref).abs().max())
+            if name != "rastrigin":
+                assert bool(_is_perm(x[key]).all()), f"rank {r}: a non-permutation row entered ({key})"
+        rows_after = {tuple(v.tolist()) for v in x["after"]}
+        if name == "tsp_forged":
+            # the three forged rows became the identity tour, scored as one
+            # (no 1e9 claim survives); the other migrants arrived intact
+            ident = tuple(range(L))
+            assert ident in rows_after
+            assert float(x["scores_after"].max()) < 0
+            src = res[(r - 1) % world]["emigrants"]
+            assert sum(tuple(v.tolist()) in rows_after for v in src) >= src.shape[0] - 3
+        elif topology == "ring":
+            src = res[(r - 1) % world]["emigrants"]
+            assert all(tuple(v.tolist()) in rows_after for v in src)
+        else:  # all_to_all: each peer's slice of its top-k arrived
+            per = x["k"] // (world - 1)
+            for p in range(world):
+                if p != r:
+                    got = sum(tuple(v.tolist()) in rows_after for v in res[p]["emigrants"])
+                    assert got >= per, (r, p, got, per)
+
+
 class _Done:
     def wait(self, *a):
         return True
@@ -142,3 +189,27 @@ def test_rccl_engine_withheld_send_degrades_gpu():
                         "engine"], env=env, capture_output=True, text=True, timeout=110)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
     assert "rccl withheld send ok engine" in r.stdout
+
+
+def _bench_rccl_self(*extra):
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(free_port()))
+    r = subprocess.run([sys.executable, os.path.join(os.path.dirname(HERE), "bench.py"), "--rccl-self", "--steps", "30",
+                        "--warmup", "5", *extra], env=env, capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    import json
+
+    out = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    assert out["transport"] == "engine" and out["rccl_ranks"] == 1 and out["self_exchange"]
+    assert out["migrations_timed"] == out["migrations_expected"] == 3
+    assert out["degraded"] is False and out["failures"] == 0
+    return out
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("problem", ["onemax", "tsp256", "rastrigin30"])
+def test_bench_rccl_self_engine_gpu(problem):
+    """The driver's bench path with real RCCL migration on one GPU (the
+    island exchanges with itself over the engine communicator): every
+    BASELINE multi-GPU config migrates through the engine transport, and the
+    JSON line accounts for every exchange of the timed window."""
+    _bench_rccl_self("--problem", problem, "--pop", "65536")

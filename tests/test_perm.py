@@ -206,3 +206,51 @@ def test_cpu_rank_selection_tsp():
     ga.run(30)
     assert ga.best_score() > s0
     assert is_perm(ga.genomes())
+
+
+def _forged_rows(ga, n):
+    """k rows of a TSP island: valid tours, then three forgeries (every gene
+    city 0; a duplicated city; a city beyond the tour)."""
+    k = 8
+    rows = ga.rows[:k].clone()
+    g16 = rows.view(torch.int16)
+    g16[0, :n] = 0
+    g16[1, :n] = torch.arange(n, dtype=torch.int16)
+    g16[1, n // 2] = 1
+    g16[2, :n] = torch.arange(n, dtype=torch.int16)
+    g16[2, n - 1] = n + 3
+    return rows.reshape(-1), torch.full((k,), 1e9)
+
+
+@pytest.mark.parametrize("n", [9, 64, 257])
+def test_evaluate_rows_sanitizes_forged_cpu(n):
+    """Island.evaluate_rows (the migrants' re-scoring) turns a row that is
+    not a permutation into the identity tour, scored as one; valid rows keep
+    their genes and get their true score."""
+    p = M.TSP.random_euclidean(n, seed=1)
+    ga = pga.GeneticAlgorithm(p, 64, seed=3, device="cpu")
+    rows, sc = _forged_rows(ga, n)
+    orig = ga.rows[:8].clone()
+    ga.island.evaluate_rows(rows, sc)
+    genes = p.decode(rows.view(8, -1))
+    ident = torch.arange(n)
+    for i in range(3):
+        assert torch.equal(genes[i], ident)
+    assert torch.equal(rows.view(8, -1)[3:], orig[3:])
+    assert torch.allclose(sc, p.reference_fitness(genes), rtol=1e-5, atol=1e-3)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n", [9, 64, 257, 1000])
+def test_evaluate_rows_sanitizes_forged_gpu(n):
+    """The same on gfx950 (perm.hip MODE_EVAL), bit-exact with the CPU backend."""
+    p = M.TSP.random_euclidean(n, seed=1)
+    c = pga.GeneticAlgorithm(p, 64, seed=3, device="cpu")
+    g = pga.GeneticAlgorithm(p, 64, seed=3, device="cuda:0")
+    rc, sc = _forged_rows(c, n)
+    rg, sg = rc.clone().cuda(), sc.clone().cuda()
+    c.island.evaluate_rows(rc, sc)
+    g.island.evaluate_rows(rg, sg)
+    torch.cuda.synchronize()
+    assert torch.equal(rg.cpu(), rc) and torch.equal(sg.cpu(), sc)
+    assert torch.equal(p.decode(rc.view(8, -1))[0], torch.arange(n))
