@@ -23,10 +23,22 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import libpga_amd as pga  # noqa: E402
 
 
+def problem(name):
+    """PGA_MIG_PROBLEM: onemax (default), rastrigin30, tsp256 (bench.py's configs)."""
+    if name == "rastrigin30":
+        return pga.models.Rastrigin(30), 1 << 20
+    if name == "tsp256":
+        g = torch.Generator().manual_seed(7)
+        xy = torch.rand(256, 2, generator=g)
+        return pga.models.TSP(torch.cdist(xy, xy, compute_mode="donot_use_mm_for_euclid_dist")), 1 << 18
+    return pga.models.OneMax(1024), 1 << 20
+
+
 def main():
-    S = int(sys.argv[1]) if len(sys.argv) > 1 else 1 << 20
+    prob, S = problem(os.environ.get("PGA_MIG_PROBLEM", "onemax"))
+    S = int(sys.argv[1]) if len(sys.argv) > 1 else S
     pct = float(sys.argv[2]) if len(sys.argv) > 2 else 0.01
-    ga = pga.GeneticAlgorithm(pga.models.OneMax(1024), S, seed=1, device="cuda:0", elitism=1)
+    ga = pga.GeneticAlgorithm(prob, S, seed=1, device="cuda:0", elitism=1)
     ga.run(20)
     isl = ga.island
     k = int(round(pct * S))
@@ -72,7 +84,7 @@ def main():
     # island model adds every migrate_every generations)
     res["epoch_device_nofused_us"] = res["epoch_gen_nofused_us"] - res["generation_us"]
     res["epoch_device_fused_us"] = res["epoch_gen_fused_us"] - res["generation_fused_us"]
-    res.update(pop=S, k=k)
+    res.update(pop=S, k=k, problem=os.environ.get("PGA_MIG_PROBLEM", "onemax"))
     emit(res)
 
 

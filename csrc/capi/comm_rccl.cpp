@@ -71,6 +71,7 @@ class RcclComm final : public Comm {
   int size() const override { return n_; }
   const char* name() const override { return all_ ? "rccl-all" : "rccl"; }
   bool drives_all_ranks() const override { return all_; }
+  hipStream_t transport_stream(const LocalRank& l) override { return streams_[ensure_stream(l)]; }
 
   void set_fault(int every, int mode) override {
     if (mode != 0 && mode != 3 && mode != 4)
@@ -251,7 +252,10 @@ class RcclComm final : public Comm {
       if (done) return true;
       const double dt = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
       if (dt > timeout_s) return false;
-      std::this_thread::sleep_for(std::chrono::microseconds(50));
+      // spin the first 2 ms (a transfer usually lands within a generation:
+      // the next launch should follow it within microseconds, and a sleep
+      // costs a scheduler tick), then back off
+      if (dt > 2e-3) std::this_thread::sleep_for(std::chrono::microseconds(20));
     }
   }
   size_t slot_of(int rank) const {

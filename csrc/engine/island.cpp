@@ -250,17 +250,15 @@ void Island::prepare_objective() {
       std::memcpy(t.data() + o, &v, sizeof(v));
     };
     if (ints && sym) {
-      for (uint32_t i = 1; i < L; ++i)
-        for (uint32_t j = 0; j < i; ++j) put((uint16_t)d[(size_t)i * L + j]);
-      for (uint32_t i = 0; i < L; ++i) put((uint16_t)d[(size_t)i * L + i]);
+      for (uint32_t i = 0; i < L; ++i)  // rows of the lower triangle with the diagonal: (i, j <= i) at i (i + 1) / 2 + j
+        for (uint32_t j = 0; j <= i; ++j) put((uint16_t)d[(size_t)i * L + j]);
       aux_kind_ = 1;
     } else if (ints && 2ull * L * L <= lds) {
       for (size_t i = 0; i < (size_t)L * L; ++i) put((uint16_t)d[i]);
       aux_kind_ = 2;
     } else if (sym && !ints && 4 * tri <= lds) {
-      for (uint32_t i = 1; i < L; ++i)
-        for (uint32_t j = 0; j < i; ++j) put(d[(size_t)i * L + j]);
-      for (uint32_t i = 0; i < L; ++i) put(d[(size_t)i * L + i]);
+      for (uint32_t i = 0; i < L; ++i)
+        for (uint32_t j = 0; j <= i; ++j) put(d[(size_t)i * L + j]);
       aux_kind_ = 3;
     }
     if (aux_kind_) {

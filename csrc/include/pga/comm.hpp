@@ -101,6 +101,15 @@ class Comm {
   // complete, or stalls (4) every `every`-th all-gather behind a receive
   // that never completes.  Mode 0 disarms it.
   virtual void set_fault(int every, int mode) = 0;
+  // the stream this communicator moves `l`'s data on (RCCL: the rank's own
+  // communication stream, concurrent with the compute stream), or nullptr
+  // when the transport has none.  Work enqueued there runs in order with the
+  // transfers: the engine island model packs its emigrants and re-scores its
+  // immigrants on it, beside the generation kernel.
+  virtual hipStream_t transport_stream(const LocalRank& l) {
+    (void)l;
+    return nullptr;
+  }
   // test-only (pga_comm_set_self_exchange): a 1-rank communicator normally
   // skips migration; with this set it exchanges with itself, which runs the
   // real transport (and the fault injection) on one GPU

@@ -39,9 +39,6 @@ constexpr uint16_t kNone = 0xFFFF;
 #ifndef PGA_PERM_NOXO
 #define PGA_PERM_NOXO 0
 #endif
-#ifndef PGA_PERM_CHAIN  // PMX chains: 0 first links batched, 3 one gene after another, 1/2 a lane's 8 together
-#define PGA_PERM_CHAIN 0
-#endif
 #ifndef PGA_PERM_PF  // parent rows one step ahead
 #define PGA_PERM_PF 1
 #endif
@@ -362,6 +359,28 @@ __device__ __forceinline__ uint4 set16(uint4 v, uint32_t e, uint32_t x) {
   return v;
 }
 
+// bit e set when position base + e lies in [a, b) (a lane's 8 genes)
+__device__ __forceinline__ uint32_t range8(uint32_t base, uint32_t a, uint32_t b) {
+  const uint32_t lo = a > base ? min(a - base, 8u) : 0u;
+  const uint32_t hi = b > base ? min(b - base, 8u) : 0u;
+  return ((1u << hi) - 1u) & ~((1u << lo) - 1u);
+}
+// 8 gene bits -> the 16-bit lanes of a packed chunk (0xFFFF where set)
+__device__ __forceinline__ uint4 mask16x8(uint32_t m) {
+  const auto w = [m](uint32_t i) {
+    return (((m >> (2 * i)) & 1u) ? 0xFFFFu : 0u) | (((m >> (2 * i + 1)) & 1u) ? 0xFFFF0000u : 0u);
+  };
+  return make_uint4(w(0), w(1), w(2), w(3));
+}
+// per 16-bit lane: a where the mask is set, else b (v_bfi_b32)
+__device__ __forceinline__ uint4 bfi4(const uint4& m, const uint4& a, const uint4& b) {
+  return make_uint4((a.x & m.x) | (b.x & ~m.x), (a.y & m.y) | (b.y & ~m.y), (a.z & m.z) | (b.z & ~m.z),
+                    (a.w & m.w) | (b.w & ~m.w));
+}
+__device__ __forceinline__ uint4 pack16x8(const uint32_t v[8]) {
+  return make_uint4(v[0] | (v[1] << 16), v[2] | (v[3] << 16), v[4] | (v[5] << 16), v[6] | (v[7] << 16));
+}
+
 // One lane's view of its own child's ST_CHILD words (the pool's words, core.hpp
 // child_word): blocks 1 and 2 hold the selection words W_SEL .. W_SEL + 3 of
 // tournament-2, roulette and uniform selection; other words are drawn on demand
@@ -386,18 +405,22 @@ __host__ __device__ inline size_t perm_fast_lds_bytes(uint32_t GS, uint32_t chun
 
 // TBL (the launcher's choice from GenArgs::obj_aux): the distance matrix in
 // LDS (staged once per block) instead of an f32 L2 gather per edge — 1 = a
-// symmetric integer matrix's strict lower triangle plus its diagonal as u16
-// (65 KB at L = 256), 2 = a full integer matrix as u16, 3 = a symmetric f32
-// matrix's triangle plus diagonal as f32 (131.6 KB at L = 256: the 16 waves
-// of a CU share one).  Entries are the matrix's own values, so the tour sums
+// symmetric integer matrix's lower triangle with the diagonal as u16, row by
+// row (entry (i, j <= i) at i (i + 1) / 2 + j; 65 KB at L = 256), 2 = a full
+// integer matrix as u16, 3 = a symmetric f32 matrix's lower triangle with the
+// diagonal as f32 (131.6 KB at L = 256: the 16 waves of a CU share one).  Entries are the matrix's own values, so the tour sums
 // equal the f32 L2 path's bit for bit.
-template <int GS, int OBJ, int TBL = 0>
+// FULL (the launcher's choice when L = 8 GS: every lane holds a whole chunk,
+// no padding): the lane masks below fold to constants, L is a compile-time
+// constant, and for L <= 256 the tour's triangle indices are computed two
+// edges per packed 16-bit instruction.
+template <int GS, int OBJ, int TBL = 0, bool FULL = false>
 __device__ __forceinline__ void perm_gen_fast_body(GenArgs a, unsigned long long* best_parts) {
   resolve_gen(a);
   float* smem = (float*)pga_dyn_lds;
   unsigned long long* lds_red = (unsigned long long*)smem;  // 16 entries: kHdrF holds them
   uint32_t* lds_elite = (uint32_t*)(smem + 32);
-  const uint32_t L = a.L, nch = a.chunks, lp = 8 * nch;
+  const uint32_t L = FULL ? 8u * GS : a.L, nch = FULL ? (uint32_t)GS : a.chunks, lp = 8 * nch;
   const uint32_t BLK = blockDim.x, NWv = BLK >> 6;
   constexpr uint32_t NG = 64 / GS;  // children per wave per step
   float* coords = smem + kHdrF;
@@ -406,23 +429,34 @@ __device__ __forceinline__ void perm_gen_fast_body(GenArgs a, unsigned long long
   // the table after the groups' arrays (16-byte aligned: gbytes is a multiple of 16)
   const uint16_t* tab = (const uint16_t*)(arena + (size_t)(BLK / GS) * gbytes);
   const float* ftab = (const float*)tab;
-  const uint32_t tri = L * (L - 1) / 2;  // TBL 1, 3: the diagonal's offset
 
   const uint32_t lane = lane_id();
   const uint32_t q = lane & (GS - 1);
   const uint32_t gbase = lane & ~(uint32_t)(GS - 1);
   const uint32_t g = lane / GS;
-  uint16_t* Cc = (uint16_t*)(arena + (size_t)(threadIdx.x / GS) * gbytes);  // PMX: T, then the child
-  uint32_t* bits = (uint32_t*)((char*)Cc + 16u * nch);                      // OX membership
+  uint16_t* Cc = (uint16_t*)(arena + (size_t)(threadIdx.x / GS) * gbytes);  // PMX: T; OX: A's inverse; then the child
   const uint64_t rs = a.row_words >> 2;
   const uint4* cur = (const uint4*)a.cur;
   uint4* nxt = (uint4*)a.next;
-  const bool have = q < nch;
+  const bool have = FULL || q < nch;
   const uint32_t qc = have ? q : nch - 1;
   const bool mut_on = a.mutation == MUT_SWAP || a.mutation == MUT_INVERSION;
   const bool xo_kind = a.crossover == XO_PMX || a.crossover == XO_OX;
   const bool pmx = a.crossover == XO_PMX;
   const uint32_t S32 = (uint32_t)a.S;
+  // the lane's genes (bit e: position 8 q + e), loop-invariant: padding
+  // positions (all 8 for a lane without a chunk), the gene at position L - 1
+  // (its successor is the tour's first city), genes whose edge counts
+  // (FULL: no padding, and the last lane's successor lane is the group's
+  // first, so the closing edge needs no select)
+  const uint32_t base = 8u * q;
+  const uint32_t padm8 = FULL ? 0u : (have ? range8(base, L, lp) : 0xFFu);
+  const uint32_t wrapm8 = FULL ? 0u : (have ? range8(base, L - 1, L) : 0u);
+  const uint32_t edgem8 = FULL ? (OBJ == OBJ_TSP_OPEN && q == GS - 1 ? 0x7Fu : 0xFFu)
+                               : (have ? range8(base, 0, OBJ == OBJ_TSP_OPEN ? L - 1 : L) : 0u);
+  // the LDS slot a padding gene writes instead of a city's (its own padding
+  // position; a lane without a chunk: the group's spare words after C)
+  const uint32_t dslot = have ? base : lp;
 
   if (a.n_elite > 0 && a.elite_idx == nullptr && blockIdx.x == 0) {
     unsigned long long b = block_reduce_parts_n(a.best_cur, a.n_best_cur, lds_red, NWv);
@@ -503,119 +537,77 @@ __device__ __forceinline__ void perm_gen_fast_body(GenArgs a, unsigned long long
       if (elite) score = a.score_cur[pa];
 
       if (xo) {  // group-uniform
+        // Branch-free per gene: every LDS access of the 8 genes is issued
+        // unconditionally (a gene with nothing to write writes a slot the
+        // result never reads), and the child is assembled with bit selects.
+        // seg8: the lane's genes inside A's segment; from A: segment and padding
+        const uint32_t seg8 = range8(base, lo, hi);
+        const uint4 fromA = mask16x8(seg8 | padm8);
         if (pmx) {
-          // T[city] = the city PMX replaces it by: B's gene at the city's
-          // position in A's segment (kNone outside it); a gene of B outside
-          // the segment follows T until it leaves A's segment
+          // T[city] = B's gene at the city's position in A's segment, kNone
+          // elsewhere: A holds every city once, so T needs no clearing
           uint16_t* T = Cc;
-          if (have) *(uint4*)(T + 8 * q) = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu);
-          wave_sync();
 #pragma unroll
           for (uint32_t e = 0; e < 8; ++e) {
-            const uint32_t k = 8 * q + e;
-            if (have && k >= lo && k < hi) T[min(get16(Av, e), lp - 1)] = (uint16_t)get16(Bv, e);
+            const uint32_t ta = ((padm8 >> e) & 1u) ? dslot + e : min(get16(Av, e), lp - 1);
+            T[ta] = (uint16_t)(((seg8 >> e) & 1u) ? get16(Bv, e) : (uint32_t)kNone);
           }
           wave_sync();
-#if PGA_PERM_CHAIN == 0
-          // the first link of all 8 genes in one batch of LDS reads (most
-          // genes of B are not in A's segment: their chain ends there), the
-          // rest of each chain one gene after another; a chain takes at most
-          // L links
-          uint32_t y0[8];
+          // a gene of B outside the segment follows T until it leaves A's
+          // segment (at most L links); the first link of all 8 in one batch
+          uint32_t y0[8], v[8];
 #pragma unroll
           for (uint32_t e = 0; e < 8; ++e) y0[e] = T[min(get16(Bv, e), lp - 1)];
 #pragma unroll
           for (uint32_t e = 0; e < 8; ++e) {
-            const uint32_t p = 8 * q + e;
-            uint32_t v = get16(Bv, e);
-            if (p < L && !(p >= lo && p < hi)) {
+            v[e] = get16(Bv, e);
+            if (!(((seg8 | padm8) >> e) & 1u)) {
               uint32_t y = y0[e];
               for (uint32_t guard = 0; y != kNone && guard < L;) {
-                v = y;
+                v[e] = y;
                 if (++guard >= L) break;
-                y = T[min(v, lp - 1)];
+                y = T[min(v[e], lp - 1)];
               }
             }
-            Cv = set16(Cv, e, p >= L ? 0u : ((p >= lo && p < hi) ? get16(Av, e) : v));
           }
-#elif PGA_PERM_CHAIN == 3  // one gene after another (round 4's form)
+          Cv = bfi4(fromA, Av, pack16x8(v));
+        } else {  // OX1 (the ranks of perm_kernel): Cc first holds A's inverse, then the child
 #pragma unroll
           for (uint32_t e = 0; e < 8; ++e) {
-            const uint32_t p = 8 * q + e;
-            uint32_t v = get16(Bv, e);
-            if (p < L && !(p >= lo && p < hi))
-              for (uint32_t guard = 0; guard < L; ++guard) {
-                const uint32_t w = T[min(v, lp - 1)];
-                if (w == kNone) break;
-                v = w;
-              }
-            Cv = set16(Cv, e, p >= L ? 0u : ((p >= lo && p < hi) ? get16(Av, e) : v));
-          }
-#else
-          // the lane's 8 chains advance together (8 independent LDS reads per
-          // step instead of 8 loops each as long as the wave's longest
-          // chain); each chain still takes at most L steps
-          uint32_t v[8], act = 0;
-#pragma unroll
-          for (uint32_t e = 0; e < 8; ++e) {
-            const uint32_t p = 8 * q + e;
-            v[e] = get16(Bv, e);
-            act |= (p < L && !(p >= lo && p < hi)) ? 1u << e : 0u;
-          }
-          for (uint32_t guard = 0; act != 0u && guard < L; ++guard) {
-            uint32_t w[8];
-#pragma unroll
-            for (uint32_t e = 0; e < 8; ++e)
-              w[e] = (PGA_PERM_CHAIN == 2 || ((act >> e) & 1u)) ? (uint32_t)T[min(v[e], lp - 1)] : (uint32_t)kNone;
-#pragma unroll
-            for (uint32_t e = 0; e < 8; ++e) {
-              const bool adv = ((act >> e) & 1u) && w[e] != kNone;
-              v[e] = adv ? w[e] : v[e];
-              act = adv ? act : act & ~(1u << e);
-            }
-          }
-#pragma unroll
-          for (uint32_t e = 0; e < 8; ++e) {
-            const uint32_t p = 8 * q + e;
-            Cv = set16(Cv, e, p >= L ? 0u : ((p >= lo && p < hi) ? get16(Av, e) : v[e]));
-          }
-#endif
-        } else {  // OX1 (same ranks as perm_kernel); membership of A's segment as bits
-          if (q < (nch + 3) / 4) bits[q] = 0u;
-          wave_sync();
-#pragma unroll
-          for (uint32_t e = 0; e < 8; ++e) {
-            const uint32_t k = 8 * q + e, c = get16(Av, e);
-            if (have && k >= lo && k < hi)
-              __hip_atomic_fetch_or(&bits[(c >> 5) & 15u], 1u << (c & 31u), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+            const uint32_t ia = ((padm8 >> e) & 1u) ? dslot + e : min(get16(Av, e), lp - 1);
+            Cc[ia] = (uint16_t)(base + e);  // city -> its position in A
           }
           wave_sync();
-          uint32_t keep = 0, eb_part = 0;
+          uint32_t pa8[8];
 #pragma unroll
-          for (uint32_t e = 0; e < 8; ++e) {
-            const uint32_t p = 8 * q + e, c = get16(Bv, e);
-            const bool k = have && p < L && !((bits[(c >> 5) & 15u] >> (c & 31u)) & 1u);
-            keep |= k ? (1u << e) : 0u;
-            eb_part += (k && p < hi) ? 1u : 0u;
-          }
-          const uint32_t Eb = group_sum_u<GS>(eb_part);
-          const uint32_t K = L - (hi - lo), tail = L - hi;
+          for (uint32_t e = 0; e < 8; ++e) pa8[e] = Cc[min(get16(Bv, e), lp - 1)];
+          // keep: B's genes outside A's segment, in B order
+          uint32_t keep = 0;
+#pragma unroll
+          for (uint32_t e = 0; e < 8; ++e)
+            keep |= (!((padm8 >> e) & 1u) && pa8[e] - lo >= hi - lo) ? (1u << e) : 0u;
+          const uint32_t below = range8(base, 0, hi);  // B positions before the segment end
+          const uint32_t Eb = group_sum_u<GS>(__popc(keep & below));
+          const uint32_t K = L - (hi - lo);
           uint32_t seg_total;
           uint32_t run = group_excl_scan<GS>(__popc(keep), q, seg_total);
+          wave_sync();  // every read of A's inverse is done before the child overwrites it
+          // kept gene of rank r (B order from position 0) -> child position
+          // hi + ((r - Eb) mod K), wrapped at L; a gene not kept writes the
+          // slot lo + (its rank among those), inside the segment, which the
+          // result takes from A (padding: its own padding slot)
 #pragma unroll
           for (uint32_t e = 0; e < 8; ++e) {
-            const uint32_t p = 8 * q + e;
-            if (have && p >= L) Cc[p] = 0;
-            if (have && p < L && p >= lo && p < hi) Cc[p] = (uint16_t)get16(Av, e);
-            if ((keep >> e) & 1u) {
-              const uint32_t r = p >= hi ? run - Eb : (K - Eb) + run;
-              const uint32_t pos = r < tail ? hi + r : r - tail;
-              Cc[pos] = (uint16_t)get16(Bv, e);
-              ++run;
-            }
+            const uint32_t p = base + e;
+            uint32_t x = run + hi - Eb + (((below >> e) & 1u) ? K : 0u);
+            x = min(x, x - L);  // x mod L (x < 2 L): the unsigned wrap of x - L loses the min below L
+            const uint32_t d = ((padm8 >> e) & 1u) ? dslot + e : lo + (p - run);
+            const bool k = (keep >> e) & 1u;
+            Cc[k ? x : d] = (uint16_t)get16(Bv, e);
+            run += k ? 1u : 0u;
           }
           wave_sync();
-          Cv = *(const uint4*)(Cc + 8 * qc);
+          Cv = bfi4(fromA, Av, *(const uint4*)(Cc + 8 * qc));
         }
       }
 
@@ -643,51 +635,73 @@ __device__ __forceinline__ void perm_gen_fast_body(GenArgs a, unsigned long long
         wave_sync();
         Cv = *(const uint4*)(Cc + 8 * qc);
       }
-      wave_sync();  // the next child of this group rewrites C / T / bits
+      wave_sync();  // the next child of this group rewrites C / T
 
       if (valid && have) nxt[(uint64_t)child * rs + q] = Cv;
       if (!elite && !PGA_PERM_NOEVAL) {
-        // edges (p, p+1) and the closing edge; the city after a lane's chunk is
-        // the next lane's first city
+        // edge of gene e: to gene e + 1, the next lane's first city (e = 7),
+        // or the tour's first city (position L - 1); every lookup of the 8
+        // issued before the sum, which keeps perm_kernel's order (e = 0..7
+        // from 0.f, then the butterfly)
         const uint32_t c0 = Cv.x & 0xFFFFu;
         const uint32_t next_first = (uint32_t)__shfl((int)c0, (int)(gbase + ((q + 1) & (GS - 1))), 64);
         const uint32_t first = (uint32_t)__shfl((int)c0, (int)gbase, 64);
-        const uint32_t last = (OBJ == OBJ_TSP_OPEN) ? L - 1 : L;
-        float len = 0.f;
+        uint32_t u[8], w[8];
+#pragma unroll
+        for (uint32_t e = 0; e < 8; ++e) {
+          const uint32_t nx = ((wrapm8 >> e) & 1u) ? first : (e < 7 ? get16(Cv, e + 1) : next_first);
+          u[e] = min(get16(Cv, e), L - 1);
+          w[e] = min(nx, L - 1);
+        }
+        float dv[8];
         if (OBJ == OBJ_TSP_EUC) {
-          // one float2 per city of the chunk (+ the following city), reused by both edge ends
           const float2* xy = (const float2*)coords;
-          float2 pu = xy[min(get16(Cv, 0), L - 1)];
 #pragma unroll
           for (uint32_t e = 0; e < 8; ++e) {
-            const uint32_t p = 8 * q + e;
-            const uint32_t nx = p + 1 < L ? (e < 7 ? get16(Cv, e + 1) : next_first) : first;
-            const float2 pw = xy[min(nx, L - 1)];
-            if (have && p < last) {
-              const float dx = pu.x - pw.x, dy = pu.y - pw.y;
-              len += sqrtf(fmaf(dx, dx, dy * dy));
-            }
-            pu = pw;
+            const float2 pu = xy[u[e]], pw = xy[w[e]];
+            const float dx = pu.x - pw.x, dy = pu.y - pw.y;
+            dv[e] = sqrtf(fmaf(dx, dx, dy * dy));
+          }
+        } else if constexpr (FULL && GS <= 32 && (TBL == 1 || TBL == 3)) {
+          // L <= 256: hi (hi + 1) <= 65280 fits 16 bits, so each pair of
+          // edges takes one packed clamp / max / min / multiply-add / shift /
+          // add; (hi, lo) of edge e is (max, min) of gene e and its successor
+          using us2 = unsigned short __attribute__((ext_vector_type(2)));
+          const us2 lm = {(unsigned short)(L - 1), (unsigned short)(L - 1)};
+          const uint32_t wv[4] = {Cv.x, Cv.y, Cv.z, Cv.w};
+          uint32_t gw[4];
+#pragma unroll
+          for (uint32_t i = 0; i < 4; ++i)
+            gw[i] = __builtin_bit_cast(uint32_t, __builtin_elementwise_min(__builtin_bit_cast(us2, wv[i]), lm));
+          const uint32_t nf = min(next_first, L - 1);
+#pragma unroll
+          for (uint32_t i = 0; i < 4; ++i) {
+            const uint32_t sw = i < 3 ? __builtin_amdgcn_alignbit(gw[i + 1], gw[i], 16) : ((gw[3] >> 16) | (nf << 16));
+            const us2 a2 = __builtin_bit_cast(us2, gw[i]), b2 = __builtin_bit_cast(us2, sw);
+            const us2 h2 = __builtin_elementwise_max(a2, b2), l2 = __builtin_elementwise_min(a2, b2);
+            const uint32_t ix = __builtin_bit_cast(uint32_t, ((us2)(h2 * h2 + h2) >> (us2){1, 1}) + l2);
+            dv[2 * i] = TBL == 1 ? (float)tab[ix & 0xFFFFu] : ftab[ix & 0xFFFFu];
+            dv[2 * i + 1] = TBL == 1 ? (float)tab[ix >> 16] : ftab[ix >> 16];
           }
         } else {
 #pragma unroll
           for (uint32_t e = 0; e < 8; ++e) {
-            const uint32_t p = 8 * q + e;
-            if (have && p < last) {
-              const uint32_t nx = p + 1 < L ? (e < 7 ? get16(Cv, e + 1) : next_first) : first;
-              const uint32_t u = min(get16(Cv, e), L - 1), w = min(nx, L - 1);
-              if constexpr (TBL == 1 || TBL == 3) {
-                const uint32_t hi_ = u > w ? u : w, lo_ = u > w ? w : u;
-                const uint32_t ix = hi_ == lo_ ? tri + u : hi_ * (hi_ - 1) / 2 + lo_;
-                len += TBL == 1 ? (float)tab[ix] : ftab[ix];
-              } else if constexpr (TBL == 2) {
-                len += (float)tab[u * L + w];
-              } else {
-                len += a.obj_data[u * L + w];
-              }
+            if constexpr (TBL == 1 || TBL == 3) {
+              // rows of the lower triangle with the diagonal: (hi, lo) at hi (hi + 1) / 2 + lo
+              const uint32_t hi_ = max(u[e], w[e]), lo_ = min(u[e], w[e]);
+              const uint32_t ix = (__umul24(hi_, hi_ + 1u) >> 1) + lo_;
+              dv[e] = TBL == 1 ? (float)tab[ix] : ftab[ix];
+            } else if constexpr (TBL == 2) {
+              dv[e] = (float)tab[__umul24(u[e], L) + w[e]];
+            } else {
+              dv[e] = a.obj_data[u[e] * L + w[e]];
             }
           }
         }
+        float len = 0.f;
+#pragma unroll
+        for (uint32_t e = 0; e < 8; ++e)
+          if ((edgem8 >> e) & 1u) len += dv[e];
         score = -group_sum<GS>(len);
       }
       if (valid && q == 0) {
@@ -707,9 +721,9 @@ __device__ __forceinline__ void perm_gen_fast_body(GenArgs a, unsigned long long
 
 // the LDS-table variants launch up to 1024 threads (one table per CU); the L2
 // path and the batch kernel launch kBlock, so they keep kBlock's register cap
-template <int GS, int OBJ, int TBL = 0>
+template <int GS, int OBJ, int TBL = 0, bool FULL = false>
 __global__ __launch_bounds__(TBL ? 1024 : kBlock) void perm_gen_fast(GenArgs a, unsigned long long* best_parts) {
-  perm_gen_fast_body<GS, OBJ, TBL>(a, best_parts);
+  perm_gen_fast_body<GS, OBJ, TBL, FULL>(a, best_parts);
 }
 
 // Batched islands: up to kPermMaxBatch same-shape islands in ONE launch,
@@ -785,13 +799,13 @@ inline bool perm_tbl_on(const GenArgs& a) {
   return a.crossover != XO_PMX || pmx_tbl;
 }
 
-template <int GS, int OBJ, int TBL>
+template <int GS, int OBJ, int TBL, bool FULL>
 uint32_t go_fast_blk(const GenArgs& a0, unsigned long long* parts, hipStream_t s, uint32_t blk) {
   const size_t lds = perm_fast_lds_bytes(GS, a0.chunks, OBJ == OBJ_TSP_EUC, blk) + (TBL ? a0.obj_aux_bytes : 0);
-  auto k = perm_gen_fast<GS, OBJ, TBL>;
+  auto k = perm_gen_fast<GS, OBJ, TBL, FULL>;
   const size_t avail = allow_dynamic_lds((const void*)k);
   if constexpr (TBL != 0) {  // the table did not fit this device's limit: the L2 matrix path
-    if (lds > avail) return go_fast_blk<GS, OBJ, 0>(a0, parts, s, kBlock);
+    if (lds > avail) return go_fast_blk<GS, OBJ, 0, FULL>(a0, parts, s, kBlock);
   }
   int per_cu = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)k, (int)blk, lds) != hipSuccess || per_cu <= 0)
@@ -807,8 +821,8 @@ uint32_t go_fast_blk(const GenArgs& a0, unsigned long long* parts, hipStream_t s
   return grid;
 }
 
-template <int GS, int OBJ>
-uint32_t go_fast(const GenArgs& a, unsigned long long* parts, hipStream_t s) {
+template <int GS, int OBJ, bool FULL>
+uint32_t go_fast_tbl(const GenArgs& a, unsigned long long* parts, hipStream_t s) {
   if constexpr (OBJ == OBJ_TSP || OBJ == OBJ_TSP_OPEN) {
     // the matrix in LDS (obj_aux): the largest block (up to 16 waves, one
     // table per CU) whose group arrays fit beside it
@@ -821,13 +835,24 @@ uint32_t go_fast(const GenArgs& a, unsigned long long* parts, hipStream_t s) {
       const uint32_t order[3] = {big ? 1024u : 256u, 512u, big ? 256u : 1024u};
       for (uint32_t blk : order) {
         if (perm_fast_lds_bytes(GS, a.chunks, false, blk) + a.obj_aux_bytes > avail) continue;
-        if (a.obj_aux_kind == 1) return go_fast_blk<GS, OBJ, 1>(a, parts, s, blk);
-        if (a.obj_aux_kind == 2) return go_fast_blk<GS, OBJ, 2>(a, parts, s, blk);
-        return go_fast_blk<GS, OBJ, 3>(a, parts, s, blk);
+        if (a.obj_aux_kind == 1) return go_fast_blk<GS, OBJ, 1, FULL>(a, parts, s, blk);
+        if (a.obj_aux_kind == 2) return go_fast_blk<GS, OBJ, 2, FULL>(a, parts, s, blk);
+        return go_fast_blk<GS, OBJ, 3, FULL>(a, parts, s, blk);
       }
     }
   }
-  return go_fast_blk<GS, OBJ, 0>(a, parts, s, kBlock);
+  return go_fast_blk<GS, OBJ, 0, FULL>(a, parts, s, kBlock);
+}
+
+template <int GS, int OBJ>
+uint32_t go_fast(const GenArgs& a, unsigned long long* parts, hipStream_t s) {
+  // whole chunks on every lane (L = 8 GS: TSP-64 / 128 / 256 / 512): the FULL variants
+  if constexpr (GS >= 8) {
+    static const bool off = std::getenv("PGA_PERM_NO_FULL") != nullptr;  // A/B runs: the general variants
+    if (a.L == 8u * GS && a.chunks == (uint32_t)GS && !off)
+      return go_fast_tbl<GS, OBJ, true>(a, parts, s);
+  }
+  return go_fast_tbl<GS, OBJ, false>(a, parts, s);
 }
 
 template <int GS, int OBJ>

@@ -504,7 +504,11 @@ __device__ __forceinline__ uint32_t load_keys16(const uint16_t* k16, uint64_t c0
   return m;
 }
 
-constexpr uint32_t kTopkMoveSlots = 4096;  // selections per block listed in LDS for the cooperative row move
+// selections per block listed in LDS for the cooperative row move (a
+// migration's k / blocks is ~41 at the headline; more go row by row).  Small:
+// with ~9 KB of LDS the selections fit beside a generation kernel's block
+// (120 KB), so one on the transport stream runs concurrently with it.
+constexpr uint32_t kTopkMoveSlots = 1024;
 
 // What the fused selection does with the i-th selected individual at output
 // position pos (besides idx_out[pos] = i when idx_out is set):
@@ -713,7 +717,6 @@ __global__ __launch_bounds__(kBlock) void topk16_select_kernel(const uint16_t* k
                                                                uint32_t R, bool largest, uint32_t k, uint32_t* G,
                                                                uint64_t* status, uint32_t* ctr, uint32_t nblocks,
                                                                uint32_t* idx_out, TopkMove mv, bool fused) {
-  __shared__ uint32_t gl[kTopkMaxRange];  // this block's copy of the histogram
   __shared__ uint32_t sel_pos[kTopkMoveSlots], sel_src[kTopkMoveSlots];  // row moves: output position, source
   __shared__ uint32_t sh_T, sh_need, sh_b;
   __shared__ uint32_t lds[kBlock / 64];
@@ -723,20 +726,16 @@ __global__ __launch_bounds__(kBlock) void topk16_select_kernel(const uint16_t* k
   uint32_t mine = 0;
   for (uint32_t j = 0; j < per; ++j) {
     const int64_t b = (int64_t)R - 1 - (int64_t)threadIdx.x * per - j;
-    if (b >= 0) {
-      const uint32_t c = G[fused && !largest ? R - 1 - b : b];
-      gl[b] = c;  // re-read below by this same thread only
-      mine += c;
-    }
+    if (b >= 0) mine += G[fused && !largest ? R - 1 - b : b];
   }
   uint32_t tot;
   const uint32_t before = block_excl_scan_u(mine, lds, tot);
-  if (before < k && before + mine >= k) {
+  if (before < k && before + mine >= k) {  // the one thread holding the threshold re-reads its bins
     uint32_t acc = before;
     for (uint32_t j = 0; j < per; ++j) {
       const int64_t b = (int64_t)R - 1 - (int64_t)threadIdx.x * per - j;
       if (b < 0) break;
-      const uint32_t c = gl[b];
+      const uint32_t c = G[fused && !largest ? R - 1 - b : b];
       if (acc + c >= k) {
         sh_T = (uint32_t)b;
         sh_need = k - acc;
@@ -878,6 +877,290 @@ __global__ __launch_bounds__(kBlock) void topk16_select_kernel(const uint16_t* k
         mv.dst_scores[i] = v;
         if (mv.dst_keys) mv.dst_keys[i] = (uint16_t)(!(v > 0.f) ? 0.f : (v >= 65535.f ? 65535.f : v));
       }
+    }
+  }
+}
+
+// ---- f32 scores: the exact top-k in selection order from three radix
+// digits of the 32-bit orderable keys (11 / 11 / 10 bits) and one ticketed
+// select: 4 launches per selection (the 8-bit radix path above takes 11, and
+// the gather / scatter / best passes after it 3 more).  Each histogram
+// kernel's blocks re-derive the previous digit's threshold from its global
+// histogram themselves (block 0 also records it for the next launch), so no
+// single-block digit kernels sit between the passes; the select kernel
+// derives the last digit, counts, orders (status words, as
+// topk16_select_kernel) and moves the rows.  Same result as topk_run: every
+// key above the threshold by index, then the first ties by index. ----
+constexpr uint32_t kT32R1 = 2048, kT32R2 = 2048, kT32R3 = 1024;  // digit bins: key >> 21, (key >> 10) & 2047, key & 1023
+constexpr uint32_t kT32State = kT32R1 + kT32R2 + kT32R3;         // G word offset of {T1, k2, T2, k3}
+
+// 16 keys of [c0, c0 + 16) clipped to end (float4 loads when whole and aligned)
+__device__ __forceinline__ uint32_t load_keys32(const float* s, uint64_t c0, uint64_t end, bool largest,
+                                                uint32_t (&kv)[16]) {
+  if (c0 + 16 <= end && (c0 & 3) == 0) {
+    float4 v[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[j] = *(const float4*)(s + c0 + 4 * j);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      kv[4 * j] = topk_key(v[j].x, largest);
+      kv[4 * j + 1] = topk_key(v[j].y, largest);
+      kv[4 * j + 2] = topk_key(v[j].z, largest);
+      kv[4 * j + 3] = topk_key(v[j].w, largest);
+    }
+    return 0xFFFFu;
+  }
+  uint32_t m = 0;
+#pragma unroll
+  for (int e = 0; e < 16; ++e) {
+    const bool ok = c0 + e < end;
+    kv[e] = ok ? topk_key(s[c0 + e], largest) : 0u;
+    m |= ok ? (1u << e) : 0u;
+  }
+  return m;
+}
+
+// the threshold bin of R (from the top: the bin where the count of keys in
+// higher bins first reaches k) and the k left for it; block-wide, every
+// thread returns the same.  G: R global counts.
+__device__ __forceinline__ void t32_threshold(const uint32_t* G, uint32_t R, uint32_t k, uint32_t* lds,
+                                              uint32_t* sh, uint32_t& T, uint32_t& rem) {
+  const uint32_t per = R / kBlock;  // 8 or 4
+  uint32_t c[8], mine = 0;
+#pragma unroll
+  for (uint32_t j = 0; j < 8; ++j) {
+    c[j] = j < per ? G[R - 1 - threadIdx.x * per - j] : 0u;
+    mine += c[j];
+  }
+  uint32_t tot;
+  const uint32_t before = block_excl_scan_u(mine, lds, tot);
+  if (before < k && before + mine >= k) {
+    uint32_t acc = before;
+#pragma unroll
+    for (uint32_t j = 0; j < 8; ++j) {
+      if (j < per && acc < k && acc + c[j] >= k) {
+        sh[0] = R - 1 - threadIdx.x * per - j;
+        sh[1] = k - acc;
+      }
+      acc += c[j];
+    }
+  }
+  if (threadIdx.x == 0 && tot < k) {  // k > S cannot happen (the launcher checks); keep bin 0
+    sh[0] = 0;
+    sh[1] = k;
+  }
+  __syncthreads();
+  T = sh[0];
+  rem = sh[1];
+}
+
+// histogram of digit `level` (1, 2, 3) over the keys whose higher digits
+// match the thresholds found so far; level 1 also zeroes the select's status
+// words and tickets
+__global__ __launch_bounds__(kBlock) void topk32_hist_kernel(const float* scores, uint64_t S, uint64_t per_block,
+                                                             bool largest, uint32_t k, uint32_t level, uint32_t* G,
+                                                             uint64_t* status, uint32_t n_status) {
+  __shared__ uint32_t h[kT32R1];
+  __shared__ uint32_t lds[kBlock / 64], sh[2];
+  const uint32_t R = level == 3 ? kT32R3 : kT32R1;
+  for (uint32_t i = threadIdx.x; i < R; i += kBlock) h[i] = 0;
+  uint32_t pfx = 0, pmask = 0, shift = 21, dmask = kT32R1 - 1;
+  if (level == 1) {
+    for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < n_status; i += gridDim.x * kBlock) status[i] = 0;
+    if (blockIdx.x == 0 && threadIdx.x < 2) ((uint32_t*)(status + n_status))[threadIdx.x] = 0;
+  } else {
+    uint32_t* st = G + kT32State;
+    uint32_t T1, k2;
+    if (level == 2) {
+      t32_threshold(G, kT32R1, k, lds, sh, T1, k2);
+      if (blockIdx.x == 0 && threadIdx.x == 0) {
+        st[0] = T1;
+        st[1] = k2;
+      }
+      pfx = T1 << 21;
+      pmask = 0xFFE00000u;
+      shift = 10;
+    } else {
+      T1 = st[0];
+      k2 = st[1];
+      uint32_t T2, k3;
+      t32_threshold(G + kT32R1, kT32R2, k2, lds, sh, T2, k3);
+      if (blockIdx.x == 0 && threadIdx.x == 0) {
+        st[2] = T2;
+        st[3] = k3;
+      }
+      pfx = (T1 << 21) | (T2 << 10);
+      pmask = 0xFFFFFC00u;
+      shift = 0;
+      dmask = kT32R3 - 1;
+    }
+  }
+  __syncthreads();
+  const uint32_t lane = lane_id();
+  const uint64_t pt = ((per_block + kBlock - 1) / kBlock + 15) / 16 * 16;
+  const uint64_t blo = (uint64_t)blockIdx.x * per_block;
+  const uint64_t bhi = blo + per_block < S ? blo + per_block : S;
+  const uint64_t t0 = blo + threadIdx.x * pt, t1 = t0 + pt < bhi ? t0 + pt : bhi;
+  // trip count uniform across the wave (per-thread ranges of equal length)
+  for (uint64_t c0 = blo + threadIdx.x * pt, n = 0; n < pt; c0 += 16, n += 16) {
+    uint32_t kv[16];
+    const uint32_t m = c0 < t1 ? load_keys32(scores, c0, t1, largest, kv) : 0u;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const bool act = ((m >> e) & 1u) && (kv[e] & pmask) == pfx;
+      const uint32_t bin = (kv[e] >> shift) & dmask;
+      // a converging population shares its high digits: one atomic when the
+      // wave agrees on one bin, else per-lane LDS atomics
+      const unsigned long long active = __ballot(act);
+      if (active) {
+        const int leader = __ffsll((long long)active) - 1;
+        const uint32_t b = (uint32_t)__shfl((int)bin, leader, 64);
+        const unsigned long long same = __ballot(act && bin == b);
+        if (same == active) {
+          if ((int)lane == leader) atomicAdd(&h[b], (uint32_t)__popcll(same));
+        } else if (act) {
+          atomicAdd(&h[bin], 1u);
+        }
+      }
+    }
+  }
+  __syncthreads();
+  uint32_t* Gl = G + (level == 1 ? 0u : (level == 2 ? kT32R1 : kT32R1 + kT32R2));
+  for (uint32_t i = threadIdx.x; i < R; i += kBlock)
+    if (h[i]) atomicAdd(&Gl[i], h[i]);
+}
+
+// the select: threshold key T from the three digits, per-thread (gt, eq)
+// counts over a contiguous range, block order by status words (every
+// predecessor by ticket publishes without waiting), then the ordered write
+// with the row moves; SCATTER also writes the block's packed best (the best
+// survivor, key -> score exactly, or the best immigrant placed here)
+__global__ __launch_bounds__(kBlock) void topk32_select_kernel(const float* scores, uint64_t S, uint64_t per_block,
+                                                               bool largest, uint32_t k, uint32_t* G,
+                                                               uint64_t* status, uint32_t* ctr, uint32_t nblocks,
+                                                               uint32_t* idx_out, TopkMove mv) {
+  __shared__ uint32_t sel_pos[kTopkMoveSlots], sel_src[kTopkMoveSlots];
+  __shared__ uint32_t lds[kBlock / 64], sh[2], sh_b;
+  if (threadIdx.x == 0) sh_b = atomicAdd(&ctr[0], 1u);
+  const uint32_t* st = G + kT32State;
+  const uint32_t T1 = st[0], T2 = st[2], k3 = st[3];
+  uint32_t T3, need_eq;
+  t32_threshold(G + kT32R1 + kT32R2, kT32R3, k3, lds, sh, T3, need_eq);  // (its barrier publishes sh_b)
+  const uint32_t T = (T1 << 21) | (T2 << 10) | T3;
+  const uint32_t gt_total = k - need_eq;  // every key above T
+  const uint32_t b = sh_b;
+  // G1 / G2 are read by no block of this launch: zeroed here for the next
+  // selection (a slice per block); G3 and the state by the last ticket
+  for (uint32_t i = b * kBlock + threadIdx.x; i < kT32R1 + kT32R2; i += nblocks * kBlock) G[i] = 0;
+  const uint64_t pt = ((per_block + kBlock - 1) / kBlock + 15) / 16 * 16;  // keys per thread, whole 16-key chunks
+  const uint64_t blo = (uint64_t)b * per_block;
+  const uint64_t bhi = blo + per_block < S ? blo + per_block : S;
+  const uint64_t t0 = blo + threadIdx.x * pt;
+  const uint64_t t1 = t0 + pt < bhi ? t0 + pt : bhi;
+  uint32_t gt = 0, eq = 0;
+  for (uint64_t c0 = t0; c0 < t1; c0 += 16) {
+    uint32_t kv[16];
+    const uint32_t m = load_keys32(scores, c0, t1, largest, kv);
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      gt += ((m >> e) & 1u) && kv[e] > T;
+      eq += ((m >> e) & 1u) && kv[e] == T;
+    }
+  }
+  uint32_t bg, be;
+  uint32_t og = block_excl_scan_u(gt, lds, bg);
+  __syncthreads();
+  uint32_t oe = block_excl_scan_u(eq, lds, be);
+  if (threadIdx.x == 0)
+    __hip_atomic_store(&status[b], kLbAgg | ((uint64_t)bg << 31) | (uint64_t)be, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+  // block prefix = sum of the predecessors' aggregates, read in parallel
+  uint32_t pg = 0, pe = 0;
+  for (uint32_t j = threadIdx.x; j < b; j += kBlock) {
+    uint64_t w = 0;
+    for (uint32_t spins = 0; spins < (1u << 26); ++spins) {  // bound: never hang the device
+      w = __hip_atomic_load(&status[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (w) break;
+    }
+    pg += (uint32_t)((w >> 31) & kLbMask31);
+    pe += (uint32_t)(w & kLbMask31);
+  }
+  auto add = [](uint32_t x, uint32_t y) { return x + y; };
+  pg = block_reduce(pg, lds, add);
+  pe = block_reduce(pe, lds, add);
+  // every other block published, hence had read G3 and the state: the last
+  // ticket zeroes them for the next selection
+  if (b == nblocks - 1)
+    for (uint32_t i = threadIdx.x; i < kT32R3 + 4; i += kBlock) G[kT32R1 + kT32R2 + i] = 0;
+  uint32_t gpos = pg + og, epos = pe + oe;
+  const bool move = mv.mode != TopkMove::NONE;
+  const bool bests = mv.mode == TopkMove::SCATTER && mv.best_parts != nullptr;
+  unsigned long long keep_best = 0, imm_best = 0;
+  uint32_t lg = og, le = bg + oe;
+  for (uint64_t c0 = t0; c0 < t1; c0 += 16) {
+    uint32_t kv[16];
+    const uint32_t m = load_keys32(scores, c0, t1, largest, kv);
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      if (!((m >> e) & 1u)) continue;
+      uint32_t pos = 0xFFFFFFFFu, slot = 0;
+      if (kv[e] > T && gpos < gt_total) {
+        pos = gpos++;
+        slot = lg++;
+      }
+      if (kv[e] == T) {
+        if (epos < need_eq) {
+          pos = gt_total + epos;
+          slot = le;
+        }
+        ++epos;
+        ++le;
+      }
+      if (bests) {
+        if (pos == 0xFFFFFFFFu) {  // a survivor: its own score, exactly, from the key
+          const float v = key_score(largest ? kv[e] : ~kv[e]);
+          const unsigned long long kb = pack_best(v, c0 + e);
+          keep_best = kb > keep_best ? kb : keep_best;
+        } else {
+          const unsigned long long ib = pack_best(mv.src_scores[pos], c0 + e);
+          imm_best = ib > imm_best ? ib : imm_best;
+        }
+      }
+      if (pos == 0xFFFFFFFFu) continue;
+      if (idx_out) idx_out[pos] = (uint32_t)(c0 + e);
+      if (move && slot < kTopkMoveSlots) {
+        sel_pos[slot] = pos;
+        sel_src[slot] = (uint32_t)(c0 + e - blo);
+      } else if (move) {
+        topk_emit(mv, nullptr, pos, c0 + e);  // beyond the LDS list (huge blocks): per thread
+      }
+    }
+  }
+  if (bests) {  // block-uniform: the block's new packed best
+    __shared__ unsigned long long red[kBlock / 64];
+    const unsigned long long kb = block_max_u64(keep_best, red);
+    const unsigned long long ib = block_max_u64(imm_best, red);
+    if (threadIdx.x == 0) mv.best_parts[b] = kb > ib ? kb : ib;
+  }
+  if (!move) return;
+  // slots [0, bg): keys above T (those with a global rank < gt_total were
+  // taken), [bg, bg + be): ties, of which those with a tie rank < need_eq
+  __syncthreads();
+  const uint32_t taken_eq = pe >= need_eq ? 0u : min(be, need_eq - pe);
+  const uint32_t n_gt = pg >= gt_total ? 0u : min(bg, gt_total - pg);
+  const uint32_t nsel = min(bg + taken_eq, kTopkMoveSlots);
+  const uint32_t rw16 = mv.rw16;
+  for (uint32_t t = threadIdx.x; t < nsel * rw16; t += kBlock) {
+    const uint32_t r = t / rw16, c = t % rw16;
+    if (r >= n_gt && r < bg) continue;
+    const uint64_t i = blo + sel_src[r];
+    const uint64_t pos = sel_pos[r];
+    if (mv.mode == TopkMove::GATHER) {
+      mv.dst_rows[pos * rw16 + c] = mv.src_rows[i * rw16 + c];
+      if (c == 0) mv.dst_scores[pos] = mv.src_scores[i];
+    } else {
+      mv.dst_rows[i * rw16 + c] = mv.src_rows[pos * rw16 + c];
+      if (c == 0) mv.dst_scores[i] = mv.src_scores[pos];
     }
   }
 }
@@ -1210,7 +1493,19 @@ void topk_run(TopkKeys<BITS> keys, uint64_t S, uint32_t k, bool sorted, uint32_t
 }  // namespace
 
 bool topk_move_supported(const uint16_t* keys16, uint32_t key_range, uint64_t S) {
-  return keys16 && key_range >= 2 && key_range <= kTopkMaxRange && S < (1ull << 31);
+  // u16 keys: the value-histogram select; f32 scores: the 3-digit radix select
+  return (!keys16 || (key_range >= 2 && key_range <= kTopkMaxRange)) && S < (1ull << 31);
+}
+
+// keys per thread of the selection-order kernels (their grid: S / (256 kpt)
+// blocks, at most 1024); PGA_TOPK_KPT overrides (16, 32, 64 or 128)
+static uint32_t topk_kpt() {
+  static const uint32_t v = [] {
+    const char* e = std::getenv("PGA_TOPK_KPT");
+    const uint32_t x = e ? (uint32_t)std::strtoul(e, nullptr, 10) : 16u;
+    return (x == 16 || x == 32 || x == 64 || x == 128) ? x : 16u;
+  }();
+  return v;
 }
 
 uint32_t topk_launch(const float* scores, const uint16_t* keys16, uint32_t key_range, uint64_t S, uint32_t k,
@@ -1231,7 +1526,7 @@ uint32_t topk_launch(const float* scores, const uint16_t* keys16, uint32_t key_r
     p += align_up(radix_sort_workspace_bytes(k));
     uint32_t* G = (uint32_t*)p;  // zero on allocation and after every use
     const uint32_t R = key_range;
-    uint32_t grid = launch_grid(S, kBlock * 16);
+    uint32_t grid = launch_grid(S, kBlock * topk_kpt());
     const uint32_t cgrid = grid > 1024 ? 1024 : grid;
     const uint64_t per_block = (S + cgrid - 1) / cgrid;
     uint64_t* status = (uint64_t*)cnt;  // cgrid aggregate words, then 2 ticket counters
@@ -1260,6 +1555,27 @@ uint32_t topk_launch(const float* scores, const uint16_t* keys16, uint32_t key_r
                        per_block, st, cnt, cgrid, (uint32_t*)nullptr, idx_out);
     PGA_HIP_CHECK(hipGetLastError());
     return 0;
+  }
+  if (!keys16 && !sorted && S < (1ull << 31)) {
+    // f32 scores, selection order: 3 radix digits + the ticketed select (topk32_*)
+    char* p = (char*)ws;
+    p += align_up(sizeof(TopkState));
+    uint64_t* status = (uint64_t*)p;  // cgrid aggregate words, then 2 ticket counters
+    p += align_up(sizeof(uint32_t) * (2 * 1024 + 4));
+    p += 3 * align_up(4ull * k);
+    p += align_up(radix_sort_workspace_bytes(k));
+    uint32_t* G = (uint32_t*)p;  // digit histograms + state: zero on allocation and after every use
+    static_assert(kT32State + 4 <= kTopkMaxRange, "f32 selection histograms fit the value-histogram region");
+    const uint32_t grid = launch_grid(S, kBlock * topk_kpt());
+    const uint32_t cgrid = grid > 1024 ? 1024 : grid;
+    const uint64_t per_block = ((S + cgrid - 1) / cgrid + 15) / 16 * 16;  // whole 16-key chunks per thread
+    for (uint32_t level = 1; level <= 3; ++level)
+      hipLaunchKernelGGL(topk32_hist_kernel, cgrid, kBlock, 0, s, scores, S, per_block, largest, k, level, G, status,
+                         cgrid);
+    hipLaunchKernelGGL(topk32_select_kernel, cgrid, kBlock, 0, s, scores, S, per_block, largest, k, G, status,
+                       (uint32_t*)(status + cgrid), cgrid, idx_out, mv ? *mv : TopkMove{});
+    PGA_HIP_CHECK(hipGetLastError());
+    return mv && mv->mode == TopkMove::SCATTER && mv->best_parts ? cgrid : 0u;
   }
   if (keys16)
     topk_run<16>(TopkKeys<16>{scores, keys16, largest}, S, k, sorted, idx_out, ws, s);

@@ -21,12 +21,14 @@
 #include <c10/hip/HIPStream.h>
 #include <torch/extension.h>
 
+#include <cstdlib>
 #include <memory>
 #include <string>
 #include <vector>
 
 #include "pga/comm.hpp"
 #include "pga/island.hpp"
+#include "pga/ops.hpp"
 
 namespace py = pybind11;
 
@@ -66,7 +68,37 @@ struct EngineComm {
   std::shared_ptr<pga::Comm> comm;
   int rank = 0, nranks = 1;
   std::vector<pga::LocalRank> pending;  // the posted epoch (empty: none)
+  hipStream_t compute = nullptr;        // the island's stream at post time
+  bool on_transport = false;            // the epoch's device work runs on the transport stream
+  hipEvent_t ev_pop = nullptr, ev_out = nullptr, ev_in = nullptr;
+  ~EngineComm() {
+    for (hipEvent_t ev : {ev_pop, ev_out, ev_in})
+      if (ev) (void)hipEventDestroy(ev);
+  }
 };
+
+// Where the epoch's device work runs.  Emigrant selection only reads the
+// current population, and re-scoring only touches the receive buffers, so
+// both CAN go on the communicator's transport stream, in order with the
+// transfer and beside the next generation kernel (IslandModel._fence orders
+// the generation that overwrites the emigrants' population after the
+// packing).  Off by default (PGA_MIG_ON_TRANSPORT=1 turns it on): measured
+// on MI355X (bench.py --rccl-self, profiles/migration_ab_r06.txt) the
+// headline generation kernel holds every CU's LDS, so nothing beside it
+// runs until it drains, and the cross-stream hops cost more than they hide
+// (OneMax 98.2 vs 95.6 us/gen, TSP-256 147.0 vs 143.8).  Never with
+// elitism > 1: the elite top-k of every generation shares the island's
+// selection workspace with the emigrant selection.
+bool use_transport(EngineComm& e, const pga::Island& isl, const pga::LocalRank& l) {
+  if (isl.config().n_elite > 1 || !std::getenv("PGA_MIG_ON_TRANSPORT")) return false;
+  if (!e.comm->transport_stream(l)) return false;
+  if (!e.ev_pop) {
+    PGA_HIP_CHECK(hipEventCreateWithFlags(&e.ev_pop, hipEventDisableTiming));
+    PGA_HIP_CHECK(hipEventCreateWithFlags(&e.ev_out, hipEventDisableTiming));
+    PGA_HIP_CHECK(hipEventCreateWithFlags(&e.ev_in, hipEventDisableTiming));
+  }
+  return true;
+}
 
 }  // namespace
 
@@ -111,7 +143,25 @@ void bind_comm(py::module& m) {
                          "staging buffers too small");
              TORCH_CHECK(dst >= 0 && dst < e.nranks && src >= 0 && src < e.nranks, "peer out of range");
              std::vector<pga::LocalRank> local{local_of(*isl, e.rank, send_rows, send_scores, recv_rows, recv_scores)};
-             isl->emigrate(k, send_rows.data_ptr(), send_scores.data_ptr<float>());
+             e.compute = isl->stream;
+             e.on_transport = use_transport(e, *isl, local[0]);
+             if (e.on_transport) {  // the transport stream waits for the population, then selects the emigrants
+               hipStream_t ts = e.comm->transport_stream(local[0]);
+               PGA_HIP_CHECK(hipEventRecord(e.ev_pop, e.compute));
+               PGA_HIP_CHECK(hipStreamWaitEvent(ts, e.ev_pop, 0));
+               isl->stream = ts;
+               local[0].stream = ts;
+             }
+             try {
+               isl->emigrate(k, send_rows.data_ptr(), send_scores.data_ptr<float>());
+             } catch (...) {
+               isl->stream = e.compute;
+               throw;
+             }
+             isl->stream = e.compute;
+             // the emigrants are packed: fence() lets the compute stream
+             // overwrite the population they came from (generation + 2)
+             if (e.on_transport) PGA_HIP_CHECK(hipEventRecord(e.ev_out, local[0].stream));
              e.comm->self_exchange = e.nranks == 1;
              e.comm->exchange(ring_plan(e.rank, dst, src, k), local);
              e.pending = std::move(local);
@@ -124,18 +174,42 @@ void bind_comm(py::module& m) {
              TORCH_CHECK(!e.pending.empty(), "no exchange in flight");
              std::vector<pga::LocalRank> local = std::move(e.pending);
              e.pending.clear();
-             isl->stream = c10::hip::getCurrentHIPStream(isl->device()).stream();
-             local[0].stream = isl->stream;
+             const hipStream_t compute = c10::hip::getCurrentHIPStream(isl->device()).stream();
+             isl->stream = compute;
+             // on_transport: local[0].stream is the transport stream itself
+             // (the wait orders nothing); else the compute stream waits
+             if (!e.on_transport) local[0].stream = compute;
              bool ok;
              {
                py::gil_scoped_release nogil;
                ok = e.comm->wait(local, timeout_s);
              }
              if (!ok) return false;
-             if (validate) isl->evaluate_rows(local[0].recv_rows, local[0].recv_scores, k);
+             if (validate) {
+               isl->stream = e.on_transport ? local[0].stream : compute;
+               try {
+                 isl->evaluate_rows(local[0].recv_rows, local[0].recv_scores, k);
+               } catch (...) {
+                 isl->stream = compute;
+                 throw;
+               }
+               isl->stream = compute;
+             }
+             if (e.on_transport) {  // the compute stream takes the re-scored immigrants
+               PGA_HIP_CHECK(hipEventRecord(e.ev_in, local[0].stream));
+               PGA_HIP_CHECK(hipStreamWaitEvent(compute, e.ev_in, 0));
+             }
              isl->immigrate(k, local[0].recv_rows, local[0].recv_scores);
              return true;
            },
            py::arg("island"), py::arg("k"), py::arg("timeout_s") = 0.0, py::arg("validate") = true)
+      // order the compute stream after the epoch's emigrant packing: call
+      // once the generation after the epoch's departure is enqueued (the
+      // packing reads the population the generation after that overwrites)
+      .def("fence",
+           [](EngineComm& e, const IslandPtr& isl) {
+             if (e.pending.empty() || !e.on_transport) return;
+             PGA_HIP_CHECK(hipStreamWaitEvent(c10::hip::getCurrentHIPStream(isl->device()).stream(), e.ev_out, 0));
+           })
       .def_property_readonly("in_flight", [](const EngineComm& e) { return !e.pending.empty(); });
 }

@@ -103,11 +103,26 @@ class IslandModel:
         policy: str = "topk",
         transport: str = "auto",
         self_exchange: bool = False,
+        lag: Optional[int] = None,
     ):
         if topology not in TOPOLOGIES:
             raise ValueError(f"topology must be one of {TOPOLOGIES}")
         self.ga = ga
         self.migrate_every = int(migrate_every)
+        # lag: generations from an epoch's departure to its arrival.  The
+        # exchange overlaps the next generation kernel, but on one device the
+        # transfer's kernel only gets the CUs as that generation drains, so it
+        # completes at the generation's end; with lag 1 the host then enqueues
+        # the immigration while the compute queue sits empty (measured on
+        # MI355X: a ~100 us idle gap per epoch, host poll + launch latency).
+        # With lag 2 the host checks the exchange only after the generation
+        # after it is queued too: the GPU never waits for the host.  Capped at
+        # migrate_every - 1 (an epoch ends before the next one starts).
+        # (default: 2 for GPU islands, 1 for CPU islands, which have no queue)
+        if lag is None:
+            lag = int(os.environ.get("PGA_MIG_LAG", "2")) if ga.island.rows(0).device.type == "cuda" else 1
+        self.lag = max(1, min(int(lag), self.migrate_every - 1)) if self.migrate_every > 1 else 1
+        self._start_gen = 0
         self.topology = topology
         self.group = group
         self.overlap = overlap
@@ -180,7 +195,7 @@ class IslandModel:
         if transport == "engine" and self.distributed and not engine_ok:
             raise ValueError(f"transport='engine' cannot run this model: {why}")
         self._use_engine = engine_ok and self.distributed and (
-            transport == "engine" or os.environ.get("PGA_MIGRATION_TRANSPORT", "") != "torch")
+            transport == "engine" or (transport == "auto" and os.environ.get("PGA_MIGRATION_TRANSPORT", "") != "torch"))
         self.fallbacks = 0  # engine -> torch switches made by connect()
         # test-only fault: post the receive but withhold the matching send, so
         # the exchange can never complete (exercises the deadline + abort path)
@@ -354,8 +369,8 @@ class IslandModel:
             if pending and time.monotonic() > deadline:
                 self._abort()
                 raise TimeoutError(f"migration epoch {self._epoch} exceeded {self.timeout.total_seconds()} s")
-            if pending:
-                time.sleep(50e-6)
+            if pending and time.monotonic() > deadline - self.timeout.total_seconds() + 2e-3:
+                time.sleep(20e-6)  # spin the first 2 ms, then back off
         for wk in works:
             wk.wait()  # completed: raises a transport error, else just orders the stream
 
@@ -435,28 +450,49 @@ class IslandModel:
             g = self.ga.generation
             if migrates and g > 0 and g % self.migrate_every == 0 and self._pending is None and not self.degraded:
                 self.start_migration()
+                self._start_gen = g
                 if not self.overlap:
                     self.finish_migration()
-            if self._pending is None and self.ga.torch_objective is None and target is None:
-                # no exchange in flight and nothing to do between generations:
-                # every generation up to the next migration point in ONE
-                # engine call (C++ enqueues them back to back, no per-step
-                # Python on the host path)
+            if self.ga.torch_objective is None and target is None and (
+                    self._pending is None or self.ga.generation - self._start_gen < self.lag - 1):
+                # nothing to do between generations until the next migration
+                # point, or until the generation before the exchange in flight
+                # completes: those generations in ONE engine call (C++
+                # enqueues them back to back, no per-step Python on the host
+                # path)
                 step = n - done
-                if migrates:
+                if self._pending is not None:
+                    # the first generation alone: _fence() follows it
+                    ahead = self.ga.generation - self._start_gen
+                    step = min(step, 1 if ahead == 0 else self.lag - 1 - ahead)
+                elif migrates:
                     step = min(step, self.migrate_every - g % self.migrate_every)
                 self.ga.island.run(step)
+                self._fence()
                 done += step
                 continue
             self.ga.island.run(1)
+            self._fence()
             if self.ga.torch_objective is not None:
                 self.ga._custom_eval()
-            if self._pending is not None:
+            if self._pending is not None and self.ga.generation - self._start_gen >= self.lag:
                 self.finish_migration()
             done += 1
             if target is not None and self.ga.generation % every == 0 and self.global_reduce_best() >= target:
                 break
         return done
+
+    def _fence(self) -> None:
+        """With the engine transport the emigrants are packed on the transport
+        stream, concurrently with the generation after their departure; the
+        generation after THAT overwrites the population they come from, so
+        the compute stream waits for the packing once the first is enqueued."""
+        if self._pending is None or self.ga.generation != self._start_gen + 1:
+            return
+        if self._pending == "engine":
+            self._ec.fence(self.ga.island)
+        elif self._side is not None:  # the same for the packing on the side stream
+            torch.cuda.current_stream(self._side.device).wait_stream(self._side)
 
     def flush(self) -> None:
         self.finish_migration()

@@ -50,6 +50,7 @@ def match(pga, IslandModel, side: bool, transport: str) -> None:
     a = model(pga, IslandModel, side_stream=side, transport=transport)
     assert a._use_engine == (transport == "engine")
     a.run(31)
+    a.flush()  # (lag 2 on GPU islands: the epoch that left at 30 lands here)
     torch.cuda.synchronize()
 
     real_batch, real_p2p = dist.batch_isend_irecv, dist.P2POp
@@ -65,6 +66,7 @@ def match(pga, IslandModel, side: bool, transport: str) -> None:
     try:
         b = model(pga, IslandModel, side_stream=side, transport="torch")
         b.run(31)
+        b.flush()
         torch.cuda.synchronize()
     finally:
         dist.batch_isend_irecv, dist.P2POp = real_batch, real_p2p
@@ -90,7 +92,8 @@ def withhold(port: int) -> None:
     torch.cuda.set_device(0)
     dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
     engine = len(sys.argv) > 3 and sys.argv[3] == "engine"
-    m = model(pga, IslandModel, timeout_s=2.0, transport="engine" if engine else "torch")
+    # lag 1: each epoch completes one generation after it leaves (the counts below)
+    m = model(pga, IslandModel, timeout_s=2.0, transport="engine" if engine else "torch", lag=1)
     if engine:  # the engine communicator's own fault injection: the 3rd exchange's sends withheld
         m._engine().set_fault(3, 3)
     m.run(7)  # epochs at generations 3 and 6 complete

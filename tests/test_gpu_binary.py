@@ -432,3 +432,69 @@ def test_rank_selection_u16_keys_partial_tile_bitexact():
         torch.cuda.synchronize()
         assert torch.equal(g.rows.cpu(), c.rows)
         assert torch.equal(g.scores.cpu(), c.scores)
+
+
+@pytest.mark.parametrize("S", [4099, 1 << 20, (1 << 22) + 12345])
+@pytest.mark.parametrize("dist", ["ties", "spread"])
+def test_gpu_topk32_selection_order(S, dist):
+    """f32-score top-k in selection order (3 radix digits + one ticketed
+    select, topk32_*): the indices with a score beyond the threshold in
+    population order, then the first ties; heavy ties, +-inf and a negative
+    zero included; repeated so the histogram / state / ticket reset between
+    calls is exercised."""
+    ga = pga.GeneticAlgorithm(pga.models.Rastrigin(8), S, seed=11, device=DEV)
+    g = torch.Generator().manual_seed(S)
+    if dist == "ties":  # a converged population: few distinct values sharing their high bits
+        sc = -(100.0 + torch.randint(0, 7, (S,), generator=g).float() * 2 ** -10)
+    else:
+        sc = torch.randn(S, generator=g) * 1e3
+    sc[5], sc[S // 2], sc[7] = float("inf"), float("-inf"), -0.0
+    ga.scores.copy_(sc.to(DEV))
+    ga.island.rebest()
+    key_src = sc.double()
+    for k in (10486 % S, 1, S // 3, 10486 % S, S):
+        k = max(1, k)
+        for largest in (True, False):
+            got = ga.island.topk(k, largest, False).cpu().long()
+            key = key_src if largest else -key_src
+            T = key.sort(descending=True).values[k - 1]
+            gt = (key > T).nonzero().flatten()
+            eq = (key == T).nonzero().flatten()[: k - gt.numel()]
+            assert torch.equal(got, torch.cat([gt, eq])), (k, largest)
+
+
+@pytest.mark.parametrize("S,k", [(5000, 50), (1 << 20, 10486)])
+@pytest.mark.parametrize("prob", ["rastrigin", "tsp"])
+def test_fused_migration_matches_unfused_f32(S, k, prob):
+    """f32-score islands (REAL, PERMUTATION): Island.emigrate / immigrate
+    (the radix select with the row gather / scatter and the new best partials
+    fused in) == topk + gather / topk + scatter + best pass, bit for bit."""
+    mk = {"rastrigin": lambda: pga.models.Rastrigin(30),
+          "tsp": lambda: pga.models.TSP.random_euclidean(64, seed=2)}[prob]
+    S = S if prob == "rastrigin" else min(S, 1 << 18)
+    kw = dict(seed=9, device=DEV, elitism=1)
+    a, b = pga.GeneticAlgorithm(mk(), S, **kw), pga.GeneticAlgorithm(mk(), S, **kw)
+    a.run(3)
+    b.run(3)
+    ia, ib = a.island, b.island
+    ia.migration_policy = pga._ext.C.MIG_TOPK
+    rw = int(ia.row_words)
+    ra, sa = torch.empty(k * rw, dtype=torch.int32, device=DEV), torch.empty(k, device=DEV)
+    rb, sb = torch.empty_like(ra), torch.empty_like(sa)
+    ia.emigrate(k, ra, sa)
+    ib.gather(ib.topk(k, True, False), rb, sb)
+    torch.cuda.synchronize()
+    assert torch.equal(ra, rb) and torch.equal(sa, sb)
+    c = pga.GeneticAlgorithm(mk(), S, seed=10, device=DEV, elitism=1)
+    c.run(5)
+    rc, sc = torch.empty_like(ra), torch.empty_like(sa)
+    c.island.emigrate(k, rc, sc)
+    ia.immigrate(k, rc, sc)
+    ib.scatter(ib.topk(k, False, False), rc, sc)
+    torch.cuda.synchronize()
+    assert torch.equal(a.rows, b.rows) and torch.equal(a.scores, b.scores)
+    assert a.best_score() == b.best_score() and a.best_index() == b.best_index()
+    a.run(2)
+    b.run(2)
+    torch.cuda.synchronize()
+    assert torch.equal(a.rows, b.rows) and torch.equal(a.scores, b.scores)

@@ -150,6 +150,8 @@ def test_overlapped_migration_stream_order_gpu(monkeypatch):
     assert a._side is not None
     a.run(31)
     b.run(31)
+    a.flush()  # (lag 2 on GPU islands: the epoch that left at 30 lands here)
+    b.flush()
     torch.cuda.synchronize()
     assert a.migrations == b.migrations == 10
     assert torch.equal(a.ga.rows, b.ga.rows) and torch.equal(a.ga.scores, b.ga.scores)
