@@ -3,8 +3,8 @@
 // A wave owns a contiguous range of children; a SEGMENT of up to
 // kSegBatches batches of 64 children is selected one lane per child with
 // every score / key load of the segment in flight at once (the second phase,
-// breeding, is encoding specific: real.hip real_gen_tp; binary.hip keeps its
-// own inlined copy of this phase).  Selection words are the ST_SEL layout of
+// breeding, is encoding specific: real_dev.hpp real_gen_tp and binary_dev.hpp
+// binary_gen_tp both call tp_select_segment for this one).  Selection words are the ST_SEL layout of
 // core.hpp, so the result equals st_select_parents() child by child.
 #pragma once
 

@@ -54,10 +54,24 @@ def pmc(d: str) -> str:
         der = []
         if "TCC_HIT_sum" in avg and "TCC_MISS_sum" in avg and avg["TCC_HIT_sum"] + avg["TCC_MISS_sum"] > 0:
             der.append(f"L2 hit rate {avg['TCC_HIT_sum'] / (avg['TCC_HIT_sum'] + avg['TCC_MISS_sum']):.1%}")
+        # fabric bytes from the request-size split when the pass collected it
+        # (an L2 read request is 32, 64 or 128 B, a write 32 or 64 B); else
+        # the request count at 64 B, a lower bound for 128-B row reads
         if "TCC_EA0_RDREQ_sum" in avg:
-            der.append(f"HBM read ≈ {avg['TCC_EA0_RDREQ_sum'] * 64 / 1e6:.1f} MB")
+            n = avg["TCC_EA0_RDREQ_sum"]
+            if "TCC_EA0_RDREQ_128B_sum" in avg and "TCC_EA0_RDREQ_64B_sum" in avg:
+                b128, b64 = avg["TCC_EA0_RDREQ_128B_sum"], avg["TCC_EA0_RDREQ_64B_sum"]
+                rd = 128 * b128 + 64 * b64 + 32 * max(0.0, n - b128 - b64)
+                der.append(f"fabric read {rd / 1e6:.1f} MB ({b128 / max(n, 1):.1%} of requests 128 B)")
+            else:
+                der.append(f"fabric read >= {n * 64 / 1e6:.1f} MB (requests x 64 B)")
         if "TCC_EA0_WRREQ_sum" in avg:
-            der.append(f"HBM write ≈ {avg['TCC_EA0_WRREQ_sum'] * 64 / 1e6:.1f} MB")
+            n = avg["TCC_EA0_WRREQ_sum"]
+            if "TCC_EA0_WRREQ_64B_sum" in avg:
+                w64 = avg["TCC_EA0_WRREQ_64B_sum"]
+                der.append(f"fabric write {(64 * w64 + 32 * max(0.0, n - w64)) / 1e6:.1f} MB")
+            else:
+                der.append(f"fabric write ≈ {n * 64 / 1e6:.1f} MB (requests x 64 B)")
         if "SQ_INSTS_VALU" in avg and "SQ_WAVES" in avg and avg["SQ_WAVES"]:
             der.append(f"VALU insts/wave {avg['SQ_INSTS_VALU'] / avg['SQ_WAVES']:.0f}")
         if "SQ_WAIT_ANY" in avg and "SQ_WAVE_CYCLES" in avg and avg["SQ_WAVE_CYCLES"]:
