@@ -54,6 +54,10 @@ Island::Island(const Config& cfg, int device) : cfg_(cfg), device_(device) {
   out_best_ = alloc(64);
   stats_ = alloc(4ull * (4 + 3 * 1024));
   aux_on_ = std::getenv("PGA_TSP_NO_LDS") == nullptr;  // verification: the f32 L2 matrix path
+  persistent_ = [] {
+    const char* e = std::getenv("PGA_TP_MULTI");
+    return e && e[0] == '1';
+  }();
   if (on_gpu() && cfg_.encoding == ENC_BINARY) {  // binary_gen_tp's pair-pool counters (stamp 0 = stale)
     tp_pool_ = alloc(tp_pool_bytes(kMaxGrid));
     PGA_HIP_CHECK(hipMemset(tp_pool_.ptr, 0, tp_pool_.bytes));
@@ -75,7 +79,7 @@ Island::~Island() {
                    &obj_data_[0], &obj_data_[1], &keys_[0], &keys_[1], &elite_idx_, &cumfit_, &cum_ws_, &roul_guide_, &topk_ws_, &stats_,
                    &out_best_,  &scratch_, &compat_rand_, &ev_parts_, &gen_dev_, &rank_order_, &rank_ws_, &qubo_qt_,
                    &knap_tab_, &stats_parts_[0], &stats_parts_[1], &hist_, &qk_ws_, &tp_pool_, &obj_aux_,
-                   &fhist_[0], &fhist_[1], &fhist_[2]};
+                   &fhist_[0], &fhist_[1], &fhist_[2], &multi_bar_};
   drop_graph();
   if (cap_stream_) (void)hipStreamDestroy(cap_stream_);
   for (Buffer* b : all) {
@@ -362,6 +366,11 @@ GenArgs Island::make_args(int mode) {
   }
   a.best_cur = (const unsigned long long*)best_[cur_].ptr;
   a.n_best_cur = n_best_[cur_];
+  static const uint32_t nt = [] {
+    const char* e = std::getenv("PGA_TP_NT_STORE");
+    return e && e[0] == '1' ? 1u : 0u;
+  }();
+  a.nt_store = nt;
   a.last_mask = last_mask_;
   if (capturing_) {
     a.gen_dev = (const uint32_t*)gen_dev_.ptr;
@@ -501,7 +510,57 @@ void Island::run(uint32_t n) {
     fhist_of_[0] = fhist_of_[1] = -1;  // replays do not produce the fused histograms
     if (run_graph(reps, fresh)) n -= reps * graph_g_;
   }
+  if (run_multi(n)) return;
   run_plain(n);
+}
+
+bool Island::run_multi(uint32_t n) {
+  // off by default (PGA_TP_MULTI=1 turns it on): measured slower on MI355X,
+  // the barrier's L2 writeback + invalidate and its polling cost more than the
+  // launch ramp it removes (interleaved A/B, profiles/persistent_ab_r06.txt:
+  // 94.7 vs 89.5 us/gen over 500 generations, 97.3 vs 91.7 over 20)
+  if (!persistent_ || n < 2 || !on_gpu() || cfg_.encoding != ENC_BINARY || jit_ || capturing_ || hist_on_) return false;
+  if (!integer_objective(cfg_.objective, cfg_.L) || cfg_.objective == OBJ_KNAPSACK || cfg_.n_elite > 1 ||
+      (cfg_.selection != SEL_TOURNAMENT && cfg_.selection != SEL_RANDOM))
+    return false;  // (no per-generation host work between the generations: prepare_generation is empty)
+  GenArgs a = make_args(MODE_GEN);
+  const int nx = cur_ ^ 1;
+  MultiGenArgs mg;
+  mg.parts[0] = (unsigned long long*)best_[nx].ptr;  // generation i writes the partials of parity cur_ ^ 1 ^ (i & 1)
+  mg.parts[1] = (unsigned long long*)best_[cur_].ptr;
+  mg.stats[0] = a.stats_parts;
+  mg.stats[1] = a.stats_parts ? (float*)stats_parts_[cur_].ptr : nullptr;
+  mg.gens = n;
+  if (!multi_bar_.ptr) multi_bar_ = alloc(256);
+  mg.barrier = (uint32_t*)multi_bar_.ptr;
+  bool fh = fhist_ready_for(a);
+  if (fh) {
+    for (int j = 0; j < 3; ++j) mg.hist[j] = (uint32_t*)fhist_[j].ptr;
+    mg.hist_rot = fhist_rot_ % 3;
+    mg.hist_bins = cfg_.L + 1;
+    mg.hist_zero_words = fused_hist_words(cfg_.L + 1);
+  }
+  TraceRange tr("pga.generations_multi", 2);
+  const uint32_t grid = binary_launch_multi(a, mg, stream);
+  if (grid == 0) return false;
+  fh = fh && binary_hist_written();
+  for (uint32_t i = 0; i < n; ++i) {  // the bookkeeping of n plain generations
+    n_best_[cur_ ^ 1] = grid;
+    stats_ok_[cur_ ^ 1] = a.stats_parts != nullptr;
+    if (fh) {
+      const int w = (int)(fhist_rot_ % 3), z = (int)((fhist_rot_ + 1) % 3);
+      ++fhist_rot_;
+      fhist_of_[cur_ ^ 1] = w;
+      fhist_clean_[w] = true;
+      fhist_clean_[z] = true;
+      if (fhist_of_[cur_] == z) fhist_of_[cur_] = -1;
+    } else {
+      fhist_of_[cur_ ^ 1] = -1;
+    }
+    qk_valid_[cur_ ^ 1] = false;
+    swap();
+  }
+  return true;
 }
 
 bool Island::run_tiny(uint32_t n) {

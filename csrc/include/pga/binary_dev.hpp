@@ -442,6 +442,8 @@ __device__ __forceinline__ uint32_t pos16(uint4 r1, uint32_t k) {  // k-th packe
 #define PGA_TP_XOMASK(c, q) u4(draw<true>(a.key, ST_XO, (c), (q)))
 #endif
 
+typedef uint32_t u32v4 __attribute__((ext_vector_type(4)));
+
 template <int GS, int OBJ, bool FULL, bool DENSE>
 __device__ __forceinline__ void binary_gen_tp_body(GenArgs a, unsigned long long* best_parts) {
   resolve_gen(a);
@@ -843,7 +845,12 @@ __device__ __forceinline__ void binary_gen_tp_body(GenArgs a, unsigned long long
       if (have) acc.add(a, v, q);                                                                           \
       sc = acc.template finish<GS>(a);                                                                      \
     }                                                                                                       \
-    if (have) ROW(nxt, c, q) = v;                                                                           \
+    if (have) {                                                                                             \
+      if (a.nt_store) /* block-uniform */                                                                   \
+        __builtin_nontemporal_store(__builtin_bit_cast(u32v4, v), (u32v4*)&ROW(nxt, c, q));                 \
+      else                                                                                                  \
+        ROW(nxt, c, q) = v;                                                                                 \
+    }                                                                                                       \
     if constexpr (JIT) {                                                                                    \
       lds_stage[(i % kJitStageSteps) * 64u + lane] = v;                                                     \
       if (i % kJitStageSteps == kJitStageSteps - 1u || i + 1u == nst) PGA_TP_JIT_EVAL                       \
@@ -985,6 +992,77 @@ __device__ __forceinline__ void binary_gen_tp_body(GenArgs a, unsigned long long
 template <int GS, int OBJ, bool FULL, bool DENSE>
 __global__ __launch_bounds__(kTpMaxWaves * 64) void binary_gen_tp(GenArgs a, unsigned long long* best_parts) {
   binary_gen_tp_body<GS, OBJ, FULL, DENSE>(a, best_parts);
+}
+
+// ---------------------------------------------------------------------------
+// Persistent multi-generation launch (the headline geometry only: one
+// 16-wave block per CU, every block resident at once): G generations of the
+// same island in ONE launch, a device-wide barrier between them in place of
+// the kernel boundary, so the next generation's blocks start together the
+// moment the barrier drops instead of re-entering one by one through the
+// dispatcher (the launch ramp: the last of 4096 waves started 3.4-4 us after
+// the first, pmc_r05.md).  The barrier does what the kernel boundary did for
+// memory: every block's stores leave its XCD's L2 (agent-scope release) before
+// it arrives, and every block drops stale L2 lines (agent-scope acquire) once
+// all have arrived; the next generation reads the population just written.
+// Integer objectives with tournament / random selection, elitism <= 1, no
+// fused histogram (the launcher checks).  Generation i writes parts[i & 1] and
+// stats[i & 1], so the host's parity bookkeeping is that of G plain launches.
+// ---------------------------------------------------------------------------
+struct GenMulti {
+  GenArgs a;                     // generation 0
+  unsigned long long* parts[2];  // best partials written by even / odd generations
+  float* stats[2];               // {min, sum} partials likewise (nullptr: none)
+  uint32_t gens;
+  uint32_t* bar;  // arrival counter, zero at launch; generation i's barrier waits for grid * (i + 1)
+  uint32_t* hist[3];  // fused key histograms, rotated as Island::run_plain does (hist[0] nullptr: off)
+  uint32_t hist_rot;
+};
+
+__device__ __forceinline__ void tp_grid_sync(uint32_t* bar, uint32_t target) {
+  __syncthreads();  // every wave's stores of the generation are in the L2 (workgroup release)
+  if (threadIdx.x < 64u) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");  // ... and out of this XCD's L2
+    if (threadIdx.x == 0) {
+      __hip_atomic_fetch_add(bar, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      // bounded: a grid that is not co-resident (never expected: the launcher
+      // takes one block per CU) would otherwise hang the device
+      for (uint32_t spins = 0; spins < (1u << 24); ++spins) {
+        if (__hip_atomic_load(bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= target) break;
+        __builtin_amdgcn_s_sleep(1);
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // no stale line of the new population survives
+  }
+  __syncthreads();
+}
+
+template <int GS, int OBJ, bool FULL, bool DENSE>
+__global__ __launch_bounds__(kTpMaxWaves * 64) void binary_gen_tp_multi(GenMulti m) {
+  GenArgs a = m.a;
+  for (uint32_t i = 0;; ++i) {
+    a.stats_parts = m.stats[i & 1u];
+    if (m.hist[0]) {
+      a.key_hist = m.hist[(m.hist_rot + i) % 3u];
+      a.hist_zero = m.hist[(m.hist_rot + i + 1u) % 3u];
+    }
+    binary_gen_tp_body<GS, OBJ, FULL, DENSE>(a, m.parts[i & 1u]);
+    if (i + 1u >= m.gens) break;
+    tp_grid_sync(m.bar, gridDim.x * (i + 1u));
+    // the population just written is the next generation's current one
+    const void* c = a.cur;
+    a.cur = a.next;
+    a.next = const_cast<void*>(c);
+    const float* sc = a.score_cur;
+    a.score_cur = a.score_next;
+    a.score_next = const_cast<float*>(sc);
+    const uint16_t* kc = a.key_cur;
+    a.key_cur = a.key_next;
+    a.key_next = const_cast<uint16_t*>(kc);
+    a.best_cur = m.parts[i & 1u];
+    a.n_best_cur = gridDim.x;
+    ++a.key.gen;
+  }
 }
 
 // ---------------------------------------------------------------------------

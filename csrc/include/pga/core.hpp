@@ -378,6 +378,9 @@ struct GenArgs {
   uint32_t* key_hist;
   uint32_t* hist_zero;
   uint32_t hist_bins, hist_zero_words;
+  // binary_gen_tp: child rows stored non-temporally (experiment knob,
+  // PGA_TP_NT_STORE=1; 0: ordinary stores)
+  uint32_t nt_store;
 };
 // the fused histogram's LDS bins (binary_gen_tp): objectives with more key
 // values use the separate histogram pass

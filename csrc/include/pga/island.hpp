@@ -165,6 +165,11 @@ class Island {
   bool fused_histogram() const { return fhist_on_; }
   // a fused histogram of the current population is available (tests, benches)
   bool fused_histogram_ready() const { return fhist_of_[cur_] >= 0; }
+  // Persistent multi-generation launches of the headline kernel (run(n) as
+  // ONE launch with a device-wide barrier between generations); off by
+  // default: measured slower than one launch per generation on MI355X
+  bool persistent() const { return persistent_; }
+  void set_persistent(bool on) { persistent_ = on; }
 
   // raw buffers (cur = current generation)
   void* rows(int which) { return rows_[which ^ cur_].ptr; }
@@ -269,6 +274,8 @@ class Island {
   // graph replay state
   void run_plain(uint32_t n);
   bool run_tiny(uint32_t n);
+  bool run_multi(uint32_t n);  // n headline generations in one persistent launch (binary_gen_tp_multi)
+  bool persistent_ = false;    // run_multi on (PGA_TP_MULTI=1 or set_persistent)
   bool run_graph(uint32_t reps, bool fresh);
   bool capture_graph();
   void drop_graph();
@@ -291,6 +298,7 @@ class Island {
   uint32_t capture_base_ = 0;
   Buffer gen_dev_;
   Buffer tp_pool_;        // binary_gen_tp pair-pool counters (tp.hpp), GPU BINARY only
+  Buffer multi_bar_;      // binary_gen_tp_multi's grid-barrier counter
   Buffer obj_aux_;        // derived objective table (TSP: the integer matrix as u16, GenArgs::obj_aux)
   uint32_t aux_kind_ = 0, aux_bytes_ = 0, aux_version_ = ~0u;
   bool aux_on_ = true;    // PGA_TSP_NO_LDS unset at construction

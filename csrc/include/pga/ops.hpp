@@ -77,6 +77,25 @@ uint32_t binary_launch(int mode, const GenArgs& a, unsigned long long* best_part
 // binary_launch for one group size GS (binary_gs.hip, one translation unit per GS)
 template <int GS>
 uint32_t binary_launch_group(int mode, const GenArgs& a, unsigned long long* best_parts, hipStream_t s);
+// Persistent multi-generation launch of the headline kernel
+// (binary_dev.hpp binary_gen_tp_multi): `gens` generations from `a`
+// (generation 0), generation i writing best / stats partials parts[i & 1] /
+// stats[i & 1]; barrier: 4 device bytes (zeroed by the launch).  Returns the
+// grid (every generation's partial count) or 0 when the arguments do not
+// qualify (nothing launched: run plain launches).
+struct MultiGenArgs {
+  unsigned long long* parts[2];
+  float* stats[2];
+  uint32_t gens;
+  uint32_t* barrier;
+  // fused key histogram (GenArgs::key_hist) rotation: generation i writes
+  // hist[(rot + i) % 3] and zeroes hist[(rot + i + 1) % 3] (hist[0] nullptr: off)
+  uint32_t* hist[3] = {nullptr, nullptr, nullptr};
+  uint32_t hist_rot = 0, hist_bins = 0, hist_zero_words = 0;
+};
+uint32_t binary_launch_multi(const GenArgs& a, const MultiGenArgs& mg, hipStream_t s);
+template <int GS>
+uint32_t binary_launch_multi_group(const GenArgs& a, const MultiGenArgs& mg, hipStream_t s);
 // whether the last binary_launch on this host thread handed GenArgs::key_hist
 // to its kernel (so the fused key histogram was written and hist_zero
 // cleared); the island marks a histogram valid only on this report

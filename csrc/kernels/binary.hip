@@ -99,6 +99,22 @@ bool& binary_hist_written() {
   return w;
 }
 
+uint32_t binary_launch_multi(const GenArgs& a, const MultiGenArgs& mg, hipStream_t s) {
+  if (mg.gens < 2 || force_generic_kernels()) return 0;
+  uint32_t grid = 0;
+  switch (group_size(a.chunks)) {
+    case 1: grid = binary_launch_multi_group<1>(a, mg, s); break;
+    case 2: grid = binary_launch_multi_group<2>(a, mg, s); break;
+    case 4: grid = binary_launch_multi_group<4>(a, mg, s); break;
+    case 8: grid = binary_launch_multi_group<8>(a, mg, s); break;
+    case 16: grid = binary_launch_multi_group<16>(a, mg, s); break;
+    case 32: grid = binary_launch_multi_group<32>(a, mg, s); break;
+    default: grid = binary_launch_multi_group<64>(a, mg, s); break;
+  }
+  PGA_HIP_CHECK(hipGetLastError());
+  return grid;
+}
+
 uint32_t binary_launch(int mode, const GenArgs& a, unsigned long long* best_parts, hipStream_t s) {
   uint32_t grid = 0;
   binary_hist_written() = false;  // go_tp sets it when its kernel takes the histogram

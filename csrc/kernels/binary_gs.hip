@@ -46,6 +46,60 @@ uint32_t go_tp(K kernel, const GenArgs& a0, unsigned long long* parts, hipStream
   return t.grid;
 }
 
+// G generations in one persistent launch (binary_dev.hpp binary_gen_tp_multi):
+// only the headline geometry (one 16-wave block per CU), else 0 (run them
+// one launch each)
+template <typename K>
+uint32_t go_tp_multi(K kernel, const GenArgs& a0, const MultiGenArgs& mg, hipStream_t s) {
+  const TpGeom t = tp_geometry(a0.S, 1, (const void*)kernel, 64 / group_size(a0.chunks));
+  if (t.block != kTpMaxWaves * 64 || t.grid > (uint32_t)device_cu_count()) return 0;
+  GenMulti m;
+  m.a = a0;
+  m.a.tp_unit = t.unit;
+  m.a.tp_pool = nullptr;
+  m.a.tp_pool_units = 0;
+  m.a.tp_skew = tp_skew_units(t, a0.S);
+  const bool hist = mg.hist[0] && mg.hist[1] && mg.hist[2] && mg.hist_bins > 0 && mg.hist_bins <= kHistMaxBins;
+  m.a.key_hist = nullptr;
+  m.a.hist_zero = nullptr;
+  m.a.hist_bins = hist ? mg.hist_bins : 0u;
+  m.a.hist_zero_words = hist ? mg.hist_zero_words : 0u;
+  for (int j = 0; j < 3; ++j) m.hist[j] = hist ? mg.hist[j] : nullptr;
+  m.hist_rot = mg.hist_rot;
+  m.parts[0] = mg.parts[0];
+  m.parts[1] = mg.parts[1];
+  m.stats[0] = mg.stats[0];
+  m.stats[1] = mg.stats[1];
+  m.gens = mg.gens;
+  m.bar = mg.barrier;
+  PGA_HIP_CHECK(hipMemsetAsync(mg.barrier, 0, 4, s));
+  hipLaunchKernelGGL(kernel, t.grid, t.block, t.lds + (hist ? 4u * mg.hist_bins : 0u), s, m);
+  binary_hist_written() = hist;
+  return t.grid;
+}
+
+template <int GS, int OBJ>
+uint32_t launch_multi(const GenArgs& a, const MultiGenArgs& mg, hipStream_t s) {
+  if constexpr (OBJ == OBJ_ONEMAX || OBJ == OBJ_LEADING_ONES || OBJ == OBJ_TRAP) {
+    uint32_t gs = 0;
+    bool full = false, dense = false;
+    if (a.chunks > (uint32_t)GS || !binary_tp_plan(a, gs, full, dense) || gs != (uint32_t)GS) return 0;
+    if (a.key_cur == nullptr || a.key_next == nullptr || a.n_elite > 1 ||
+        !(a.selection == SEL_TOURNAMENT || a.selection == SEL_RANDOM))
+      return 0;
+    if (full) {
+      if (dense) return go_tp_multi(binary_gen_tp_multi<GS, OBJ, true, true>, a, mg, s);
+      return go_tp_multi(binary_gen_tp_multi<GS, OBJ, true, false>, a, mg, s);
+    }
+    if (dense) return go_tp_multi(binary_gen_tp_multi<GS, OBJ, false, true>, a, mg, s);
+    return go_tp_multi(binary_gen_tp_multi<GS, OBJ, false, false>, a, mg, s);
+  }
+  (void)a;
+  (void)mg;
+  (void)s;
+  return 0;
+}
+
 template <int GS, int OBJ>
 uint32_t launch_mode(int mode, const GenArgs& a, unsigned long long* parts, hipStream_t s) {
   constexpr uint32_t gpb = kBlock / GS;
@@ -110,6 +164,16 @@ uint32_t launch_obj(int mode, const GenArgs& a, unsigned long long* parts, hipSt
 template <>
 uint32_t binary_launch_group<PGA_BIN_GS>(int mode, const GenArgs& a, unsigned long long* best_parts, hipStream_t s) {
   return launch_obj<PGA_BIN_GS>(mode, a, best_parts, s);
+}
+
+template <>
+uint32_t binary_launch_multi_group<PGA_BIN_GS>(const GenArgs& a, const MultiGenArgs& mg, hipStream_t s) {
+  switch (a.objective) {
+    case OBJ_ONEMAX: return launch_multi<PGA_BIN_GS, OBJ_ONEMAX>(a, mg, s);
+    case OBJ_TRAP: return launch_multi<PGA_BIN_GS, OBJ_TRAP>(a, mg, s);
+    case OBJ_LEADING_ONES: return launch_multi<PGA_BIN_GS, OBJ_LEADING_ONES>(a, mg, s);
+    default: return 0;
+  }
 }
 
 #if defined(PGA_TP_TIMING) && PGA_BIN_GS == 8

@@ -198,6 +198,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def_property("migration_policy", &Island::migration_policy, &Island::set_migration_policy)
       .def_property("fused_histogram", &Island::fused_histogram, &Island::set_fused_histogram)
       .def_property_readonly("fused_histogram_ready", &Island::fused_histogram_ready)
+      .def_property("persistent", &Island::persistent, &Island::set_persistent)
       .def("config", [](Island& i) { return i.config(); })
       .def("set_operators", [](Island& i, const pga::Config& c) { bind_stream(i); i.set_operators(c); })
       .def("set_objective_data",

@@ -498,3 +498,28 @@ def test_fused_migration_matches_unfused_f32(S, k, prob):
     b.run(2)
     torch.cuda.synchronize()
     assert torch.equal(a.rows, b.rows) and torch.equal(a.scores, b.scores)
+
+
+@pytest.mark.parametrize("S,L,mut", [(1 << 20, 1024, "bit_flip"), (300_000, 512, "bit_flip"), (400_000, 100, "reset_one")])
+def test_persistent_multi_generation_bitexact(S, L, mut):
+    """Island.run(n) at the headline geometry takes ONE persistent launch of n
+    generations (binary_gen_tp_multi: device-wide barrier between them):
+    rows, scores and the best equal n plain launches (PGA_TP_MULTI=0 path
+    inside one process is not switchable, so: the CPU backend) bit for bit,
+    also at partial lane groups (L = 100) and with the fused key histogram
+    the island model turns on (its top-k then matches the CPU's)."""
+    g, c = pair(pga.models.OneMax(L), S, seed=13, elitism=1, mutation=mut)
+    g.island.persistent = True  # (off by default: measured slower)
+    g.island.fused_histogram = True
+    g.run(5)
+    c.run(5)
+    same(g, c)
+    assert g.best_score() == c.best_score() and g.generation == c.generation == 5
+    assert g.island.fused_histogram_ready
+    for largest in (True, False):
+        assert torch.equal(g.island.topk(777, largest, False).cpu(), c.island.topk(777, largest, False))
+    g.run(1)  # a single generation: the plain launch after the persistent one
+    c.run(1)
+    g.run(3)
+    c.run(3)
+    same(g, c)
