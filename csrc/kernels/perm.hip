@@ -69,6 +69,34 @@ __device__ __forceinline__ uint32_t group_excl_scan(uint32_t v, uint32_t q, uint
   return inc - v;
 }
 
+// The same exclusive scan for groups of 16, 32 or 64 lanes on DPP row
+// shifts and row broadcasts (VALU, no LDS crossbar round trip per level);
+// smaller groups take group_excl_scan.  Integer sums: any order is exact.
+template <int GS>
+__device__ __forceinline__ uint32_t group_excl_scan_dpp(uint32_t v, uint32_t q, uint32_t& total) {
+  if constexpr (GS < 16) {
+    return group_excl_scan<GS>(v, q, total);
+  } else {
+    int inc = (int)v;
+    inc += __builtin_amdgcn_update_dpp(0, inc, 0x111, 0xf, 0xf, false);  // row_shr:1
+    inc += __builtin_amdgcn_update_dpp(0, inc, 0x112, 0xf, 0xf, false);  // row_shr:2
+    inc += __builtin_amdgcn_update_dpp(0, inc, 0x114, 0xf, 0xf, false);  // row_shr:4
+    inc += __builtin_amdgcn_update_dpp(0, inc, 0x118, 0xf, 0xf, false);  // row_shr:8
+    if constexpr (GS >= 32) inc += __builtin_amdgcn_update_dpp(0, inc, 0x142, 0xa, 0xf, false);  // row_bcast:15 -> rows 1, 3
+    if constexpr (GS == 64) inc += __builtin_amdgcn_update_dpp(0, inc, 0x143, 0xc, 0xf, false);  // row_bcast:31 -> rows 2, 3
+    if constexpr (GS == 16) {
+      total = (uint32_t)__shfl(inc, (int)((lane_id() & ~15u) | 15u), 64);
+    } else if constexpr (GS == 32) {
+      const uint32_t t0 = (uint32_t)__builtin_amdgcn_readlane(inc, 31), t1 = (uint32_t)__builtin_amdgcn_readlane(inc, 63);
+      total = lane_id() < 32u ? t0 : t1;
+    } else {
+      total = (uint32_t)__builtin_amdgcn_readlane(inc, 63);
+    }
+    (void)q;
+    return (uint32_t)inc - v;
+  }
+}
+
 __device__ __forceinline__ void ld8(const uint16_t* p, uint32_t e[8]) {
   const uint4 v = *(const uint4*)p;
   e[0] = v.x & 0xFFFF; e[1] = v.x >> 16; e[2] = v.y & 0xFFFF; e[3] = v.y >> 16;
@@ -587,10 +615,14 @@ __device__ __forceinline__ void perm_gen_fast_body(GenArgs a, unsigned long long
           for (uint32_t e = 0; e < 8; ++e)
             keep |= (!((padm8 >> e) & 1u) && pa8[e] - lo >= hi - lo) ? (1u << e) : 0u;
           const uint32_t below = range8(base, 0, hi);  // B positions before the segment end
-          const uint32_t Eb = group_sum_u<GS>(__popc(keep & below));
+          // one scan of both counts (16 bits each: at most L <= 65535 genes): the
+          // group's kept genes before this lane (low half) and, in total, the
+          // kept genes before the segment end (high half)
+          uint32_t both;
+          const uint32_t ex2 = group_excl_scan_dpp<GS>(__popc(keep) | (__popc(keep & below) << 16), q, both);
+          const uint32_t Eb = both >> 16;
           const uint32_t K = L - (hi - lo);
-          uint32_t seg_total;
-          uint32_t run = group_excl_scan<GS>(__popc(keep), q, seg_total);
+          uint32_t run = ex2 & 0xFFFFu;
           wave_sync();  // every read of A's inverse is done before the child overwrites it
           // kept gene of rank r (B order from position 0) -> child position
           // hi + ((r - Eb) mod K), wrapped at L; a gene not kept writes the

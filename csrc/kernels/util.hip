@@ -713,14 +713,75 @@ constexpr uint64_t kLbAgg = 1ull << 62, kLbMask31 = 0x7FFFFFFFull;
 // unless grev: then G is a value-order histogram read only (the generation
 // kernel's fused histogram, GenArgs::key_hist), bin b at G[R - 1 - b] for the
 // smallest, and nothing re-zeroes it
+// Two-pass selection, first pass (fused value-order histogram): the
+// threshold exactly as topk16_select_kernel derives it, and the block's (gt,
+// eq) counts over the same range -> counts[2 b], counts[2 b + 1]
+__global__ __launch_bounds__(kBlock) void topk16_count2_kernel(const uint16_t* k16, uint64_t S, uint64_t per_block,
+                                                               uint32_t R, bool largest, uint32_t k, const uint32_t* G,
+                                                               uint32_t* counts) {
+  __shared__ uint32_t sh_T;
+  __shared__ uint32_t lds[kBlock / 64];
+  const uint32_t per = (R + kBlock - 1) / kBlock;
+  uint32_t mine = 0;
+  for (uint32_t j = 0; j < per; ++j) {
+    const int64_t b = (int64_t)R - 1 - (int64_t)threadIdx.x * per - j;
+    if (b >= 0) mine += G[!largest ? R - 1 - b : b];
+  }
+  uint32_t tot;
+  const uint32_t before = block_excl_scan_u(mine, lds, tot);
+  if (before < k && before + mine >= k) {
+    uint32_t acc = before;
+    for (uint32_t j = 0; j < per; ++j) {
+      const int64_t b = (int64_t)R - 1 - (int64_t)threadIdx.x * per - j;
+      if (b < 0) break;
+      const uint32_t c = G[!largest ? R - 1 - b : b];
+      if (acc + c >= k) {
+        sh_T = (uint32_t)b;
+        break;
+      }
+      acc += c;
+    }
+  }
+  __syncthreads();
+  const uint32_t T = largest ? sh_T : sh_T + 0x10000u - R;
+  const uint32_t flip = largest ? 0u : 0xFFFFu;
+  const uint64_t pt = ((per_block + kBlock - 1) / kBlock + 15) / 16 * 16;
+  const uint64_t blo = (uint64_t)blockIdx.x * per_block;
+  const uint64_t bhi = blo + per_block < S ? blo + per_block : S;
+  const uint64_t t0 = blo + threadIdx.x * pt;
+  const uint64_t t1 = t0 + pt < bhi ? t0 + pt : bhi;
+  uint32_t gt = 0, eq = 0;
+  for (uint64_t c0 = t0; c0 < t1; c0 += 16) {
+    uint32_t kv[16];
+    const uint32_t m = load_keys16(k16, c0, t1, kv);
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const uint32_t key = min(kv[e], R - 1) ^ flip;
+      gt += ((m >> e) & 1u) && key > T;
+      eq += ((m >> e) & 1u) && key == T;
+    }
+  }
+  auto add = [](uint32_t x, uint32_t y) { return x + y; };
+  gt = block_reduce(gt, lds, add);
+  eq = block_reduce(eq, lds, add);
+  if (threadIdx.x == 0) {
+    counts[2 * blockIdx.x] = gt;
+    counts[2 * blockIdx.x + 1] = eq;
+  }
+}
+
+// counts (two-pass mode, fused histograms only): the per-block (gt, eq)
+// counts of topk16_count2_kernel, complete before this launch — every block
+// reads its predecessors' instead of publishing and polling status words
 __global__ __launch_bounds__(kBlock) void topk16_select_kernel(const uint16_t* k16, uint64_t S, uint64_t per_block,
                                                                uint32_t R, bool largest, uint32_t k, uint32_t* G,
                                                                uint64_t* status, uint32_t* ctr, uint32_t nblocks,
-                                                               uint32_t* idx_out, TopkMove mv, bool fused) {
+                                                               uint32_t* idx_out, TopkMove mv, bool fused,
+                                                               const uint32_t* counts = nullptr) {
   __shared__ uint32_t sel_pos[kTopkMoveSlots], sel_src[kTopkMoveSlots];  // row moves: output position, source
   __shared__ uint32_t sh_T, sh_need, sh_b;
   __shared__ uint32_t lds[kBlock / 64];
-  if (threadIdx.x == 0) sh_b = atomicAdd(&ctr[0], 1u);
+  if (threadIdx.x == 0) sh_b = counts ? blockIdx.x : atomicAdd(&ctr[0], 1u);
   // threshold bin: thread t owns bins [R-1 - (t+1)*per + 1, R-1 - t*per], counted from the top
   const uint32_t per = (R + kBlock - 1) / kBlock;
   uint32_t mine = 0;
@@ -769,12 +830,17 @@ __global__ __launch_bounds__(kBlock) void topk16_select_kernel(const uint16_t* k
   uint32_t og = block_excl_scan_u(gt, lds, bg);
   __syncthreads();
   uint32_t oe = block_excl_scan_u(eq, lds, be);
-  if (threadIdx.x == 0)
+  if (threadIdx.x == 0 && !counts)
     __hip_atomic_store(&status[b], kLbAgg | ((uint64_t)bg << 31) | (uint64_t)be, __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_AGENT);
   // block prefix = sum of the predecessors' aggregates, read in parallel
   uint32_t pg = 0, pe = 0;
   for (uint32_t j = threadIdx.x; j < b; j += kBlock) {
+    if (counts) {
+      pg += counts[2 * j];
+      pe += counts[2 * j + 1];
+      continue;
+    }
     uint64_t w = 0;
     for (uint32_t spins = 0; spins < (1u << 26); ++spins) {  // bound: never hang the device
       w = __hip_atomic_load(&status[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -788,7 +854,7 @@ __global__ __launch_bounds__(kBlock) void topk16_select_kernel(const uint16_t* k
   pe = block_reduce(pe, lds, add);
   // every other block published its aggregate, hence had read the histogram:
   // the last ticket zeroes it for the next selection
-  if (b == nblocks - 1 && !fused)
+  if (b == nblocks - 1 && !fused && !counts)
     for (uint32_t i = threadIdx.x; i < R; i += kBlock) G[i] = 0;
   uint32_t gpos = pg + og, epos = pe + oe;
   // with a row move, the block's selections are listed in LDS first (slot:
@@ -1536,9 +1602,16 @@ uint32_t topk_launch(const float* scores, const uint16_t* keys16, uint32_t key_r
         // the generation kernel's histogram of these keys, its status words
         // zeroed by that kernel: the select alone (one pass over the keys)
         uint64_t* fst = (uint64_t*)fused->status;
+        // PGA_TOPK_2PASS=1 (A/B): a count launch, then the select reads the
+        // complete counts instead of publishing and polling status words
+        static const bool two = std::getenv("PGA_TOPK_2PASS") && std::getenv("PGA_TOPK_2PASS")[0] == '1';
+        uint32_t* counts = two ? (uint32_t*)fused->status : nullptr;  // 2 words per block <= kTopkStatusWords
+        if (two)
+          hipLaunchKernelGGL(topk16_count2_kernel, cgrid, kBlock, 0, s, keys16, S, pb16, R, largest, k,
+                             fused->hist, counts);
         hipLaunchKernelGGL(topk16_select_kernel, cgrid, kBlock, 0, s, keys16, S, pb16, R, largest, k,
                            const_cast<uint32_t*>(fused->hist), fst, (uint32_t*)(fst + cgrid), cgrid, idx_out,
-                           mv ? *mv : TopkMove{}, true);
+                           mv ? *mv : TopkMove{}, true, (const uint32_t*)counts);
         PGA_HIP_CHECK(hipGetLastError());
         return mv && mv->mode == TopkMove::SCATTER && mv->best_parts ? cgrid : 0u;
       }
