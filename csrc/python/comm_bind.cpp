@@ -70,6 +70,7 @@ struct EngineComm {
   std::vector<pga::LocalRank> pending;  // the posted epoch (empty: none)
   hipStream_t compute = nullptr;        // the island's stream at post time
   bool on_transport = false;            // the epoch's device work runs on the transport stream
+  bool early_eval = false;              // the migrants were re-scored on the transport stream at post time
   hipEvent_t ev_pop = nullptr, ev_out = nullptr, ev_in = nullptr;
   ~EngineComm() {
     for (hipEvent_t ev : {ev_pop, ev_out, ev_in})
@@ -164,6 +165,26 @@ void bind_comm(py::module& m) {
              if (e.on_transport) PGA_HIP_CHECK(hipEventRecord(e.ev_out, local[0].stream));
              e.comm->self_exchange = e.nranks == 1;
              e.comm->exchange(ring_plan(e.rank, dst, src, k), local);
+             // PGA_MIG_EVAL_EARLY=1: the re-scoring of the received rows is
+             // enqueued now, behind the transfer on the transport stream, so
+             // it runs as soon as the rows land (in the drain of the
+             // generation beside it) instead of after finish()'s host check
+             e.early_eval = false;
+             static const bool early = std::getenv("PGA_MIG_EVAL_EARLY") && std::getenv("PGA_MIG_EVAL_EARLY")[0] == '1';
+             hipStream_t ts = early ? e.comm->transport_stream(local[0]) : nullptr;
+             if (ts) {
+               if (!e.ev_in) PGA_HIP_CHECK(hipEventCreateWithFlags(&e.ev_in, hipEventDisableTiming));
+               isl->stream = ts;
+               try {
+                 isl->evaluate_rows(local[0].recv_rows, local[0].recv_scores, k);
+               } catch (...) {
+                 isl->stream = e.compute;
+                 throw;
+               }
+               isl->stream = e.compute;
+               PGA_HIP_CHECK(hipEventRecord(e.ev_in, ts));
+               e.early_eval = true;
+             }
              e.pending = std::move(local);
            })
       // complete the epoch: false = failed / expired (the communicator was
@@ -185,7 +206,9 @@ void bind_comm(py::module& m) {
                ok = e.comm->wait(local, timeout_s);
              }
              if (!ok) return false;
-             if (validate) {
+             if (e.early_eval) {  // re-scored at post time: the compute stream waits for that
+               PGA_HIP_CHECK(hipStreamWaitEvent(compute, e.ev_in, 0));
+             } else if (validate) {
                isl->stream = e.on_transport ? local[0].stream : compute;
                try {
                  isl->evaluate_rows(local[0].recv_rows, local[0].recv_scores, k);
@@ -195,7 +218,7 @@ void bind_comm(py::module& m) {
                }
                isl->stream = compute;
              }
-             if (e.on_transport) {  // the compute stream takes the re-scored immigrants
+             if (e.on_transport && !e.early_eval) {  // the compute stream takes the re-scored immigrants
                PGA_HIP_CHECK(hipEventRecord(e.ev_in, local[0].stream));
                PGA_HIP_CHECK(hipStreamWaitEvent(compute, e.ev_in, 0));
              }
