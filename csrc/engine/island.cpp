@@ -390,7 +390,10 @@ GenArgs Island::make_args(int mode) {
 }
 
 uint32_t Island::launch(int mode, const GenArgs& a, unsigned long long* parts) {
-  if (mode != MODE_GEN && a.cur == rows_[cur_].ptr) fhist_of_[0] = fhist_of_[1] = -1;  // staged / init / eval
+  if (mode != MODE_GEN && a.cur == rows_[cur_].ptr) {  // staged / init / eval
+    fhist_of_[0] = fhist_of_[1] = -1;
+    rank_cnt_of_ = -1;
+  }
   if (on_gpu()) return encoding_launch(mode, a, parts, stream);
   return cpu::encoding_run(mode, a, parts);
 }
@@ -485,9 +488,13 @@ void Island::prepare_generation() {
   }
   if (cfg_.selection == SEL_RANK) {
     const float* sc = (const float*)scores_[cur_].ptr;
-    if (on_gpu() && integer_objective(cfg_.objective, cfg_.L) && keys_[cur_].ptr)
+    if (on_gpu() && integer_objective(cfg_.objective, cfg_.L) && keys_[cur_].ptr) {
+      // the tile counts of these keys, when the GEN kernel that wrote them stored them
+      const bool ready = rank_cnt_of_ == cur_ && !capturing_;
+      rank_cnt_of_ = -1;  // the sort scans them in place
       rank_order16_launch((const uint16_t*)keys_[cur_].ptr, cfg_.S, cfg_.L + 1, (uint32_t*)rank_order_.ptr,
-                          rank_ws_.ptr, stream);
+                          rank_ws_.ptr, stream, ready);
+    }
     else if (on_gpu()) rank_order_launch(sc, cfg_.S, (uint32_t*)rank_order_.ptr, rank_ws_.ptr, stream);
     else cpu::rank_order(sc, cfg_.S, (uint32_t*)rank_order_.ptr);
   }
@@ -508,6 +515,7 @@ void Island::run(uint32_t n) {
     }
     const uint32_t reps = n / graph_g_;
     fhist_of_[0] = fhist_of_[1] = -1;  // replays do not produce the fused histograms
+    rank_cnt_of_ = -1;                 // (nor rank counts; their sorts overwrite the workspace)
     if (run_graph(reps, fresh)) n -= reps * graph_g_;
   }
   if (run_multi(n)) return;
@@ -543,6 +551,7 @@ bool Island::run_multi(uint32_t n) {
   TraceRange tr("pga.generations_multi", 2);
   const uint32_t grid = binary_launch_multi(a, mg, stream);
   if (grid == 0) return false;
+  rank_cnt_of_ = -1;
   fh = fh && binary_hist_written();
   for (uint32_t i = 0; i < n; ++i) {  // the bookkeeping of n plain generations
     n_best_[cur_ ^ 1] = grid;
@@ -594,6 +603,7 @@ void Island::run_plain(uint32_t n) {
     prepare_generation();
     GenArgs a = make_args(MODE_GEN);
     if (jit_ && fused_jit_generation(a)) {  // the objective linked into the generation kernel
+      rank_cnt_of_ = -1;
       swap();
       if (hist_on_ && !hist_manual_ && !capturing_) append_history();
       continue;
@@ -605,8 +615,11 @@ void Island::run_plain(uint32_t n) {
       a.hist_bins = cfg_.L + 1;
       a.hist_zero_words = fused_hist_words(cfg_.L + 1);
     }
+    a.rank_counts = rank_counts_for_gen();
+    if (a.rank_counts) a.hist_bins = cfg_.L + 1;
     n_best_[cur_ ^ 1] = launch(MODE_GEN, a, (unsigned long long*)best_[cur_ ^ 1].ptr);
     stats_ok_[cur_ ^ 1] = a.stats_parts != nullptr;
+    rank_cnt_of_ = a.rank_counts && binary_rank_counts_written() ? (cur_ ^ 1) : -1;
     // valid only when the launcher reports that its kernel took the histogram
     // (binary_gs.hip go_tp), not on the conditions predicted above
     fh = fh && binary_hist_written();
@@ -707,6 +720,7 @@ bool Island::run_batched(const std::vector<Island*>& isls, uint32_t n, hipStream
       I.stats_ok_[nx] = args[k].stats_parts != nullptr;
       I.qk_valid_[nx] = real && args[k].qk != nullptr;  // the REAL kernel writes the keys it is given
       I.fhist_of_[nx] = -1;  // the batched launch produces no fused histogram
+      I.rank_cnt_of_ = -1;
       I.swap();
     }
   }
@@ -966,6 +980,19 @@ void Island::immigrate(uint32_t k, const void* in_rows, const float* in_scores) 
 void Island::set_fused_histogram(bool on) {
   fhist_user_ = on;
   fhist_on_ = on || cfg_.n_elite > 1;
+}
+
+uint32_t* Island::rank_counts_for_gen() const {
+  // the launcher (binary_gs.hip go_tp) takes them only at the sort's tile geometry
+  if (cfg_.selection != SEL_RANK || !on_gpu() || capturing_ || jit_ || cfg_.encoding != ENC_BINARY) return nullptr;
+  if (!integer_objective(cfg_.objective, cfg_.L) || cfg_.objective == OBJ_KNAPSACK || !keys_[0].ptr) return nullptr;
+  if (cfg_.L + 1 > kHistMaxBins || !rank_ws_.ptr) return nullptr;
+  static const bool off = [] {  // PGA_RANK_FUSED=0: the sort counts its keys itself (A/B knob)
+    const char* e = std::getenv("PGA_RANK_FUSED");
+    return e && e[0] == '0';
+  }();
+  if (off) return nullptr;
+  return rank_order16_counts(rank_ws_.ptr, cfg_.S, cfg_.L + 1);
 }
 
 bool Island::fhist_ready_for(const GenArgs& a) const {

@@ -516,7 +516,7 @@ __device__ __forceinline__ void binary_gen_tp_body(GenArgs a, unsigned long long
   uint4* lds_stage = (uint4*)(pga_dyn_lds + NW * 4096u + pcap * 8u) + wid * (kJitStageSteps * 64u);
   (void)lds_stage;
   uint32_t* lds_hist = (uint32_t*)(pga_dyn_lds + NW * 4096u + pcap * 8u);  // (never with the JIT staging)
-  const bool hist = HISTK && a.key_hist != nullptr;  // block-uniform
+  const bool hist = HISTK && (a.key_hist != nullptr || a.rank_counts != nullptr);  // block-uniform
   const uint32_t hmax = a.hist_bins - 1u;
   // the pair pool (tp.hpp): one round, tournament or random selection; the
   // block's own units end at own_end, the last P units are the pair's
@@ -977,7 +977,8 @@ __device__ __forceinline__ void binary_gen_tp_body(GenArgs a, unsigned long long
   if (hist)  // every wave passed the last round's barrier: the block's counts are complete
     for (uint32_t i = threadIdx.x; i < a.hist_bins; i += blockDim.x) {
       const uint32_t v = lds_hist[i];
-      if (v) __hip_atomic_fetch_add(&a.key_hist[i], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (a.key_hist && v) __hip_atomic_fetch_add(&a.key_hist[i], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (a.rank_counts) a.rank_counts[i * gridDim.x + blockIdx.x] = v;  // this block's sort tile
     }
   if (EVALS && best_parts) {  // block-uniform
     unsigned long long bb = block_max_u64_n(my_best, lds_red, NW);

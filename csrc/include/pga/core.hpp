@@ -381,6 +381,13 @@ struct GenArgs {
   // binary_gen_tp: child rows stored non-temporally (experiment knob,
   // PGA_TP_NT_STORE=1; 0: ordinary stores)
   uint32_t nt_store;
+  // rank selection (binary_gen_tp, integer objectives): when set, every block
+  // also stores its LDS key histogram, all hist_bins bins, to
+  // rank_counts[bin * gridDim.x + blockIdx.x]: the tile counts of the next
+  // generation's rank-order sort (sort.hip, rank_order16_counts), whose count
+  // pass then reads nothing.  The launcher sets it only when each block's
+  // children are exactly one kRankTile sort tile.
+  uint32_t* rank_counts;
 };
 // the fused histogram's LDS bins (binary_gen_tp): objectives with more key
 // values use the separate histogram pass

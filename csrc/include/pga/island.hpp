@@ -234,6 +234,7 @@ class Island {
   void invalidate_qk() {
     qk_valid_[cur_] = false;
     fhist_of_[cur_] = -1;  // the keys of the current population change
+    if (rank_cnt_of_ == cur_) rank_cnt_of_ = -1;
   }
   Buffer qk_ws_;
   bool qk_valid_[2] = {false, false};
@@ -282,6 +283,7 @@ class Island {
   void invalidate() {
     ++version_;
     fhist_of_[0] = fhist_of_[1] = -1;
+    rank_cnt_of_ = -1;
   }
   // fused key histograms: three buffers of fused_hist_words(L + 1) words
   // rotated by the generations that produce one (each zeroes the next);
@@ -292,6 +294,12 @@ class Island {
   uint32_t fhist_rot_ = 0;
   bool fhist_on_ = false, fhist_user_ = false;
   bool fhist_ready_for(const GenArgs& a) const;  // this GEN launch produces the histogram
+  // rank selection of an integer objective: the GEN kernel also stores the
+  // next rank sort's tile counts into rank_ws_ (GenArgs::rank_counts);
+  // rank_cnt_of_ = the parity whose keys they count (-1: none), consumed by
+  // the next prepare_generation's sort
+  int rank_cnt_of_ = -1;
+  uint32_t* rank_counts_for_gen() const;
   const TopkFused* fused_select(TopkFused& f);    // the current population's histogram for a select
   uint32_t graph_g_ = 0, version_ = 0;
   bool graph_broken_ = false, capturing_ = false;

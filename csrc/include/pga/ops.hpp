@@ -100,6 +100,8 @@ uint32_t binary_launch_multi_group(const GenArgs& a, const MultiGenArgs& mg, hip
 // to its kernel (so the fused key histogram was written and hist_zero
 // cleared); the island marks a histogram valid only on this report
 bool& binary_hist_written();
+// the same report for GenArgs::rank_counts (the next rank sort's tile counts)
+bool& binary_rank_counts_written();
 // whether a MODE_GEN launch of these arguments takes the hot two-phase kernel
 // (binary_gen_tp) and which variant: group size, full groups, dense mutation.
 // For f32-score objectives (the fused JIT generation kernel, jit.hpp).
@@ -213,7 +215,14 @@ void rank_order_launch(const float* scores, uint64_t S, uint32_t* order, void* w
 // the same order from the u16 tournament keys of an integer objective (keys
 // < key_range: only their bits are sorted, 2 passes for OneMax-1024)
 void rank_order16_launch(const uint16_t* keys16, uint64_t S, uint32_t key_range, uint32_t* order, void* workspace,
-                         hipStream_t s);
+                         hipStream_t s, bool counts_ready = false);
+// The sort's per-tile key counts (counts[key * tiles + tile], tiles of
+// kRankTile keys) in the workspace, when the u16 sort of this key range is a
+// single pass whose digit is the whole key; else nullptr.  A producer that
+// stores exactly these counts (binary_gen_tp's GenArgs::rank_counts) lets
+// the next rank_order16_launch run with counts_ready, skipping its count pass.
+constexpr uint32_t kRankTile = 4096;
+uint32_t* rank_order16_counts(void* workspace, uint64_t S, uint32_t key_range);
 // top-k by score (descending, ties -> lower index); idx_out[k]; workspace: topk_workspace_bytes(S)
 size_t topk_workspace_bytes(uint64_t S, uint32_t k);
 // sorted = false: the k indices in selection order (keys above the threshold by

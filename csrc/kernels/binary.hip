@@ -99,6 +99,11 @@ bool& binary_hist_written() {
   return w;
 }
 
+bool& binary_rank_counts_written() {
+  static thread_local bool w = false;
+  return w;
+}
+
 uint32_t binary_launch_multi(const GenArgs& a, const MultiGenArgs& mg, hipStream_t s) {
   if (mg.gens < 2 || force_generic_kernels()) return 0;
   uint32_t grid = 0;
@@ -118,6 +123,7 @@ uint32_t binary_launch_multi(const GenArgs& a, const MultiGenArgs& mg, hipStream
 uint32_t binary_launch(int mode, const GenArgs& a, unsigned long long* best_parts, hipStream_t s) {
   uint32_t grid = 0;
   binary_hist_written() = false;  // go_tp sets it when its kernel takes the histogram
+  binary_rank_counts_written() = false;
   switch (group_size(a.chunks)) {  // one translation unit per group size (binary_gs.hip)
     case 1: grid = binary_launch_group<1>(mode, a, best_parts, s); break;
     case 2: grid = binary_launch_group<2>(mode, a, best_parts, s); break;

@@ -41,8 +41,18 @@ uint32_t go_tp(K kernel, const GenArgs& a0, unsigned long long* parts, hipStream
   const bool hist = key_obj && a.key_cur != nullptr && a.key_hist != nullptr && a.hist_bins > 0 &&
                     a.hist_bins <= kHistMaxBins;
   if (!hist) a.key_hist = nullptr;
-  hipLaunchKernelGGL(kernel, t.grid, t.block, t.lds + (hist ? 4u * a.hist_bins : 0u), s, a, parts);
+  // the rank sort's tile counts: only when block b's children are exactly
+  // sort tile b (tp_share with a share of kRankTile, a multiple of every
+  // unit; no pair pool).  The share skew (PGA_TP_SKEW, worth ~0.5 us at the
+  // headline) is dropped for it: the count pass it saves costs ~6 us.
+  const bool rk = key_obj && a.key_cur != nullptr && a.rank_counts != nullptr && a.hist_bins > 0 &&
+                  a.hist_bins <= kHistMaxBins && a.tp_pool_units == 0 &&
+                  (a.S + t.grid - 1) / t.grid == kRankTile && (uint64_t)t.grid == (a.S + kRankTile - 1) / kRankTile;
+  if (rk) a.tp_skew = 0;
+  else a.rank_counts = nullptr;
+  hipLaunchKernelGGL(kernel, t.grid, t.block, t.lds + (hist || rk ? 4u * a.hist_bins : 0u), s, a, parts);
   binary_hist_written() = hist;
+  binary_rank_counts_written() = rk;
   return t.grid;
 }
 
@@ -62,6 +72,7 @@ uint32_t go_tp_multi(K kernel, const GenArgs& a0, const MultiGenArgs& mg, hipStr
   const bool hist = mg.hist[0] && mg.hist[1] && mg.hist[2] && mg.hist_bins > 0 && mg.hist_bins <= kHistMaxBins;
   m.a.key_hist = nullptr;
   m.a.hist_zero = nullptr;
+  m.a.rank_counts = nullptr;
   m.a.hist_bins = hist ? mg.hist_bins : 0u;
   m.a.hist_zero_words = hist ? mg.hist_zero_words : 0u;
   for (int j = 0; j < 3; ++j) m.hist[j] = hist ? mg.hist[j] : nullptr;

@@ -7,8 +7,8 @@
 //   COUNT    a workgroup per TILE of 4096 keys counts its digits into
 //            counts[digit * tiles + tile] (digit-major);
 //   SCAN     exclusive scan of counts: each entry becomes the global output
-//            base of (digit, tile) — one launch of 1024 threads when the table
-//            fits 16384 entries (1M keys / 6-bit digits does), else two levels;
+//            base of (digit, tile) — one launch of 4096-entry chunks whose
+//            totals (up to 256) the scatter folds itself, else two levels;
 //   SCATTER  the tile again, every wave its own 1024 consecutive keys in 16
 //            rounds of 64: the lanes that share a digit find each other with
 //            one ballot per digit bit (a match-any), rank among themselves by
@@ -30,6 +30,10 @@
 #include "pga/device.hpp"
 #include "pga/ops.hpp"
 
+// dynamic LDS of radix_scatter_wide_kernel (outside the anonymous namespace:
+// an extern __shared__ array has no definition to give it internal linkage)
+extern __shared__ __align__(16) uint8_t pga_sort_dyn_lds[];
+
 namespace pga {
 namespace {
 
@@ -44,8 +48,39 @@ constexpr uint32_t kWideDigits = 1u << kWideBits;
 constexpr uint32_t kWaveKeys = 1024;                   // per wave: 16 rounds of 64
 constexpr uint32_t kRounds = kWaveKeys / 64;
 constexpr uint32_t kTile = kWaveKeys * (kBlock / 64);  // 4096 keys per workgroup
-constexpr uint32_t kScanBlock = 1024, kScanPer = 16;   // one scan workgroup: 16384 entries
+static_assert(kTile == kRankTile, "the fused rank counts (binary_gen_tp) assume the sort's tile");
+// one scan workgroup: 4096 entries.  The rank order of OneMax-1024 at 1M
+// keys scans 1025 x 256 counts: 65 workgroups of 256 threads take 4.9 us
+// where 17 of 1024 threads took 5.5 (profiles/rank_fused_r06.md)
+constexpr uint32_t kScanBlock = 256, kScanPer = 16;
 constexpr uint32_t kScanChunk = kScanBlock * kScanPer;
+// the scatters fold up to this many chunk totals themselves (fold_chunk_sums)
+constexpr uint32_t kScanFold = 256;
+
+// cpre[c] = exclusive prefix of the chunk totals csums[0, nchunks), nchunks
+// <= kScanFold: one wave, 4 totals per lane
+__device__ __forceinline__ void fold_chunk_sums(const uint32_t* __restrict__ csums, uint32_t nchunks, uint32_t* cpre,
+                                                uint32_t lane) {
+  uint32_t c[kScanFold / 64], s = 0;
+#pragma unroll
+  for (uint32_t j = 0; j < kScanFold / 64; ++j) {
+    const uint32_t i = lane * (kScanFold / 64) + j;
+    c[j] = i < nchunks ? csums[i] : 0u;
+    s += c[j];
+  }
+  uint32_t incl = s;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = (uint32_t)__shfl_up((int)incl, o, 64);
+    if (lane >= (uint32_t)o) incl += y;
+  }
+  uint32_t run = incl - s;
+#pragma unroll
+  for (uint32_t j = 0; j < kScanFold / 64; ++j) {
+    cpre[lane * (kScanFold / 64) + j] = run;
+    run += c[j];
+  }
+}
 
 inline size_t al(size_t x) { return (x + 255) & ~(size_t)255; }
 inline uint64_t tiles_of(uint64_t n) { return (n + kTile - 1) / kTile; }
@@ -232,19 +267,10 @@ __global__ __launch_bounds__(kBlock) void radix_scatter_kernel(KeySrc src, const
     key[r] = load_key<SRC>(src, ec);
     val[r] = VAL == 2 ? vin[ec] : (VAL == 1 ? src.vals[ec] : (uint32_t)e);
   }
-  // exclusive prefix of the scan-chunk totals (nchunks <= kScanFold = 64):
+  // exclusive prefix of the scan-chunk totals (nchunks <= kScanFold):
   // one wave's scan into LDS, read per digit below
-  __shared__ uint32_t cpre[64];
-  if (csums && wid == 0) {
-    const uint32_t c = lane < nchunks ? csums[lane] : 0u;
-    uint32_t incl = c;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const uint32_t y = (uint32_t)__shfl_up((int)incl, o, 64);
-      if (lane >= (uint32_t)o) incl += y;
-    }
-    cpre[lane] = incl - c;
-  }
+  __shared__ uint32_t cpre[kScanFold];
+  if (csums && wid == 0) fold_chunk_sums(csums, nchunks, cpre, lane);
   const uint64_t below = (1ull << lane) - 1ull;
   uint32_t pos[kRounds];
 #pragma unroll
@@ -330,13 +356,128 @@ __global__ __launch_bounds__(kBlock) void radix_scatter_kernel(KeySrc src, const
   }
 }
 
+// Single-pass scatter of u16 keys (digit = the whole key, D <= 2048; the
+// value is the key's index): the rank order of an integer objective.  The
+// same stable ranking as radix_scatter_kernel with 16 waves per tile instead
+// of 4 (256 keys each, 4 rounds): one workgroup per CU at the headline, so the
+// 4-wave version left each SIMD a single wave to hide the ranking's LDS
+// round trips and the ballots behind.  Per-wave digit counters are u16 (a
+// tile has 4096 keys) in dynamic LDS sized by D, the tile is staged as u16
+// keys and u16 tile-local indices.
+constexpr uint32_t kWideWaves = 16;
+constexpr uint32_t kWideThreads = kWideWaves * 64;
+constexpr uint32_t kWideRounds = kTile / kWideThreads;  // 4 rounds of 64 keys per wave
+static_assert(kWideDigits % kWideThreads == 0, "digits per thread");
+
+inline uint32_t wide_scatter_lds(uint32_t D) {
+  const uint32_t Dp = (D + 1u) & ~1u;  // u16 rows keep 4-byte alignment
+  return kWideWaves * Dp * 2u + kTile * 2u * 2u + Dp * 4u;
+}
+
+__global__ __launch_bounds__(kWideThreads) void radix_scatter_wide_kernel(
+    const uint16_t* __restrict__ keys, uint64_t n, uint32_t bits, uint32_t D, uint64_t tiles,
+    const uint32_t* __restrict__ base, const uint32_t* __restrict__ csums, uint32_t nchunks,
+    uint32_t* __restrict__ kout, uint32_t* __restrict__ vout) {
+  const uint32_t Dp = (D + 1u) & ~1u;
+  uint16_t* cnt = (uint16_t*)pga_sort_dyn_lds;  // [kWideWaves][Dp]: running counts, then local starts
+  uint16_t* sk = cnt + kWideWaves * Dp;         // the tile in digit order: keys ...
+  uint16_t* sv = sk + kTile;                    // ... and their tile-local indices
+  uint32_t* gofs = (uint32_t*)(sv + kTile);     // [Dp]: output index = gofs[d] + staged position
+  __shared__ uint32_t wsum[kWideWaves];
+  __shared__ uint32_t cpre[kScanFold];
+  const uint32_t lane = lane_id(), wid = threadIdx.x >> 6, t = threadIdx.x;
+  uint16_t* mine = cnt + wid * Dp;
+  for (uint32_t d = lane; d < D; d += 64) mine[d] = 0;  // this wave's row (its LDS ops retire in order)
+  const uint64_t t0 = (uint64_t)blockIdx.x * kTile;
+  const uint32_t l0 = wid * (kTile / kWideWaves);  // this wave's first tile-local key
+  uint32_t key[kWideRounds];
+#pragma unroll
+  for (uint32_t r = 0; r < kWideRounds; ++r) {  // every load in flight before the ranking
+    const uint64_t e = t0 + l0 + r * 64u + lane;
+    key[r] = keys[e < n ? e : n - 1];  // unconditional load
+  }
+  if (csums && wid == 0) fold_chunk_sums(csums, nchunks, cpre, lane);  // (nchunks <= kScanFold)
+  const uint64_t below = (1ull << lane) - 1ull;
+  uint32_t pos[kWideRounds];
+#pragma unroll
+  for (uint32_t r = 0; r < kWideRounds; ++r) {
+    const bool ok = t0 + l0 + r * 64u + lane < n;
+    const uint32_t dig = ok ? min(key[r], D - 1) : D;
+    key[r] = dig;
+    const uint64_t peers = match_digit(dig, ok, bits);
+    const uint32_t rk = (uint32_t)__popcll(peers & below);
+    const uint32_t c = ok ? mine[dig] : 0u;
+    __builtin_amdgcn_wave_barrier();
+    if (ok && rk == 0u) mine[dig] = (uint16_t)(c + (uint32_t)__popcll(peers));
+    __builtin_amdgcn_wave_barrier();
+    pos[r] = ok ? c + rk : 0xFFFFFFFFu;
+  }
+  __syncthreads();
+  // per digit: the waves' counts become waves-before offsets, then local starts
+  constexpr uint32_t P = kWideDigits / kWideThreads;  // digits per thread: [t P, t P + P)
+  uint32_t tcs[P], tsum = 0;
+#pragma unroll
+  for (uint32_t j = 0; j < P; ++j) {
+    const uint32_t d = t * P + j;
+    uint32_t tc = 0;
+    if (d < D) {
+#pragma unroll
+      for (uint32_t w = 0; w < kWideWaves; ++w) {
+        const uint32_t c = cnt[w * Dp + d];
+        cnt[w * Dp + d] = (uint16_t)tc;
+        tc += c;
+      }
+    }
+    tcs[j] = tc;
+    tsum += tc;
+  }
+  uint32_t incl = tsum;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = (uint32_t)__shfl_up((int)incl, o, 64);
+    if (lane >= (uint32_t)o) incl += y;
+  }
+  if (lane == 63) wsum[wid] = incl;
+  __syncthreads();
+  uint32_t ls = incl - tsum;
+  for (uint32_t w = 0; w < wid; ++w) ls += wsum[w];
+#pragma unroll
+  for (uint32_t j = 0; j < P; ++j) {
+    const uint32_t d = t * P + j;
+    if (d < D) {
+#pragma unroll
+      for (uint32_t w = 0; w < kWideWaves; ++w) cnt[w * Dp + d] = (uint16_t)(cnt[w * Dp + d] + ls);
+      const uint64_t e = (uint64_t)d * tiles + blockIdx.x;
+      const uint32_t pre = csums ? cpre[e / kScanChunk] : 0u;
+      gofs[d] = base[e] + pre - ls;
+    }
+    ls += tcs[j];
+  }
+  __syncthreads();
+#pragma unroll
+  for (uint32_t r = 0; r < kWideRounds; ++r) {
+    if (pos[r] != 0xFFFFFFFFu) {
+      const uint32_t lp = mine[key[r]] + pos[r];
+      sk[lp] = (uint16_t)key[r];
+      sv[lp] = (uint16_t)(l0 + r * 64u + lane);
+    }
+  }
+  __syncthreads();
+  const uint32_t nt = (uint32_t)(n - t0 < kTile ? n - t0 : kTile);
+  for (uint32_t i = t; i < nt; i += kWideThreads) {
+    const uint32_t k = sk[i];
+    const uint32_t o = gofs[k] + i;
+    if (kout) kout[o] = k;
+    vout[o] = (uint32_t)t0 + sv[i];
+  }
+}
+
 // The scatter's bases with at most kScanFold scan chunks: ONE launch scans
 // each chunk in place and stores the chunk totals; the scatter adds the
 // prefix of the totals itself (one wave scan into LDS) instead of two
 // more launches (scan of the totals, add back: ~4.8 + 5.0 us for the rank
 // order of 1M u16 keys, profiles/rank_kernel_stats_r03.csv).  Returns the
 // chunk count (0: x is fully scanned, nothing to fold).
-constexpr uint32_t kScanFold = 64;
 uint32_t scan_chunks(uint32_t* x, uint64_t m, const RadixWs& w, hipStream_t s);
 
 // exclusive scan of m entries in place (m <= kScanChunk^3)
@@ -373,14 +514,23 @@ uint32_t scan_chunks(uint32_t* x, uint64_t m, const RadixWs& w, hipStream_t s) {
 // one sort: per pass count -> scan -> scatter.  The passes ping-pong between
 // the workspace staging (W) and the output (O); pass i writes O when an even
 // number of passes follows it, so the last one lands in O.
+// Single-pass mode: the keys are below a known range of at most 2^11 values
+// and the digit is the whole key
+bool wide_mode(uint32_t bits, uint32_t key_range) {
+  return key_range >= 2 && key_range <= kWideDigits && bits > kMaxDigitBits && bits <= kWideBits &&
+         (1u << bits) >= key_range;
+}
+
+// counts_ready (single-pass mode only): w.counts already holds the pass's
+// tile counts (a fused producer wrote them), the count launch is skipped.
+// want_keys = false: the last pass stores only the values (kout is still the
+// ping-pong buffer of the passes before it).
 void radix_run(const KeySrc& src0, uint64_t n, uint32_t bits, uint32_t* kout, uint32_t* vout, void* ws, hipStream_t s,
-               uint32_t key_range = 0) {
+               uint32_t key_range = 0, bool counts_ready = false, bool want_keys = true) {
   if (n == 0) return;
   if (n > 0xFFFFFFFFull) throw std::invalid_argument("radix sort: more than 2^32 - 1 keys");
   bits = bits < 1 ? 1 : (bits > 32 ? 32 : bits);
-  // keys below a known range of at most 2^11 values: ONE pass whose digit is the key
-  const bool wide = key_range >= 2 && key_range <= kWideDigits && bits > kMaxDigitBits && bits <= kWideBits &&
-                    (1u << bits) >= key_range;
+  const bool wide = wide_mode(bits, key_range);  // ONE pass whose digit is the key
   const uint32_t passes = wide ? 1u : (bits + kMaxDigitBits - 1) / kMaxDigitBits;
   RadixWs w = radix_ws(ws, n);
   const uint64_t tiles = tiles_of(n);
@@ -392,6 +542,7 @@ void radix_run(const KeySrc& src0, uint64_t n, uint32_t bits, uint32_t* kout, ui
     const uint32_t pb = bits / passes + (p < bits % passes ? 1u : 0u);
     const bool to_out = (passes - 1 - p) % 2 == 0;
     uint32_t* dk = to_out ? kout : w.k;
+    if (p + 1 == passes && !want_keys) dk = nullptr;
     uint32_t* dv = to_out ? vout : w.v;
     KeySrc src = p == 0 ? src0 : KeySrc{ck, nullptr, nullptr, nullptr, false};
     const int kind = p > 0 ? SRC_U32 : (src.k32 ? SRC_U32 : (src.k16 ? SRC_U16 : SRC_F32));
@@ -402,9 +553,12 @@ void radix_run(const KeySrc& src0, uint64_t n, uint32_t bits, uint32_t* kout, ui
 #define PGA_SCATTER(K, V, MD) hipLaunchKernelGGL((radix_scatter_kernel<K, V, MD>), g, kBlock, 0, s, src, cv, n, shift, pb, D, tiles, w.counts, nch ? w.sums : nullptr, nch, dk, dv)
     if (wide) {  // one pass over u16 keys (rank order of an integer objective)
       if (kind != SRC_U16 || vk != 0) throw std::logic_error("radix sort: single-pass mode is for u16 keys");
-      PGA_COUNT(SRC_U16, kWideDigits);
+      if (!counts_ready) PGA_COUNT(SRC_U16, kWideDigits);
       const uint32_t nch = scan_chunks(w.counts, (uint64_t)D * tiles, w, s);
-      PGA_SCATTER(SRC_U16, 0, kWideDigits);
+      const uint32_t lds = wide_scatter_lds(D);
+      if (lds > 64u * 1024u) (void)allow_dynamic_lds((const void*)radix_scatter_wide_kernel);
+      hipLaunchKernelGGL(radix_scatter_wide_kernel, g, kWideThreads, lds, s, src.k16, n, pb, D, tiles, w.counts,
+                         nch ? w.sums : nullptr, nch, dk, dv);
     } else {
       if (kind == SRC_U32) PGA_COUNT(SRC_U32, kMaxDigits);
       if (kind == SRC_U16) PGA_COUNT(SRC_U16, kMaxDigits);
@@ -444,17 +598,31 @@ size_t rank_order_workspace_bytes(uint64_t S) { return radix_sort_workspace_byte
 
 void rank_order_launch(const float* scores, uint64_t S, uint32_t* order, void* ws, hipStream_t s) {
   uint32_t* keys_out = (uint32_t*)((char*)ws + radix_sort_workspace_bytes(S));
-  radix_run(KeySrc{nullptr, nullptr, scores, nullptr, false}, S, 32, keys_out, order, ws, s);
+  radix_run(KeySrc{nullptr, nullptr, scores, nullptr, false}, S, 32, keys_out, order, ws, s, 0, false, false);
 }
 
 // integer objectives: the u16 tournament keys order exactly like the scores;
 // only the bits of the largest possible key (key_range - 1) are sorted
-void rank_order16_launch(const uint16_t* keys16, uint64_t S, uint32_t key_range, uint32_t* order, void* ws,
-                         hipStream_t s) {
+namespace {
+uint32_t key_bits(uint32_t key_range) {
   uint32_t bits = 1;
   while (bits < 16 && (1u << bits) < key_range) ++bits;
+  return bits;
+}
+}  // namespace
+
+void rank_order16_launch(const uint16_t* keys16, uint64_t S, uint32_t key_range, uint32_t* order, void* ws,
+                         hipStream_t s, bool counts_ready) {
+  const uint32_t bits = key_bits(key_range);
+  if (counts_ready && !wide_mode(bits, key_range)) throw std::logic_error("rank order: fused counts need the single pass");
   uint32_t* keys_out = (uint32_t*)((char*)ws + radix_sort_workspace_bytes(S));
-  radix_run(KeySrc{nullptr, keys16, nullptr, nullptr, false}, S, bits, keys_out, order, ws, s, key_range);
+  radix_run(KeySrc{nullptr, keys16, nullptr, nullptr, false}, S, bits, keys_out, order, ws, s, key_range, counts_ready,
+            false);
+}
+
+uint32_t* rank_order16_counts(void* ws, uint64_t S, uint32_t key_range) {
+  if (!ws || S == 0 || !wide_mode(key_bits(key_range), key_range)) return nullptr;
+  return radix_ws(ws, S).counts;
 }
 
 }  // namespace pga

@@ -91,6 +91,7 @@ def test_knapsack_matrix_cores_bitexact(L, scale, digits):
 
 @pytest.mark.parametrize("S,L,sel,elitism", [(1048576, 1024, "tournament", 1), (1048576, 1024, "rank", 3),
                                               (1600000, 1024, "tournament", 3), (1600000, 1024, "rank", 1),
+                                              (1047576, 1024, "rank", 1),
                                               (1900000, 256, "tournament", 1), (300000, 64, "roulette", 1),
                                               (200000, 1024, "tournament", 2)])
 def test_headline_geometry_bitexact(S, L, sel, elitism):
@@ -426,6 +427,24 @@ def test_rank_selection_u16_keys_partial_tile_bitexact():
     kw = dict(seed=13, elitism=1, selection="rank")
     g = pga.GeneticAlgorithm(p, 70_001, device="cuda:0", **kw)
     c = pga.GeneticAlgorithm(p, 70_001, device="cpu", **kw)
+    for _ in range(3):
+        g.run(1)
+        c.run(1)
+        torch.cuda.synchronize()
+        assert torch.equal(g.rows.cpu(), c.rows)
+        assert torch.equal(g.scores.cpu(), c.scores)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("L,S", [(300, 9000), (2000, 5000), (1500, 20_000)])
+def test_rank_selection_single_pass_widths(L, S):
+    """The single-pass rank order (digit = the whole u16 key, 9..11 bits;
+    L = 2000 needs more than 64 KiB of dynamic LDS in the 16-wave scatter)
+    against the CPU backend over partial tiles."""
+    p = pga.models.OneMax(L)
+    kw = dict(seed=3, elitism=1, selection="rank", rank_pressure=1.8)
+    g = pga.GeneticAlgorithm(p, S, device="cuda:0", **kw)
+    c = pga.GeneticAlgorithm(p, S, device="cpu", **kw)
     for _ in range(3):
         g.run(1)
         c.run(1)
