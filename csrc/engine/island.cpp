@@ -180,7 +180,7 @@ void Island::set_operators(const Config& c) {
     elite_idx_ = alloc(4ull * cfg_.n_elite);
   }
   if (cfg_.selection == SEL_ROULETTE && !cumfit_.ptr) {
-    cumfit_ = alloc(4ull * cfg_.S);
+    cumfit_ = alloc(4ull * (cfg_.S + 4));  // + 4: the GEN kernels' 16-byte window loads (tp.hpp)
     if (on_gpu()) {
       cum_ws_ = alloc(4ull * roulette_workspace_floats(cfg_.S));
       roul_guide_ = alloc(4ull * (cfg_.S + 1));

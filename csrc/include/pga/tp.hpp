@@ -118,9 +118,25 @@ __device__ __forceinline__ void tp_select_segment(const GenArgs& a, uint32_t beg
       tg[i] = word_to_unit(w) * total;
       ix[i] = total > 0.f ? ld32<uint32_t>(a.roul_guide, roulette_bucket(tg[i], scale, S)) : word_to_index(w, S);
     }
+    // the first cumfit load is the aligned 16-byte window holding the guide
+    // entry (cumfit is padded by 4 floats): a pick within it is resolved
+    // without a dependent load, one past it scans on from the window's end
     float v[NS];
     #pragma unroll
-    for (uint32_t i = 0; i < NS; ++i) v[i] = ld32<float>(a.cumfit, ix[i]);
+    for (uint32_t i = 0; i < NS; ++i) {
+      const uint32_t b = ix[i] & ~3u, off = ix[i] - b;
+      const float4 w = *(const float4*)((const char*)a.cumfit + b * 4u);
+      // step over the window entries below the target, in order (the padding
+      // past cumfit[S - 1] = total is never reached: total >= every target)
+      uint32_t p = off;
+      p = p == 0u && w.x < tg[i] ? 1u : p;
+      p = p == 1u && w.y < tg[i] ? 2u : p;
+      p = p == 2u && w.z < tg[i] ? 3u : p;
+      p = p == 3u && w.w < tg[i] ? 4u : p;
+      const bool live = total > 0.f;
+      ix[i] = live ? (p == 4u ? b + 3u : b + p) : ix[i];
+      v[i] = live && p == 4u ? -INFINITY : tg[i];  // -inf: step to b + 4 and load it below
+    }
     for (uint32_t it = 0; it < S; ++it) {  // wave-uniform: until every pick of every lane is resolved
       bool more = false;
       #pragma unroll
