@@ -336,10 +336,13 @@ void score_stats(const float* s, uint64_t S, float* out) {
 void roulette_prefix(const float* s, uint64_t S, float* cumfit) {
   float st[4];
   score_stats(s, S, st);
-  float acc = 0.f;
+  // accumulated in f64 and rounded once per entry: integer weights give the
+  // exact prefix the GPU's integer roulette computes (util.hip
+  // roulette_fused_kernel) at any population size
+  double acc = 0.0;
   for (uint64_t i = 0; i < S; ++i) {
-    acc += std::fmax(s[i] - st[0], 0.f);
-    cumfit[i] = acc;
+    acc += (double)std::fmax(s[i] - st[0], 0.f);
+    cumfit[i] = (float)acc;
   }
 }
 

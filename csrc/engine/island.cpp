@@ -403,10 +403,10 @@ void Island::initialize() {
   invalidate_qk();
   GenArgs a = make_args(MODE_INIT);
   n_best_[cur_] = launch(MODE_INIT, a, (unsigned long long*)best_[cur_].ptr);
-  stats_ok_[cur_] = a.stats_parts != nullptr;
+  set_stats_ok(cur_, a.stats_parts != nullptr);
   if (jit_) {
     n_best_[cur_] = jit_eval(rows_[cur_].ptr, (float*)scores_[cur_].ptr, cfg_.S, (unsigned long long*)best_[cur_].ptr);
-    stats_ok_[cur_] = false;
+    set_stats_ok(cur_, false);
   } else if (cfg_.objective == OBJ_NONE) {
     rebest();
   }
@@ -417,16 +417,16 @@ void Island::evaluate() {
   invalidate_qk();
   if (jit_) {
     n_best_[cur_] = jit_eval(rows_[cur_].ptr, (float*)scores_[cur_].ptr, cfg_.S, (unsigned long long*)best_[cur_].ptr);
-    stats_ok_[cur_] = false;
+    set_stats_ok(cur_, false);
     return;
   }
   GenArgs a = make_args(MODE_EVAL);
   n_best_[cur_] = launch(MODE_EVAL, a, (unsigned long long*)best_[cur_].ptr);
-  stats_ok_[cur_] = a.stats_parts != nullptr;
+  set_stats_ok(cur_, a.stats_parts != nullptr);
 }
 
 void Island::rebest() {
-  stats_ok_[cur_] = false;
+  set_stats_ok(cur_, false);
   invalidate_qk();
   const float* sc = (const float*)scores_[cur_].ptr;
   if (on_gpu()) {
@@ -477,10 +477,17 @@ void Island::prepare_generation() {
   }
   if (cfg_.selection == SEL_ROULETTE) {
     const float* sc = (const float*)scores_[cur_].ptr;
-    if (on_gpu()) {
-      const bool fused = stats_ok_[cur_] && stats_parts_[cur_].ptr;  // min from the GEN kernel's partials
+    const bool fused = on_gpu() && stats_ok_[cur_] && stats_parts_[cur_].ptr;  // min from the GEN kernel's partials
+    // integer objectives after a two-phase GEN launch: one exact launch
+    // (the partials give every block its carry)
+    const bool one = fused && stats_part_[cur_].grid && integer_objective(cfg_.objective, cfg_.L) &&
+                     cfg_.objective != OBJ_KNAPSACK && !roul_fused_off() &&
+                     roulette_fused_launch(sc, cfg_.S, (const float*)stats_parts_[cur_].ptr, stats_part_[cur_], cfg_.L,
+                                           (float*)cumfit_.ptr, (uint32_t*)roul_guide_.ptr, (float*)cum_ws_.ptr, stream);
+    if (one) {
+    } else if (on_gpu()) {
       roulette_prefix_launch(sc, cfg_.S, fused ? (const float*)stats_parts_[cur_].ptr : nullptr, n_best_[cur_],
-                             (float*)cumfit_.ptr, (float*)cum_ws_.ptr, stream);
+                             (float*)cumfit_.ptr, (float*)cum_ws_.ptr, stream, integer_objective(cfg_.objective, cfg_.L));
       roulette_guide_launch((const float*)cumfit_.ptr, cfg_.S, (uint32_t*)roul_guide_.ptr, (float*)cum_ws_.ptr, stream);
     } else {
       cpu::roulette_prefix(sc, cfg_.S, (float*)cumfit_.ptr);
@@ -555,7 +562,7 @@ bool Island::run_multi(uint32_t n) {
   fh = fh && binary_hist_written();
   for (uint32_t i = 0; i < n; ++i) {  // the bookkeeping of n plain generations
     n_best_[cur_ ^ 1] = grid;
-    stats_ok_[cur_ ^ 1] = a.stats_parts != nullptr;
+    set_stats_ok(cur_ ^ 1, a.stats_parts != nullptr);
     if (fh) {
       const int w = (int)(fhist_rot_ % 3), z = (int)((fhist_rot_ + 1) % 3);
       ++fhist_rot_;
@@ -591,8 +598,8 @@ bool Island::run_tiny(uint32_t n) {
   // generations lived in LDS): no valid partials there until a kernel writes them
   n_best_[cur_] = 1;
   n_best_[cur_ ^ 1] = 0;
-  stats_ok_[cur_] = a.stats_parts != nullptr;
-  stats_ok_[cur_ ^ 1] = false;
+  set_stats_ok(cur_, a.stats_parts != nullptr);
+  set_stats_ok(cur_ ^ 1, false);
   qk_valid_[0] = qk_valid_[1] = false;
   return true;
 }
@@ -618,7 +625,9 @@ void Island::run_plain(uint32_t n) {
     a.rank_counts = rank_counts_for_gen();
     if (a.rank_counts) a.hist_bins = cfg_.L + 1;
     n_best_[cur_ ^ 1] = launch(MODE_GEN, a, (unsigned long long*)best_[cur_ ^ 1].ptr);
-    stats_ok_[cur_ ^ 1] = a.stats_parts != nullptr;
+    set_stats_ok(cur_ ^ 1, a.stats_parts != nullptr);
+    if (a.stats_parts && cfg_.encoding == ENC_BINARY && on_gpu() && binary_tp_partition().grid == n_best_[cur_ ^ 1])
+      stats_part_[cur_ ^ 1] = binary_tp_partition();  // (the roulette prefix's carries, roulette_fused_launch)
     rank_cnt_of_ = a.rank_counts && binary_rank_counts_written() ? (cur_ ^ 1) : -1;
     // valid only when the launcher reports that its kernel took the histogram
     // (binary_gs.hip go_tp), not on the conditions predicted above
@@ -637,7 +646,7 @@ void Island::run_plain(uint32_t n) {
     if (jit_) {
       n_best_[cur_ ^ 1] = jit_eval(rows_[cur_ ^ 1].ptr, (float*)scores_[cur_ ^ 1].ptr, cfg_.S,
                                    (unsigned long long*)best_[cur_ ^ 1].ptr);
-      stats_ok_[cur_ ^ 1] = false;
+      set_stats_ok(cur_ ^ 1, false);
     }
     swap();
     if (hist_on_ && !hist_manual_ && !capturing_) append_history();
@@ -717,7 +726,7 @@ bool Island::run_batched(const std::vector<Island*>& isls, uint32_t n, hipStream
       Island& I = *isls[k];
       const int nx = I.cur_ ^ 1;
       I.n_best_[nx] = grid;
-      I.stats_ok_[nx] = args[k].stats_parts != nullptr;
+      I.set_stats_ok(nx, args[k].stats_parts != nullptr);
       I.qk_valid_[nx] = real && args[k].qk != nullptr;  // the REAL kernel writes the keys it is given
       I.fhist_of_[nx] = -1;  // the batched launch produces no fused histogram
       I.rank_cnt_of_ = -1;
@@ -944,7 +953,7 @@ void Island::immigrate(uint32_t k, const void* in_rows, const float* in_scores) 
       float* sp = fused_stats() ? (float*)stats_parts_[cur_].ptr : nullptr;
       n_best_[cur_] = stripe_immigrate_launch((float*)scores_[cur_].ptr, k16, rows_[cur_].ptr, row_words_, cfg_.S, k,
                                               in_rows, in_scores, (unsigned long long*)best_[cur_].ptr, sp, stream);
-      stats_ok_[cur_] = sp != nullptr;
+      set_stats_ok(cur_, sp != nullptr);
     } else {
       cpu::stripe_immigrate((float*)scores_[cur_].ptr, rows_[cur_].ptr, row_words_, cfg_.S, k, in_rows, in_scores);
       rebest();
@@ -969,7 +978,7 @@ void Island::immigrate(uint32_t k, const void* in_rows, const float* in_scores) 
     n_best_[cur_] = nb ? nb
                        : best_of_scores_launch((const float*)scores_[cur_].ptr, cfg_.S,
                                                (unsigned long long*)best_[cur_].ptr, stream, nullptr);
-    stats_ok_[cur_] = false;
+    set_stats_ok(cur_, false);
     return;
   }
   uint32_t* idx = (uint32_t*)scratch(4ull * k);
@@ -980,6 +989,14 @@ void Island::immigrate(uint32_t k, const void* in_rows, const float* in_scores) 
 void Island::set_fused_histogram(bool on) {
   fhist_user_ = on;
   fhist_on_ = on || cfg_.n_elite > 1;
+}
+
+bool Island::roul_fused_off() {
+  static const bool off = [] {
+    const char* e = std::getenv("PGA_ROUL_FUSED");
+    return e && e[0] == '0';
+  }();
+  return off;
 }
 
 uint32_t* Island::rank_counts_for_gen() const {
@@ -1078,7 +1095,7 @@ bool Island::fused_jit_generation(GenArgs& a) {
   const int nx = cur_ ^ 1;
   a.stats_parts = (float*)stats_parts_[nx].ptr;  // the fused kernel stores {min, sum} partials like the built-ins
   n_best_[nx] = jit_->gen_launch(f, &a, sizeof(a), cfg_.S, (unsigned long long*)best_[nx].ptr, kMaxGrid, stream);
-  stats_ok_[nx] = a.stats_parts != nullptr;
+  set_stats_ok(nx, a.stats_parts != nullptr);
   qk_valid_[nx] = false;
   ++jit_fused_gens_;
   return true;

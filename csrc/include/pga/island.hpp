@@ -20,6 +20,7 @@
 
 #include "pga/core.hpp"
 #include "pga/jit.hpp"
+#include "pga/ops.hpp"
 
 namespace pga {
 struct TopkFused;  // ops.hpp
@@ -249,6 +250,14 @@ class Island {
   // that wrote best_[p]); stats_ok_[p]: they belong to the current best_[p]
   Buffer stats_parts_[2];
   bool stats_ok_[2] = {false, false};
+  // stats_part_[p]: the block partition of the binary_gen_tp launch whose
+  // partials stats_parts_[p] holds (grid 0: another kernel wrote them)
+  TpPartition stats_part_[2] = {{0, 0, 0}, {0, 0, 0}};
+  void set_stats_ok(int p, bool ok) {
+    stats_ok_[p] = ok;
+    stats_part_[p] = TpPartition{0, 0, 0};
+  }
+  static bool roul_fused_off();  // PGA_ROUL_FUSED=0: the three-launch roulette prefix (A/B knob)
   bool fused_stats() const;  // the evaluating kernels of this configuration store them
   void append_history();
   Buffer hist_;

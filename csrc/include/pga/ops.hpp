@@ -102,6 +102,14 @@ uint32_t binary_launch_multi_group(const GenArgs& a, const MultiGenArgs& mg, hip
 bool& binary_hist_written();
 // the same report for GenArgs::rank_counts (the next rank sort's tile counts)
 bool& binary_rank_counts_written();
+// the block partition of the last binary_gen_tp launch on this host thread
+// (grid 0: the launch took another kernel): block j wrote children
+// tp_share(S, unit, j, skew) and stored their {min, sum} partials at
+// stats_parts[2 j] (no pair pool)
+struct TpPartition {
+  uint32_t grid, unit, skew;
+};
+TpPartition& binary_tp_partition();
 // whether a MODE_GEN launch of these arguments takes the hot two-phase kernel
 // (binary_gen_tp) and which variant: group size, full groups, dense mutation.
 // For f32-score objectives (the fused JIT generation kernel, jit.hpp).
@@ -199,9 +207,19 @@ void stats_from_parts_launch(const float* parts, const unsigned long long* best,
 // (parts, nparts blocks) when given, else from a score pass.
 constexpr uint32_t kRoulScale = 4 + 3 * 1024 + 1024;
 size_t roulette_workspace_floats(uint64_t S);
+// integer = true: the scores are integers (integer_objective): u64 sums, the
+// exact prefix rounded once per entry
 void roulette_prefix_launch(const float* scores, uint64_t S, const float* parts, uint32_t nparts, float* cumfit,
-                            float* workspace, hipStream_t s);
+                            float* workspace, hipStream_t s, bool integer = false);
 void roulette_guide_launch(const float* cumfit, uint64_t S, uint32_t* guide, float* workspace, hipStream_t s);
+// Both in ONE launch for an integer objective whose current population came
+// from binary_gen_tp with partition `part`: its {min, sum} partials (parts,
+// part.grid blocks) give every block its carry, so no pass precedes the scan.
+// The weights and prefix sums are exact integers (cumfit[i] = the prefix
+// rounded to f32 once).  max_score: the objective's largest score; returns
+// false (nothing launched) when a partial sum could be inexact in f32.
+bool roulette_fused_launch(const float* scores, uint64_t S, const float* parts, const TpPartition& part,
+                           uint32_t max_score, float* cumfit, uint32_t* guide, float* workspace, hipStream_t s);
 // stable LSD radix sort (sort.hip: reduce-then-scan, digits of up to 8 bits,
 // count / scan / scatter launches per pass): (keys, vals) by the low `bits`
 // bits of the keys, ascending, or descending (all 32 bits; equal keys keep

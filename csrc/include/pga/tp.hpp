@@ -221,7 +221,7 @@ constexpr uint32_t kTpMaxSegs = tp_par_cap(kTpMaxWaves) / (kSegBatches * 64);  /
 #endif
 __host__ __device__ constexpr uint32_t tp_prefetch_depth(uint32_t gs) { return gs < PGA_TP_PD ? gs : PGA_TP_PD; }
 
-__device__ __forceinline__ uint32_t tp_unit(const GenArgs& a, uint32_t NG) {
+__host__ __device__ inline uint32_t tp_unit(const GenArgs& a, uint32_t NG) {  // (the launchers record it)
   const uint32_t u = a.tp_unit, lo = NG * tp_prefetch_depth(64u / NG);
   return u >= lo && u <= 64u && (u & (u - 1u)) == 0u ? u : 64u;
 }

@@ -104,6 +104,11 @@ bool& binary_rank_counts_written() {
   return w;
 }
 
+TpPartition& binary_tp_partition() {
+  static thread_local TpPartition p{0, 0, 0};
+  return p;
+}
+
 uint32_t binary_launch_multi(const GenArgs& a, const MultiGenArgs& mg, hipStream_t s) {
   if (mg.gens < 2 || force_generic_kernels()) return 0;
   uint32_t grid = 0;
@@ -124,6 +129,7 @@ uint32_t binary_launch(int mode, const GenArgs& a, unsigned long long* best_part
   uint32_t grid = 0;
   binary_hist_written() = false;  // go_tp sets it when its kernel takes the histogram
   binary_rank_counts_written() = false;
+  binary_tp_partition() = TpPartition{0, 0, 0};
   switch (group_size(a.chunks)) {  // one translation unit per group size (binary_gs.hip)
     case 1: grid = binary_launch_group<1>(mode, a, best_parts, s); break;
     case 2: grid = binary_launch_group<2>(mode, a, best_parts, s); break;

@@ -53,6 +53,7 @@ uint32_t go_tp(K kernel, const GenArgs& a0, unsigned long long* parts, hipStream
   hipLaunchKernelGGL(kernel, t.grid, t.block, t.lds + (hist || rk ? 4u * a.hist_bins : 0u), s, a, parts);
   binary_hist_written() = hist;
   binary_rank_counts_written() = rk;
+  if (a.tp_pool_units == 0) binary_tp_partition() = TpPartition{t.grid, tp_unit(a, 64u / group_size(a.chunks)), a.tp_skew};
   return t.grid;
 }
 

@@ -334,6 +334,77 @@ __global__ __launch_bounds__(kBlock) void prefix_final_kernel(const float* s, ui
   }
 }
 
+// Integer objectives: the same two passes with u64 weight sums, so cumfit[i]
+// is the exact prefix rounded once to f32 — what roulette_fused_kernel and the
+// CPU backend's f64 prefix give, at any population size.
+template <int BLK>
+__device__ __forceinline__ unsigned long long block_sum_u64(unsigned long long v, unsigned long long* lds) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  __syncthreads();
+  if (lane_id() == 0) lds[threadIdx.x >> 6] = v;
+  __syncthreads();
+  unsigned long long t = 0;
+  for (uint32_t w = 0; w < BLK / 64; ++w) t += lds[w];
+  return t;
+}
+
+__global__ __launch_bounds__(kBlock) void prefix_part_int_kernel(const float* s, uint64_t S, uint64_t per_block,
+                                                                 const float* parts, uint32_t nparts, float* stats,
+                                                                 unsigned long long* block_sums) {
+  __shared__ float lds[kBlock / 64];
+  __shared__ unsigned long long lds64[kBlock / 64];
+  float mn;
+  if (parts) {
+    mn = parts_min(parts, nparts, lds);
+    if (blockIdx.x == 0 && threadIdx.x == 0) stats[0] = mn;
+  } else {
+    mn = stats[0];
+  }
+  const uint64_t b0 = (uint64_t)blockIdx.x * per_block;
+  const uint64_t b1 = b0 + per_block < S ? b0 + per_block : S;
+  unsigned long long sm = 0;
+  for (uint64_t i = b0 + threadIdx.x; i < b1; i += kBlock) sm += (unsigned long long)fmaxf(s[i] - mn, 0.f);
+  sm = block_sum_u64<kBlock>(sm, lds64);
+  if (threadIdx.x == 0) block_sums[blockIdx.x] = sm;
+}
+
+__global__ __launch_bounds__(kBlock) void prefix_final_int_kernel(const float* s, uint64_t S, uint64_t per_block,
+                                                                  const float* stats,
+                                                                  const unsigned long long* block_sums, float* cumfit,
+                                                                  float* meta) {
+  __shared__ unsigned long long lds64[kBlock / 64];
+  const float mn = stats[0];
+  unsigned long long pre = 0;
+  for (uint32_t j = threadIdx.x; j < blockIdx.x; j += kBlock) pre += block_sums[j];
+  unsigned long long carry = block_sum_u64<kBlock>(pre, lds64);
+  const uint32_t lane = lane_id(), wid = threadIdx.x >> 6;
+  const uint64_t b0 = (uint64_t)blockIdx.x * per_block;
+  const uint64_t b1 = b0 + per_block < S ? b0 + per_block : S;
+  for (uint64_t t0 = b0; t0 < b1; t0 += kBlock) {
+    const uint64_t i = t0 + threadIdx.x;
+    const unsigned long long v = i < b1 ? (unsigned long long)fmaxf(s[i] - mn, 0.f) : 0ull;
+    unsigned long long inc = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const unsigned long long y = __shfl_up(inc, o, 64);
+      if (lane >= (uint32_t)o) inc += y;
+    }
+    __syncthreads();
+    if (lane == 63) lds64[wid] = inc;
+    __syncthreads();
+    unsigned long long off = 0, total = 0;
+    for (uint32_t w = 0; w < kBlock / 64; ++w) {
+      off += w < wid ? lds64[w] : 0ull;
+      total += lds64[w];
+    }
+    const float c = __ull2float_rn(carry + off + inc);
+    if (i < b1) cumfit[i] = c;
+    if (i == S - 1) meta[0] = c > 0.f ? (float)S / c : 0.f;  // guide scale (roulette_bucket)
+    carry += total;
+  }
+}
+
 // guide[b] = i for every bucket b in (bucket(cumfit[i-1]), bucket(cumfit[i])].
 // Spans of 32 buckets or more (one individual holding >= 32/S of the total
 // weight) are queued in LDS and filled by the whole block, so no thread loops
@@ -366,6 +437,133 @@ __global__ __launch_bounds__(kBlock) void roulette_guide_kernel(const float* c, 
       for (uint32_t b = sp.x + threadIdx.x; b <= sp.y; b += kBlock) guide[b] = sp.z;
     }
     __syncthreads();
+  }
+}
+
+// Roulette in ONE launch for an integer objective (roulette_fused_launch):
+// block j of this grid takes the children block j of the generation kernel
+// wrote (tp_share over the same grid), whose {min, sum} partials are exact
+// integers in f32.  Every block reduces all partials itself: the minimum, the
+// weight total sum_i - n_i * min of every partial, the total and the sum of
+// the partials before it (its carry), in u64 — so the three-launch chain
+// (partials pass, carry + scan, guide) becomes one, and the prefix sums are
+// exact (cumfit[i] = the integer prefix rounded once; the guide scale is
+// S / cumfit[S - 1] as in prefix_final_kernel).  The block then scans its
+// range (kRoulPer consecutive individuals per thread, loaded and stored
+// coalesced through LDS) and fills the guide
+// buckets of its individuals as roulette_guide_kernel does.
+constexpr uint32_t kRoulThreads = 1024, kRoulPer = 8, kRoulSpans = 1024;
+
+__global__ __launch_bounds__(kRoulThreads) void roulette_fused_kernel(const float* __restrict__ s, uint64_t S,
+                                                                      const float* __restrict__ parts, uint32_t unit,
+                                                                      uint32_t skew, float* __restrict__ cumfit,
+                                                                      uint32_t* __restrict__ guide, float* meta) {
+  __shared__ unsigned long long red[kRoulThreads / 64];
+  __shared__ float fred[kRoulThreads / 64];
+  __shared__ uint32_t wsum[kRoulThreads / 64];
+  __shared__ uint4 spans[kRoulSpans];
+  __shared__ uint32_t nsp;
+  __shared__ __align__(16) uint32_t xch[kRoulThreads * kRoulPer];  // a chunk's weights, then its cumfit values
+  const uint32_t t = threadIdx.x, lane = lane_id(), wid = t >> 6, np = gridDim.x;
+  const uint32_t Su = (uint32_t)S;
+  float mn = __builtin_inff();
+  for (uint32_t i = t; i < np; i += kRoulThreads) mn = fminf(mn, parts[2 * i]);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) mn = fminf(mn, __shfl_xor(mn, o, 64));
+  if (lane == 0) fred[wid] = mn;
+  __syncthreads();
+  mn = fred[0];
+  for (uint32_t w = 1; w < kRoulThreads / 64; ++w) mn = fminf(mn, fred[w]);
+  const unsigned long long mnu = (unsigned long long)mn;  // an integer objective's scores are >= 0
+  unsigned long long below = 0, tot = 0;
+  for (uint32_t i = t; i < np; i += kRoulThreads) {
+    uint32_t b0, b1;
+    tp_share(Su, unit, i, b0, b1, skew);
+    const unsigned long long w = b1 > b0 ? (unsigned long long)parts[2 * i + 1] - (unsigned long long)(b1 - b0) * mnu : 0ull;
+    tot += w;
+    below += i < blockIdx.x ? w : 0ull;
+  }
+  tot = block_sum_u64<kRoulThreads>(tot, red);
+  below = block_sum_u64<kRoulThreads>(below, red);
+  const float total = __ull2float_rn(tot);
+  const float scale = tot > 0ull ? (float)S / total : 0.f;
+  if (blockIdx.x == 0 && t == 0) meta[0] = scale;
+  uint32_t bb, be;
+  tp_share(Su, unit, blockIdx.x, bb, be, skew);
+  unsigned long long carry = below;
+  for (uint32_t c0 = bb; c0 < be; c0 += kRoulThreads * kRoulPer) {  // block-uniform
+    // coalesced loads, transposed through LDS: thread t scans the kRoulPer
+    // consecutive weights [t P, t P + P) of the chunk
+#pragma unroll
+    for (uint32_t k = 0; k < kRoulPer; ++k) {
+      const uint32_t i = c0 + k * kRoulThreads + t;
+      const float v = i < be ? s[i] : mn;
+      xch[k * kRoulThreads + t] = (uint32_t)fmaxf(v - mn, 0.f);
+    }
+    if (t == 0) nsp = 0;
+    __syncthreads();
+    uint32_t w[kRoulPer], ts = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < kRoulPer; j += 4) {
+      const uint4 q = *(const uint4*)&xch[t * kRoulPer + j];
+      w[j] = q.x;
+      w[j + 1] = q.y;
+      w[j + 2] = q.z;
+      w[j + 3] = q.w;
+    }
+#pragma unroll
+    for (uint32_t j = 0; j < kRoulPer; ++j) ts += w[j];
+    uint32_t incl = ts;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t y = (uint32_t)__shfl_up((int)incl, o, 64);
+      if (lane >= (uint32_t)o) incl += y;
+    }
+    if (lane == 63) wsum[wid] = incl;
+    __syncthreads();  // (every thread has read its weights: xch is reused for the prefix sums)
+    uint32_t off = incl - ts, ctot = 0;
+    for (uint32_t q = 0; q < kRoulThreads / 64; ++q) {
+      off += q < wid ? wsum[q] : 0u;
+      ctot += wsum[q];
+    }
+    unsigned long long run = carry + off;  // the exact prefix before the thread's first individual
+    float c[kRoulPer];
+#pragma unroll
+    for (uint32_t j = 0; j < kRoulPer; ++j) {
+      run += w[j];
+      c[j] = __ull2float_rn(run);
+    }
+#pragma unroll
+    for (uint32_t j = 0; j < kRoulPer; j += 4)
+      *(float4*)&xch[t * kRoulPer + j] = make_float4(c[j], c[j + 1], c[j + 2], c[j + 3]);
+    __syncthreads();
+    // coalesced stores; the guide buckets of individual i, as roulette_guide_kernel
+    const float prev0 = __ull2float_rn(carry);  // = cumfit[c0 - 1]
+#pragma unroll
+    for (uint32_t k = 0; k < kRoulPer; ++k) {
+      const uint32_t e = k * kRoulThreads + t, i = c0 + e;
+      if (i < be) {
+        const float ci = __builtin_bit_cast(float, xch[e]);
+        const float prev = e ? __builtin_bit_cast(float, xch[e - 1]) : prev0;
+        cumfit[i] = ci;
+        const uint32_t hi = roulette_bucket(ci, scale, Su);
+        const uint32_t lo = i ? roulette_bucket(prev, scale, Su) + 1u : 0u;
+        if (hi >= lo) {
+          const uint32_t q = hi - lo < 32u ? kRoulSpans : atomicAdd(&nsp, 1u);
+          if (q < kRoulSpans) spans[q] = make_uint4(lo, hi, i, 0u);
+          else
+            for (uint32_t b = lo; b <= hi; ++b) guide[b] = i;  // short span (or a full queue)
+        }
+      }
+    }
+    __syncthreads();
+    const uint32_t n = nsp < kRoulSpans ? nsp : kRoulSpans;
+    for (uint32_t q = 0; q < n; ++q) {
+      const uint4 sp = spans[q];
+      for (uint32_t b = sp.x + t; b <= sp.y; b += kRoulThreads) guide[b] = sp.z;
+    }
+    __syncthreads();  // (nsp, wsum and xch are reused by the next chunk)
+    carry += ctot;
   }
 }
 
@@ -1485,23 +1683,46 @@ void score_stats_launch(const float* scores, uint64_t S, float* stats, hipStream
 }
 
 size_t roulette_workspace_floats(uint64_t S) {
-  // stats | stats partials | block sums | scale, pad
+  // stats | stats partials | block sums | scale, pad | u64 block sums (integer objectives)
   (void)S;
-  return kRoulScale + 4;
+  return kRoulScale + 4 + 2 * 1024;
 }
 
 void roulette_prefix_launch(const float* scores, uint64_t S, const float* parts, uint32_t nparts, float* cumfit,
-                            float* ws, hipStream_t s) {
+                            float* ws, hipStream_t s, bool integer) {
   // ws layout: [0..4) stats, [4 .. 4+3*1024) stats partials, then block sums, then [kRoulScale] the guide scale
   if (!parts) score_stats_launch(scores, S, ws, s);
   uint32_t grid = launch_grid(S, kBlock * 4);
   if (grid > 1024) grid = 1024;
   const uint64_t per_block = (S + grid - 1) / grid;
   float* block_sums = ws + 4 + 3 * 1024;
-  hipLaunchKernelGGL(prefix_part_kernel, grid, kBlock, 0, s, scores, S, per_block, parts, nparts, ws, block_sums);
-  hipLaunchKernelGGL(prefix_final_kernel, grid, kBlock, 0, s, scores, S, per_block, ws, block_sums, cumfit,
-                     ws + kRoulScale);
+  if (integer) {
+    unsigned long long* sums64 = (unsigned long long*)(ws + kRoulScale + 4);
+    hipLaunchKernelGGL(prefix_part_int_kernel, grid, kBlock, 0, s, scores, S, per_block, parts, nparts, ws, sums64);
+    hipLaunchKernelGGL(prefix_final_int_kernel, grid, kBlock, 0, s, scores, S, per_block, ws,
+                       (const unsigned long long*)sums64, cumfit, ws + kRoulScale);
+  } else {
+    hipLaunchKernelGGL(prefix_part_kernel, grid, kBlock, 0, s, scores, S, per_block, parts, nparts, ws, block_sums);
+    hipLaunchKernelGGL(prefix_final_kernel, grid, kBlock, 0, s, scores, S, per_block, ws, block_sums, cumfit,
+                       ws + kRoulScale);
+  }
   PGA_HIP_CHECK(hipGetLastError());
+}
+
+bool roulette_fused_launch(const float* scores, uint64_t S, const float* parts, const TpPartition& part,
+                           uint32_t max_score, float* cumfit, uint32_t* guide, float* ws, hipStream_t s) {
+  if (!parts || part.grid == 0 || part.unit == 0 || S == 0 || S > 0xFFFFFFFFull) return false;
+  // the largest share (tp_share: ceil(S / grid) in whole units, plus the skew)
+  // times the largest score stays below 2^24, so every f32 partial sum is exact
+  const uint64_t per = ((S + part.grid - 1) / part.grid + part.unit - 1) / part.unit * part.unit;
+  const uint64_t share = per + (uint64_t)part.skew * part.unit;
+  if (share * (uint64_t)max_score >= (1ull << 24)) return false;
+  // a chunk's u32 weight sum: kRoulThreads * kRoulPer * max_score < 2^32
+  if ((uint64_t)kRoulThreads * kRoulPer * max_score >= (1ull << 32)) return false;
+  hipLaunchKernelGGL(roulette_fused_kernel, part.grid, kRoulThreads, 0, s, scores, S, parts, part.unit, part.skew, cumfit,
+                     guide, ws + kRoulScale);
+  PGA_HIP_CHECK(hipGetLastError());
+  return true;
 }
 
 void roulette_guide_launch(const float* cumfit, uint64_t S, uint32_t* guide, float* ws, hipStream_t s) {

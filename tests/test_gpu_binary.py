@@ -92,6 +92,7 @@ def test_knapsack_matrix_cores_bitexact(L, scale, digits):
 @pytest.mark.parametrize("S,L,sel,elitism", [(1048576, 1024, "tournament", 1), (1048576, 1024, "rank", 3),
                                               (1600000, 1024, "tournament", 3), (1600000, 1024, "rank", 1),
                                               (1047576, 1024, "rank", 1),
+                                              (1048576, 1024, "roulette", 1), (700001, 300, "roulette", 2),
                                               (1900000, 256, "tournament", 1), (300000, 64, "roulette", 1),
                                               (200000, 1024, "tournament", 2)])
 def test_headline_geometry_bitexact(S, L, sel, elitism):
