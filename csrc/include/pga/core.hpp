@@ -450,6 +450,10 @@ PGA_HD bool do_crossover(const GenArgs& a, uint32_t w0) { return a.xo_always || 
 // indexed search): any monotone non-decreasing map into [0, B] works, since
 // the pick then scans forward from guide[bucket(target)] to the first
 // cumfit >= target -- the same individual as the binary search.
+// guide entries (S < 2^31): the individual's index, and kGuideCovered when
+// the bucket is not the last one the individual's weight reaches into (its
+// cumfit is then above every target in the bucket: no cumfit load)
+constexpr uint32_t kGuideCovered = 0x80000000u, kGuideIndexMask = 0x7FFFFFFFu;
 PGA_HD uint32_t roulette_bucket(float t, float scale, uint32_t B) {
   const float x = t * scale;
   return x >= (float)B ? B : (x > 0.f ? (uint32_t)x : 0u);

@@ -118,6 +118,16 @@ __device__ __forceinline__ void tp_select_segment(const GenArgs& a, uint32_t beg
       tg[i] = word_to_unit(w) * total;
       ix[i] = total > 0.f ? ld32<uint32_t>(a.roul_guide, roulette_bucket(tg[i], scale, S)) : word_to_index(w, S);
     }
+    // kGuideCovered (S < 2^31): the bucket is not the last of its
+    // individual's buckets, so that individual's cumfit is above every target
+    // in it: the pick is resolved without a cumfit load
+    const bool gflag = S <= kGuideIndexMask;  // wave-uniform
+    bool covered[NS];
+    #pragma unroll
+    for (uint32_t i = 0; i < NS; ++i) {
+      covered[i] = gflag && total > 0.f && (ix[i] & kGuideCovered) != 0u;
+      ix[i] = gflag && total > 0.f ? ix[i] & kGuideIndexMask : ix[i];
+    }
     // the first cumfit load is the aligned 16-byte window holding the guide
     // entry (cumfit is padded by 4 floats): a pick within it is resolved
     // without a dependent load, one past it scans on from the window's end
@@ -125,7 +135,8 @@ __device__ __forceinline__ void tp_select_segment(const GenArgs& a, uint32_t beg
     #pragma unroll
     for (uint32_t i = 0; i < NS; ++i) {
       const uint32_t b = ix[i] & ~3u, off = ix[i] - b;
-      const float4 w = *(const float4*)((const char*)a.cumfit + b * 4u);
+      float4 w = make_float4(tg[i], tg[i], tg[i], tg[i]);  // (covered: no entry below the target)
+      if (!covered[i]) w = *(const float4*)((const char*)a.cumfit + b * 4u);
       // step over the window entries below the target, in order (the padding
       // past cumfit[S - 1] = total is never reached: total >= every target)
       uint32_t p = off;

@@ -409,8 +409,9 @@ __global__ __launch_bounds__(kBlock) void prefix_final_int_kernel(const float* s
 // Spans of 32 buckets or more (one individual holding >= 32/S of the total
 // weight) are queued in LDS and filled by the whole block, so no thread loops
 // over a heavy individual's buckets.
+// cov: kGuideCovered, or 0 (no covered flags: S >= 2^31, or PGA_ROUL_COVER=0)
 __global__ __launch_bounds__(kBlock) void roulette_guide_kernel(const float* c, uint64_t S, const float* meta,
-                                                                 uint32_t* guide) {
+                                                                 uint32_t* guide, uint32_t cov) {
   __shared__ uint4 spans[kBlock];
   __shared__ uint32_t nsp;
   const float scale = meta[0];
@@ -424,7 +425,7 @@ __global__ __launch_bounds__(kBlock) void roulette_guide_kernel(const float* c, 
       const uint32_t lo = i ? roulette_bucket(c[i - 1], scale, B) + 1u : 0u;
       if (hi >= lo) {
         if (hi - lo < 32u) {
-          for (uint32_t b = lo; b <= hi; ++b) guide[b] = (uint32_t)i;
+          for (uint32_t b = lo; b <= hi; ++b) guide[b] = (uint32_t)i | (b < hi ? cov : 0u);
         } else {
           spans[atomicAdd(&nsp, 1u)] = make_uint4(lo, hi, (uint32_t)i, 0u);
         }
@@ -434,7 +435,7 @@ __global__ __launch_bounds__(kBlock) void roulette_guide_kernel(const float* c, 
     const uint32_t n = nsp;
     for (uint32_t k = 0; k < n; ++k) {
       const uint4 sp = spans[k];
-      for (uint32_t b = sp.x + threadIdx.x; b <= sp.y; b += kBlock) guide[b] = sp.z;
+      for (uint32_t b = sp.x + threadIdx.x; b <= sp.y; b += kBlock) guide[b] = sp.z | (b < sp.y ? cov : 0u);
     }
     __syncthreads();
   }
@@ -457,7 +458,8 @@ constexpr uint32_t kRoulThreads = 1024, kRoulPer = 8, kRoulSpans = 1024;
 __global__ __launch_bounds__(kRoulThreads) void roulette_fused_kernel(const float* __restrict__ s, uint64_t S,
                                                                       const float* __restrict__ parts, uint32_t unit,
                                                                       uint32_t skew, float* __restrict__ cumfit,
-                                                                      uint32_t* __restrict__ guide, float* meta) {
+                                                                      uint32_t* __restrict__ guide, float* meta,
+                                                                      uint32_t cov) {
   __shared__ unsigned long long red[kRoulThreads / 64];
   __shared__ float fred[kRoulThreads / 64];
   __shared__ uint32_t wsum[kRoulThreads / 64];
@@ -552,7 +554,7 @@ __global__ __launch_bounds__(kRoulThreads) void roulette_fused_kernel(const floa
           const uint32_t q = hi - lo < 32u ? kRoulSpans : atomicAdd(&nsp, 1u);
           if (q < kRoulSpans) spans[q] = make_uint4(lo, hi, i, 0u);
           else
-            for (uint32_t b = lo; b <= hi; ++b) guide[b] = i;  // short span (or a full queue)
+            for (uint32_t b = lo; b <= hi; ++b) guide[b] = i | (b < hi ? cov : 0u);  // short span (or a full queue)
         }
       }
     }
@@ -560,7 +562,7 @@ __global__ __launch_bounds__(kRoulThreads) void roulette_fused_kernel(const floa
     const uint32_t n = nsp < kRoulSpans ? nsp : kRoulSpans;
     for (uint32_t q = 0; q < n; ++q) {
       const uint4 sp = spans[q];
-      for (uint32_t b = sp.x + t; b <= sp.y; b += kRoulThreads) guide[b] = sp.z;
+      for (uint32_t b = sp.x + t; b <= sp.y; b += kRoulThreads) guide[b] = sp.z | (b < sp.y ? cov : 0u);
     }
     __syncthreads();  // (nsp, wsum and xch are reused by the next chunk)
     carry += ctot;
@@ -1709,6 +1711,16 @@ void roulette_prefix_launch(const float* scores, uint64_t S, const float* parts,
   PGA_HIP_CHECK(hipGetLastError());
 }
 
+// the guide's covered flag (tp.hpp reads it only while S < 2^31);
+// PGA_ROUL_COVER=0 leaves it out (A/B knob)
+static uint32_t guide_cover_flag(uint64_t S) {
+  static const bool off = [] {
+    const char* e = std::getenv("PGA_ROUL_COVER");
+    return e && e[0] == '0';
+  }();
+  return !off && S <= kGuideIndexMask ? kGuideCovered : 0u;
+}
+
 bool roulette_fused_launch(const float* scores, uint64_t S, const float* parts, const TpPartition& part,
                            uint32_t max_score, float* cumfit, uint32_t* guide, float* ws, hipStream_t s) {
   if (!parts || part.grid == 0 || part.unit == 0 || S == 0 || S > 0xFFFFFFFFull) return false;
@@ -1720,14 +1732,15 @@ bool roulette_fused_launch(const float* scores, uint64_t S, const float* parts, 
   // a chunk's u32 weight sum: kRoulThreads * kRoulPer * max_score < 2^32
   if ((uint64_t)kRoulThreads * kRoulPer * max_score >= (1ull << 32)) return false;
   hipLaunchKernelGGL(roulette_fused_kernel, part.grid, kRoulThreads, 0, s, scores, S, parts, part.unit, part.skew, cumfit,
-                     guide, ws + kRoulScale);
+                     guide, ws + kRoulScale, guide_cover_flag(S));
   PGA_HIP_CHECK(hipGetLastError());
   return true;
 }
 
 void roulette_guide_launch(const float* cumfit, uint64_t S, uint32_t* guide, float* ws, hipStream_t s) {
   const uint32_t grid = launch_grid(S, kBlock);
-  hipLaunchKernelGGL(roulette_guide_kernel, grid, kBlock, 0, s, cumfit, S, (const float*)(ws + kRoulScale), guide);
+  hipLaunchKernelGGL(roulette_guide_kernel, grid, kBlock, 0, s, cumfit, S, (const float*)(ws + kRoulScale), guide,
+                     guide_cover_flag(S));
   PGA_HIP_CHECK(hipGetLastError());
 }
 
