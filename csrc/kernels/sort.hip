@@ -397,6 +397,15 @@ __global__ __launch_bounds__(kWideThreads) void radix_scatter_wide_kernel(
     key[r] = keys[e < n ? e : n - 1];  // unconditional load
   }
   if (csums && wid == 0) fold_chunk_sums(csums, nchunks, cpre, lane);  // (nchunks <= kScanFold)
+  // this thread's digits' scanned counts, loaded now: their latency hides
+  // behind the ranking instead of following it
+  constexpr uint32_t P = kWideDigits / kWideThreads;  // digits per thread: [t P, t P + P)
+  uint32_t bval[P];
+#pragma unroll
+  for (uint32_t j = 0; j < P; ++j) {
+    const uint32_t d = t * P + j;
+    bval[j] = base[(uint64_t)(d < D ? d : D - 1) * tiles + blockIdx.x];  // unconditional load
+  }
   const uint64_t below = (1ull << lane) - 1ull;
   uint32_t pos[kWideRounds];
 #pragma unroll
@@ -414,7 +423,6 @@ __global__ __launch_bounds__(kWideThreads) void radix_scatter_wide_kernel(
   }
   __syncthreads();
   // per digit: the waves' counts become waves-before offsets, then local starts
-  constexpr uint32_t P = kWideDigits / kWideThreads;  // digits per thread: [t P, t P + P)
   uint32_t tcs[P], tsum = 0;
 #pragma unroll
   for (uint32_t j = 0; j < P; ++j) {
@@ -449,7 +457,7 @@ __global__ __launch_bounds__(kWideThreads) void radix_scatter_wide_kernel(
       for (uint32_t w = 0; w < kWideWaves; ++w) cnt[w * Dp + d] = (uint16_t)(cnt[w * Dp + d] + ls);
       const uint64_t e = (uint64_t)d * tiles + blockIdx.x;
       const uint32_t pre = csums ? cpre[e / kScanChunk] : 0u;
-      gofs[d] = base[e] + pre - ls;
+      gofs[d] = bval[j] + pre - ls;
     }
     ls += tcs[j];
   }

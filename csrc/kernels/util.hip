@@ -468,6 +468,17 @@ __global__ __launch_bounds__(kRoulThreads) void roulette_fused_kernel(const floa
   __shared__ __align__(16) uint32_t xch[kRoulThreads * kRoulPer];  // a chunk's weights, then its cumfit values
   const uint32_t t = threadIdx.x, lane = lane_id(), wid = t >> 6, np = gridDim.x;
   const uint32_t Su = (uint32_t)S;
+  uint32_t bb, be;
+  tp_share(Su, unit, blockIdx.x, bb, be, skew);
+  // the first chunk's scores, loaded before the partials are reduced (the two
+  // global round trips overlap; a share of up to kRoulThreads * kRoulPer, the
+  // usual case, is this one chunk)
+  float sv0[kRoulPer];
+#pragma unroll
+  for (uint32_t k = 0; k < kRoulPer; ++k) {
+    const uint32_t i = bb + k * kRoulThreads + t;
+    sv0[k] = s[i < be ? i : (be > 0u ? be - 1u : 0u)];  // unconditional load
+  }
   float mn = __builtin_inff();
   for (uint32_t i = t; i < np; i += kRoulThreads) mn = fminf(mn, parts[2 * i]);
 #pragma unroll
@@ -490,8 +501,6 @@ __global__ __launch_bounds__(kRoulThreads) void roulette_fused_kernel(const floa
   const float total = __ull2float_rn(tot);
   const float scale = tot > 0ull ? (float)S / total : 0.f;
   if (blockIdx.x == 0 && t == 0) meta[0] = scale;
-  uint32_t bb, be;
-  tp_share(Su, unit, blockIdx.x, bb, be, skew);
   unsigned long long carry = below;
   for (uint32_t c0 = bb; c0 < be; c0 += kRoulThreads * kRoulPer) {  // block-uniform
     // coalesced loads, transposed through LDS: thread t scans the kRoulPer
@@ -499,7 +508,7 @@ __global__ __launch_bounds__(kRoulThreads) void roulette_fused_kernel(const floa
 #pragma unroll
     for (uint32_t k = 0; k < kRoulPer; ++k) {
       const uint32_t i = c0 + k * kRoulThreads + t;
-      const float v = i < be ? s[i] : mn;
+      const float v = i < be ? (c0 == bb ? sv0[k] : s[i]) : mn;
       xch[k * kRoulThreads + t] = (uint32_t)fmaxf(v - mn, 0.f);
     }
     if (t == 0) nsp = 0;
