@@ -183,7 +183,7 @@ void Island::set_operators(const Config& c) {
     cumfit_ = alloc(4ull * (cfg_.S + 4));  // + 4: the GEN kernels' 16-byte window loads (tp.hpp)
     if (on_gpu()) {
       cum_ws_ = alloc(4ull * roulette_workspace_floats(cfg_.S));
-      roul_guide_ = alloc(4ull * (cfg_.S + 1));
+      roul_guide_ = alloc(8ull * (cfg_.S + 4));  // packed: {guide, cumfit} per entry (roul_packed)
     }
   }
   if (cfg_.selection == SEL_RANK && !rank_order_.ptr) {
@@ -329,6 +329,7 @@ GenArgs Island::make_args(int mode) {
   a.tour_k = cfg_.tour_k;
   a.cumfit = (const float*)cumfit_.ptr;
   a.roul_guide = (const uint32_t*)roul_guide_.ptr;
+  a.roul_packed = roul_guide_.ptr && roul_packed() ? 1u : 0u;
   a.roul_scale = cum_ws_.ptr ? (const float*)cum_ws_.ptr + kRoulScale : nullptr;
   a.rank_order = (const uint32_t*)rank_order_.ptr;
   a.rank_thresh = rank_thresh_of(cfg_.rank_pressure);
@@ -483,12 +484,14 @@ void Island::prepare_generation() {
     const bool one = fused && stats_part_[cur_].grid && integer_objective(cfg_.objective, cfg_.L) &&
                      cfg_.objective != OBJ_KNAPSACK && !roul_fused_off() &&
                      roulette_fused_launch(sc, cfg_.S, (const float*)stats_parts_[cur_].ptr, stats_part_[cur_], cfg_.L,
-                                           (float*)cumfit_.ptr, (uint32_t*)roul_guide_.ptr, (float*)cum_ws_.ptr, stream);
+                                           (float*)cumfit_.ptr, (uint32_t*)roul_guide_.ptr, (float*)cum_ws_.ptr, stream,
+                                           roul_packed());
     if (one) {
     } else if (on_gpu()) {
       roulette_prefix_launch(sc, cfg_.S, fused ? (const float*)stats_parts_[cur_].ptr : nullptr, n_best_[cur_],
                              (float*)cumfit_.ptr, (float*)cum_ws_.ptr, stream, integer_objective(cfg_.objective, cfg_.L));
-      roulette_guide_launch((const float*)cumfit_.ptr, cfg_.S, (uint32_t*)roul_guide_.ptr, (float*)cum_ws_.ptr, stream);
+      roulette_guide_launch((const float*)cumfit_.ptr, cfg_.S, (uint32_t*)roul_guide_.ptr, (float*)cum_ws_.ptr, stream,
+                            roul_packed());
     } else {
       cpu::roulette_prefix(sc, cfg_.S, (float*)cumfit_.ptr);
     }
@@ -989,6 +992,18 @@ void Island::immigrate(uint32_t k, const void* in_rows, const float* in_scores) 
 void Island::set_fused_histogram(bool on) {
   fhist_user_ = on;
   fhist_on_ = on || cfg_.n_elite > 1;
+}
+
+bool Island::roul_packed() const {
+  // PGA_ROUL_PACKED=1: the GEN kernel reads one packed {guide, cumfit} table.
+  // Off by default: measured much slower (167.7 vs 130.1 us/gen, OneMax-1024
+  // roulette; profiles/roulette_r06.md): the guide lookups' lines then hold
+  // 16 buckets instead of 32, and the pick's working set doubles
+  static const bool on = [] {
+    const char* e = std::getenv("PGA_ROUL_PACKED");
+    return e && e[0] == '1';
+  }();
+  return on && cfg_.S < (1ull << 28);
 }
 
 bool Island::roul_fused_off() {

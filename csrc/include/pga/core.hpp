@@ -388,6 +388,10 @@ struct GenArgs {
   // pass then reads nothing.  The launcher sets it only when each block's
   // children are exactly one kRankTile sort tile.
   uint32_t* rank_counts;
+  // roulette, two-phase kernels: roul_guide is the PACKED table, entry e =
+  // {guide[e], cumfit[e] bits} (8 bytes), so a pick's cumfit window usually
+  // sits in the guide line it just fetched (util.hip roulette_*_launch)
+  uint32_t roul_packed;
 };
 // the fused histogram's LDS bins (binary_gen_tp): objectives with more key
 // values use the separate histogram pass

@@ -258,6 +258,7 @@ class Island {
     stats_part_[p] = TpPartition{0, 0, 0};
   }
   static bool roul_fused_off();  // PGA_ROUL_FUSED=0: the three-launch roulette prefix (A/B knob)
+  bool roul_packed() const;      // the GEN kernels read the packed guide table (GenArgs::roul_packed; off)
   bool fused_stats() const;  // the evaluating kernels of this configuration store them
   void append_history();
   Buffer hist_;

@@ -211,7 +211,10 @@ size_t roulette_workspace_floats(uint64_t S);
 // exact prefix rounded once per entry
 void roulette_prefix_launch(const float* scores, uint64_t S, const float* parts, uint32_t nparts, float* cumfit,
                             float* workspace, hipStream_t s, bool integer = false);
-void roulette_guide_launch(const float* cumfit, uint64_t S, uint32_t* guide, float* workspace, hipStream_t s);
+// packed: guide is the packed table of GenArgs::roul_packed (8 bytes per
+// entry, S + 4 entries; S < 2^28)
+void roulette_guide_launch(const float* cumfit, uint64_t S, uint32_t* guide, float* workspace, hipStream_t s,
+                           bool packed = false);
 // Both in ONE launch for an integer objective whose current population came
 // from binary_gen_tp with partition `part`: its {min, sum} partials (parts,
 // part.grid blocks) give every block its carry, so no pass precedes the scan.
@@ -219,7 +222,8 @@ void roulette_guide_launch(const float* cumfit, uint64_t S, uint32_t* guide, flo
 // rounded to f32 once).  max_score: the objective's largest score; returns
 // false (nothing launched) when a partial sum could be inexact in f32.
 bool roulette_fused_launch(const float* scores, uint64_t S, const float* parts, const TpPartition& part,
-                           uint32_t max_score, float* cumfit, uint32_t* guide, float* workspace, hipStream_t s);
+                           uint32_t max_score, float* cumfit, uint32_t* guide, float* workspace, hipStream_t s,
+                           bool packed = false);
 // stable LSD radix sort (sort.hip: reduce-then-scan, digits of up to 8 bits,
 // count / scan / scatter launches per pass): (keys, vals) by the low `bits`
 // bits of the keys, ascending, or descending (all 32 bits; equal keys keep

@@ -110,13 +110,14 @@ __device__ __forceinline__ void tp_select_segment(const GenArgs& a, uint32_t beg
     constexpr uint32_t NS = 2 * kSegBatches;
     const float total = a.cumfit[S - 1];
     const float scale = *a.roul_scale;
+    const uint32_t gsh = a.roul_packed ? 1u : 0u;  // packed: entry e = {guide[e], cumfit[e]}
     uint32_t ix[NS];
     float tg[NS];
     #pragma unroll
     for (uint32_t i = 0; i < NS; ++i) {
       const uint32_t w = __builtin_bit_cast(uint32_t, (i & 1u) ? k1[i >> 1] : k0[i >> 1]);
       tg[i] = word_to_unit(w) * total;
-      ix[i] = total > 0.f ? ld32<uint32_t>(a.roul_guide, roulette_bucket(tg[i], scale, S)) : word_to_index(w, S);
+      ix[i] = total > 0.f ? ld32<uint32_t>(a.roul_guide, roulette_bucket(tg[i], scale, S) << gsh) : word_to_index(w, S);
     }
     // kGuideCovered (S < 2^31): the bucket is not the last of its
     // individual's buckets, so that individual's cumfit is above every target
@@ -136,7 +137,16 @@ __device__ __forceinline__ void tp_select_segment(const GenArgs& a, uint32_t beg
     for (uint32_t i = 0; i < NS; ++i) {
       const uint32_t b = ix[i] & ~3u, off = ix[i] - b;
       float4 w = make_float4(tg[i], tg[i], tg[i], tg[i]);  // (covered: no entry below the target)
-      if (!covered[i]) w = *(const float4*)((const char*)a.cumfit + b * 4u);
+      if (!covered[i]) {
+        if (gsh) {  // entries b .. b + 3: 32 bytes of the packed table
+          const uint4 q0 = *(const uint4*)((const char*)a.roul_guide + b * 8u);
+          const uint4 q1 = *(const uint4*)((const char*)a.roul_guide + b * 8u + 16u);
+          w = make_float4(__builtin_bit_cast(float, q0.y), __builtin_bit_cast(float, q0.w),
+                          __builtin_bit_cast(float, q1.y), __builtin_bit_cast(float, q1.w));
+        } else {
+          w = *(const float4*)((const char*)a.cumfit + b * 4u);
+        }
+      }
       // step over the window entries below the target, in order (the padding
       // past cumfit[S - 1] = total is never reached: total >= every target)
       uint32_t p = off;
@@ -157,7 +167,7 @@ __device__ __forceinline__ void tp_select_segment(const GenArgs& a, uint32_t beg
       for (uint32_t i = 0; i < NS; ++i) {
         const bool adv = total > 0.f && v[i] < tg[i];
         ix[i] += adv ? 1u : 0u;
-        v[i] = ld32<float>(a.cumfit, ix[i]);
+        v[i] = gsh ? ld32<float>(a.roul_guide, (ix[i] << 1) + 1u) : ld32<float>(a.cumfit, ix[i]);
       }
     }
     #pragma unroll

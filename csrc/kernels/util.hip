@@ -410,8 +410,9 @@ __global__ __launch_bounds__(kBlock) void prefix_final_int_kernel(const float* s
 // weight) are queued in LDS and filled by the whole block, so no thread loops
 // over a heavy individual's buckets.
 // cov: kGuideCovered, or 0 (no covered flags: S >= 2^31, or PGA_ROUL_COVER=0)
+// gsh 1: the packed table (GenArgs::roul_packed): guide[b] at word 2 b, cumfit[i] at word 2 i + 1
 __global__ __launch_bounds__(kBlock) void roulette_guide_kernel(const float* c, uint64_t S, const float* meta,
-                                                                 uint32_t* guide, uint32_t cov) {
+                                                                 uint32_t* guide, uint32_t cov, uint32_t gsh) {
   __shared__ uint4 spans[kBlock];
   __shared__ uint32_t nsp;
   const float scale = meta[0];
@@ -421,11 +422,13 @@ __global__ __launch_bounds__(kBlock) void roulette_guide_kernel(const float* c, 
     __syncthreads();
     const uint64_t i = t0 + threadIdx.x;
     if (i < S) {
-      const uint32_t hi = roulette_bucket(c[i], scale, B);
+      const float ci = c[i];
+      if (gsh) guide[2 * i + 1] = __builtin_bit_cast(uint32_t, ci);
+      const uint32_t hi = roulette_bucket(ci, scale, B);
       const uint32_t lo = i ? roulette_bucket(c[i - 1], scale, B) + 1u : 0u;
       if (hi >= lo) {
         if (hi - lo < 32u) {
-          for (uint32_t b = lo; b <= hi; ++b) guide[b] = (uint32_t)i | (b < hi ? cov : 0u);
+          for (uint32_t b = lo; b <= hi; ++b) guide[b << gsh] = (uint32_t)i | (b < hi ? cov : 0u);
         } else {
           spans[atomicAdd(&nsp, 1u)] = make_uint4(lo, hi, (uint32_t)i, 0u);
         }
@@ -435,7 +438,7 @@ __global__ __launch_bounds__(kBlock) void roulette_guide_kernel(const float* c, 
     const uint32_t n = nsp;
     for (uint32_t k = 0; k < n; ++k) {
       const uint4 sp = spans[k];
-      for (uint32_t b = sp.x + threadIdx.x; b <= sp.y; b += kBlock) guide[b] = sp.z | (b < sp.y ? cov : 0u);
+      for (uint32_t b = sp.x + threadIdx.x; b <= sp.y; b += kBlock) guide[b << gsh] = sp.z | (b < sp.y ? cov : 0u);
     }
     __syncthreads();
   }
@@ -459,7 +462,7 @@ __global__ __launch_bounds__(kRoulThreads) void roulette_fused_kernel(const floa
                                                                       const float* __restrict__ parts, uint32_t unit,
                                                                       uint32_t skew, float* __restrict__ cumfit,
                                                                       uint32_t* __restrict__ guide, float* meta,
-                                                                      uint32_t cov) {
+                                                                      uint32_t cov, uint32_t gsh) {
   __shared__ unsigned long long red[kRoulThreads / 64];
   __shared__ float fred[kRoulThreads / 64];
   __shared__ uint32_t wsum[kRoulThreads / 64];
@@ -557,13 +560,14 @@ __global__ __launch_bounds__(kRoulThreads) void roulette_fused_kernel(const floa
         const float ci = __builtin_bit_cast(float, xch[e]);
         const float prev = e ? __builtin_bit_cast(float, xch[e - 1]) : prev0;
         cumfit[i] = ci;
+        if (gsh) guide[2 * i + 1] = __builtin_bit_cast(uint32_t, ci);
         const uint32_t hi = roulette_bucket(ci, scale, Su);
         const uint32_t lo = i ? roulette_bucket(prev, scale, Su) + 1u : 0u;
         if (hi >= lo) {
           const uint32_t q = hi - lo < 32u ? kRoulSpans : atomicAdd(&nsp, 1u);
           if (q < kRoulSpans) spans[q] = make_uint4(lo, hi, i, 0u);
           else
-            for (uint32_t b = lo; b <= hi; ++b) guide[b] = i | (b < hi ? cov : 0u);  // short span (or a full queue)
+            for (uint32_t b = lo; b <= hi; ++b) guide[b << gsh] = i | (b < hi ? cov : 0u);  // short span (or a full queue)
         }
       }
     }
@@ -571,7 +575,7 @@ __global__ __launch_bounds__(kRoulThreads) void roulette_fused_kernel(const floa
     const uint32_t n = nsp < kRoulSpans ? nsp : kRoulSpans;
     for (uint32_t q = 0; q < n; ++q) {
       const uint4 sp = spans[q];
-      for (uint32_t b = sp.x + t; b <= sp.y; b += kRoulThreads) guide[b] = sp.z | (b < sp.y ? cov : 0u);
+      for (uint32_t b = sp.x + t; b <= sp.y; b += kRoulThreads) guide[b << gsh] = sp.z | (b < sp.y ? cov : 0u);
     }
     __syncthreads();  // (nsp, wsum and xch are reused by the next chunk)
     carry += ctot;
@@ -1731,7 +1735,7 @@ static uint32_t guide_cover_flag(uint64_t S) {
 }
 
 bool roulette_fused_launch(const float* scores, uint64_t S, const float* parts, const TpPartition& part,
-                           uint32_t max_score, float* cumfit, uint32_t* guide, float* ws, hipStream_t s) {
+                           uint32_t max_score, float* cumfit, uint32_t* guide, float* ws, hipStream_t s, bool packed) {
   if (!parts || part.grid == 0 || part.unit == 0 || S == 0 || S > 0xFFFFFFFFull) return false;
   // the largest share (tp_share: ceil(S / grid) in whole units, plus the skew)
   // times the largest score stays below 2^24, so every f32 partial sum is exact
@@ -1741,15 +1745,15 @@ bool roulette_fused_launch(const float* scores, uint64_t S, const float* parts, 
   // a chunk's u32 weight sum: kRoulThreads * kRoulPer * max_score < 2^32
   if ((uint64_t)kRoulThreads * kRoulPer * max_score >= (1ull << 32)) return false;
   hipLaunchKernelGGL(roulette_fused_kernel, part.grid, kRoulThreads, 0, s, scores, S, parts, part.unit, part.skew, cumfit,
-                     guide, ws + kRoulScale, guide_cover_flag(S));
+                     guide, ws + kRoulScale, guide_cover_flag(S), packed ? 1u : 0u);
   PGA_HIP_CHECK(hipGetLastError());
   return true;
 }
 
-void roulette_guide_launch(const float* cumfit, uint64_t S, uint32_t* guide, float* ws, hipStream_t s) {
+void roulette_guide_launch(const float* cumfit, uint64_t S, uint32_t* guide, float* ws, hipStream_t s, bool packed) {
   const uint32_t grid = launch_grid(S, kBlock);
   hipLaunchKernelGGL(roulette_guide_kernel, grid, kBlock, 0, s, cumfit, S, (const float*)(ws + kRoulScale), guide,
-                     guide_cover_flag(S));
+                     guide_cover_flag(S), packed ? 1u : 0u);
   PGA_HIP_CHECK(hipGetLastError());
 }
 
